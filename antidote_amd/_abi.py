@@ -1,0 +1,120 @@
+"""ctypes mirror of include/antidote_gpu.h (structs, constants, prototypes).
+
+Shared by the product loader (antidote_amd._lib) and by the test harness,
+which binds the same struct layout to the CPU oracle (oracle/liboracle.so).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+ABI_VERSION = 1
+
+OK = 0
+EINVAL, EHIP, ENOMEM, ECAPACITY, ENOTSUP, ERCCL, ENODEV = -1, -2, -3, -4, -5, -6, -7
+
+COUNTER_PN, SET_AW, REGISTER_MV = 1, 2, 3
+TYPE_MIXED = 0xFF
+EFFECT_INVALID = -(1 << 63)
+TAG_INVALID = 0xFFFFFFFF
+
+F_NEWSS, F_CT_IGNORE, F_ERR_UNEXPECTED, F_ERR_CORRUPTED, F_ERR_CAPACITY = 0x1, 0x2, 0x4, 0x8, 0x10
+UNIQUE_ID_BYTES = 128
+U64_MAX = (1 << 64) - 1
+
+TYPE_NAMES = {
+    COUNTER_PN: "antidote_crdt_counter_pn",
+    SET_AW: "antidote_crdt_set_aw",
+    REGISTER_MV: "antidote_crdt_register_mv",
+}
+TYPE_IDS = {v: k for k, v in TYPE_NAMES.items()}
+
+P = C.c_void_p
+
+
+class AgnLog(C.Structure):
+    _fields_ = [
+        ("crdt_type", C.c_uint32), ("n_dcs", C.c_uint32),
+        ("n_keys", C.c_uint64), ("n_entries", C.c_uint64),
+        ("key_off", P), ("key_type", P), ("oc", P), ("oc_mask", P),
+        ("op_id", P), ("txid", P), ("eff", P),
+        ("tag", P), ("add_tok", P), ("rem_off", P), ("rem_tok", P),
+    ]
+
+
+class AgnRead(C.Structure):
+    _fields_ = [
+        ("n_req", C.c_uint64), ("keys", P), ("R", P), ("R_mask", P),
+        ("sct", P), ("sct_mask", P), ("sct_ignore", P), ("txid", P),
+        ("req_type", C.c_uint32), ("_pad", C.c_uint32),
+        ("base_value", P), ("base_off", P), ("base_tag", P), ("base_tok", P),
+    ]
+
+
+class AgnResult(C.Structure):
+    _fields_ = [
+        ("value", P), ("hole", P), ("lastct", P), ("lastct_mask", P),
+        ("count", P), ("flags", P), ("err_pos", P),
+        ("out_off", P), ("out_n", P), ("out_tag", P), ("out_tok", P),
+    ]
+
+
+class AgnGenCfg(C.Structure):
+    _fields_ = [
+        ("crdt_type", C.c_uint32), ("n_dcs", C.c_uint32), ("n_keys", C.c_uint64),
+        ("ops_per_key", C.c_uint32), ("n_elems", C.c_uint32), ("seed", C.c_uint64),
+        ("key_base", C.c_uint64), ("key_stride", C.c_uint64),
+        ("warm", C.c_uint32), ("_pad", C.c_uint32),
+    ]
+
+
+# Every symbol include/antidote_gpu.h declares, with its ctypes signature.
+PROTOTYPES = {
+    "agn_abi_version": (C.c_int, []),
+    "agn_last_error": (C.c_char_p, []),
+    "agn_strerror": (C.c_char_p, [C.c_int]),
+    "agn_open": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "agn_close": (C.c_int, [P]),
+    "agn_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "agn_dev_alloc": (C.c_int, [P, C.c_size_t, C.POINTER(P)]),
+    "agn_dev_free": (C.c_int, [P, P]),
+    "agn_memcpy_h2d": (C.c_int, [P, P, P, C.c_size_t, P]),
+    "agn_memcpy_d2h": (C.c_int, [P, P, P, C.c_size_t, P]),
+    "agn_memset_d": (C.c_int, [P, P, C.c_int, C.c_size_t, P]),
+    "agn_stream_sync": (C.c_int, [P, P]),
+    "agn_materialize": (C.c_int, [P, C.POINTER(AgnLog), C.POINTER(AgnRead),
+                                  C.POINTER(AgnResult), P]),
+    "agn_materialize_host": (C.c_int, [P, C.POINTER(AgnLog), C.POINTER(AgnRead),
+                                       C.POINTER(AgnResult)]),
+    "agn_state_capacity": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead), P]),
+    "agn_select_base": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, P, P, P, P]),
+    "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
+    "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),
+    "agn_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
+    "agn_comm_unique_id": (C.c_int, [P]),
+    "agn_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
+    "agn_comm_destroy": (C.c_int, [P]),
+    "agn_gst_allreduce": (C.c_int, [P, P, C.c_uint64, P]),
+    "agn_gen_host": (C.c_int, [C.POINTER(AgnGenCfg), C.POINTER(AgnLog), C.POINTER(AgnRead)]),
+    "agn_gen_free_host": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead)]),
+    "agn_gen_dev": (C.c_int, [P, C.POINTER(AgnGenCfg), C.POINTER(AgnLog),
+                              C.POINTER(AgnRead), P]),
+    "agn_gen_free_dev": (C.c_int, [P, C.POINTER(AgnLog), C.POINTER(AgnRead)]),
+}
+
+ORACLE_PROTOTYPES = {
+    "oracle_materialize": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead),
+                                     C.POINTER(AgnResult), C.c_int]),
+    "oracle_gst_min": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, C.c_int]),
+    "oracle_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
+    "oracle_select_base": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, P, P, P]),
+    "oracle_vc_le": (C.c_int, [C.c_uint32, P, P, P, P]),
+    "oracle_vc_all_dots_greater": (C.c_int, [C.c_uint32, P, P, P, P]),
+}
+
+
+def bind(lib, protos):
+    for name, (res, args) in protos.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

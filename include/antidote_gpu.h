@@ -1,0 +1,249 @@
+/*
+ * antidote_gpu.h — C ABI of the MI355X snapshot-materialization engine.
+ *
+ * This is the drop-in boundary for AntidoteDB's materialization hot path.
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the AntidoteDB tree, snapshot 2025-01-12).  The Erlang
+ * side binds these through the thin NIF in nif/antidote_gpu_nif.c (see
+ * INTEGRATION.md); every test in this repository drives them directly.
+ *
+ * Conventions
+ *   - plain C, no torch / HIP types in the signatures (streams are void*);
+ *   - every function returns int: AGN_OK (0) or a negative AGN_E* code, and
+ *     agn_last_error() returns a per-thread message for the last failure;
+ *   - "dev" pointers live in HBM (hipMalloc / agn_dev_alloc / torch), "host"
+ *     pointers in ordinary memory;
+ *   - the library is thread-safe: a context serialises nothing but its own
+ *     RCCL communicator, so many reader threads (the reference's 20 read
+ *     servers per partition, include/antidote.hrl:28) may call
+ *     agn_materialize concurrently on different streams.
+ *
+ * Data model (the SoA "device op log", mirroring the per-key ETS ops tuple of
+ * src/materializer_vnode.erl:621-647 and include/antidote.hrl:81-90):
+ *   - a log holds n_keys keys; key k owns entries [key_off[k], key_off[k+1])
+ *     stored OLDEST -> NEWEST (tuple slot ?FIRST_OP is the oldest op);
+ *   - vector clocks are dense rows of n_dcs u64 words (DC index = column) with
+ *     an optional presence bitmask of W = ceil(n_dcs/64) words per clock; a
+ *     NULL mask means "every DC present" (the dense fast path);
+ *   - oc[e] is the op's OpSSCommit: its snapshot_time with the commit DC's
+ *     entry replaced by the commit time (src/clocksi_materializer.erl:224,
+ *     src/materializer.erl:105) — computed once at ingest;
+ *   - an op whose effect has several parts (set_aw add_all) occupies several
+ *     consecutive entries with the same op_id.
+ */
+#ifndef ANTIDOTE_GPU_H
+#define ANTIDOTE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AGN_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define AGN_OK 0
+#define AGN_EINVAL (-1)     /* malformed argument (enif_make_badarg in the NIF) */
+#define AGN_EHIP (-2)       /* HIP runtime error */
+#define AGN_ENOMEM (-3)     /* device or host allocation failed */
+#define AGN_ECAPACITY (-4)  /* a per-key table exceeded its device capacity */
+#define AGN_ENOTSUP (-5)    /* unsupported configuration */
+#define AGN_ERCCL (-6)      /* RCCL error */
+#define AGN_ENODEV (-7)     /* no GPU / library built without device code */
+
+/* ---- CRDT types (antidote_crdt 0.1.2, rebar.lock:3) --------------------- */
+#define AGN_COUNTER_PN 1   /* antidote_crdt_counter_pn */
+#define AGN_SET_AW 2       /* antidote_crdt_set_aw     */
+#define AGN_REGISTER_MV 3  /* antidote_crdt_register_mv */
+#define AGN_TYPE_MIXED 0xFF /* key_type marker: the key's ops have different types */
+
+/* counter_pn effect that the Erlang side could not encode as an i64: applying
+ * it yields {error,{unexpected_operation,Op,Type}} (src/materializer.erl:53-58) */
+#define AGN_EFFECT_INVALID INT64_MIN
+/* set_aw / register_mv entry whose effect could not be encoded */
+#define AGN_TAG_INVALID 0xFFFFFFFFu
+
+/* ---- per-key result flags --------------------------------------------- */
+#define AGN_F_NEWSS 0x1u          /* IsNewSS: at least one op was included       */
+#define AGN_F_CT_IGNORE 0x2u      /* LastOpCt == ignore (nothing included, SCT ignore) */
+#define AGN_F_ERR_UNEXPECTED 0x4u /* {error,{unexpected_operation,Op,Type}}      */
+#define AGN_F_ERR_CORRUPTED 0x8u  /* erlang:error(corrupted_ops_cache)           */
+#define AGN_F_ERR_CAPACITY 0x10u  /* a per-key device table overflowed            */
+
+/* ---- op log (device or host pointers, same layout) -------------------- */
+typedef struct agn_log {
+    uint32_t crdt_type;       /* AGN_COUNTER_PN / AGN_SET_AW / AGN_REGISTER_MV */
+    uint32_t n_dcs;           /* D: vector-clock width */
+    uint64_t n_keys;
+    uint64_t n_entries;
+    const uint64_t *key_off;  /* [n_keys+1] */
+    const uint8_t *key_type;  /* [n_keys] type of the key's ops or AGN_TYPE_MIXED; NULL: all crdt_type */
+    const uint64_t *oc;       /* [n_entries * D] OpSSCommit */
+    const uint64_t *oc_mask;  /* [n_entries * W] presence, NULL = dense */
+    const uint32_t *op_id;    /* [n_entries] per-key op number (ets update_counter, :630) */
+    const uint64_t *txid;     /* [n_entries] writer txid (0 = none) or NULL */
+    /* AGN_COUNTER_PN */
+    const int64_t *eff;       /* [n_entries] effect = signed increment */
+    /* AGN_SET_AW: entry = {Elem, AddTokens, RemoveTokens};
+     * AGN_REGISTER_MV: entry = {Value, Token, Overridden} or {reset, Overridden} */
+    const uint32_t *tag;      /* [n_entries] elem id (set) / value id (register) */
+    const uint64_t *add_tok;  /* [n_entries] token added (0 = none: remove / reset) */
+    const uint32_t *rem_off;  /* [n_entries+1] CSR into rem_tok */
+    const uint64_t *rem_tok;  /* removed (set) / overridden (register) tokens */
+} agn_log;
+
+/* ---- a batch of reads: one materialize/4 per requested key ------------- */
+typedef struct agn_read {
+    uint64_t n_req;
+    const uint64_t *keys;       /* [n_req] key index into the log, NULL = identity (n_req == n_keys) */
+    const uint64_t *R;          /* [n_req * D] MinSnapshotTime (read snapshot) */
+    const uint64_t *R_mask;     /* [n_req * W] or NULL (dense) */
+    const uint64_t *sct;        /* [n_req * D] SnapshotCommitTime of the base snapshot, NULL = all ignore */
+    const uint64_t *sct_mask;   /* [n_req * W] or NULL */
+    const uint8_t *sct_ignore;  /* [n_req] 1 = ignore (with sct != NULL), NULL = none ignored */
+    const uint64_t *txid;       /* [n_req] reading TxId (0 = ignore) or NULL = all ignore */
+    uint32_t req_type;          /* Type argument of materialize/4 */
+    uint32_t _pad;
+    /* base snapshot value (#materialized_snapshot.value) */
+    const int64_t *base_value;  /* counter: [n_req] or NULL (= 0, Type:new()) */
+    const uint64_t *base_off;   /* set/register: CSR [n_req+1] or NULL (= empty) */
+    const uint32_t *base_tag;   /* set: elem, register: value */
+    const uint64_t *base_tok;   /* token */
+} agn_read;
+
+/* ---- results ----------------------------------------------------------- */
+typedef struct agn_result {
+    int64_t *value;           /* counter: [n_req] materialized value */
+    int64_t *hole;            /* [n_req] NewLastOp (1 - id of the oldest excluded op) */
+    uint64_t *lastct;         /* [n_req * D] LastOpCt */
+    uint64_t *lastct_mask;    /* [n_req * W] or NULL when inputs are dense */
+    uint32_t *count;          /* [n_req] number of effects applied */
+    uint32_t *flags;          /* [n_req] AGN_F_* */
+    uint32_t *err_pos;        /* [n_req] entry index (global) of the failing op, or UINT32_MAX */
+    /* set/register state: pairs written at [out_off[i], out_off[i] + out_n[i]) */
+    const uint64_t *out_off;  /* [n_req+1] capacity CSR (input; see agn_state_capacity) */
+    uint32_t *out_n;          /* [n_req] live pairs */
+    uint32_t *out_tag;        /* elem / value */
+    uint64_t *out_tok;        /* token */
+} agn_result;
+
+/* ---- context ------------------------------------------------------------ */
+typedef struct agn_ctx agn_ctx;
+
+int agn_abi_version(void);
+const char *agn_last_error(void);
+const char *agn_strerror(int code);
+
+/* Open a context on HIP device `device` (riak_core vnode start analogue:
+ * src/materializer_vnode.erl:120-131). */
+int agn_open(int device, agn_ctx **out);
+int agn_close(agn_ctx *ctx);
+int agn_device_count(int *out);
+
+/* Device memory helpers (for callers without their own allocator). */
+int agn_dev_alloc(agn_ctx *ctx, size_t bytes, void **out);
+int agn_dev_free(agn_ctx *ctx, void *ptr);
+int agn_memcpy_h2d(agn_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int agn_memcpy_d2h(agn_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int agn_memset_d(agn_ctx *ctx, void *dst, int value, size_t bytes, void *stream);
+int agn_stream_sync(agn_ctx *ctx, void *stream);
+
+/* Batched clocksi_materializer:materialize/4 (src/clocksi_materializer.erl:82-101)
+ * over a device-resident log: for each requested key, the VC snapshot filter
+ * (materialize_intern/is_op_in_snapshot, :145-268) and the CRDT effect fold
+ * (apply_operations, :111-121 -> antidote_crdt update/2).  All pointers are
+ * device pointers; launched on `stream` (NULL = default stream), asynchronous.
+ * Returns AGN_EINVAL for malformed descriptors. */
+int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req,
+                    agn_result *out, void *stream);
+
+/* Host-pointer convenience: copies log, request and result through a staged
+ * device buffer and blocks.  This is what the NIF calls for a single
+ * materialize/4 whose ops list arrives as an Erlang term. */
+int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req,
+                         agn_result *out);
+
+/* Upper bound of live pairs per request for set/register types:
+ * writes cap_off[n_req+1] (host pointers): cap = #adding entries of the key
+ * + #base pairs.  Host-side helper (the bound is static per log). */
+int agn_state_capacity(const agn_log *host_log, const agn_read *host_req,
+                       uint64_t *cap_off);
+
+/* ---- base-snapshot selection: vector_orddict:get_smaller/2 --------------
+ * (src/vector_orddict.erl:74-87, called from
+ * src/materializer_vnode.erl:400).  cache_off[n_req+1] CSR over cached
+ * snapshot clocks (newest first), clocks [n_cached * D] (+ masks).  For each
+ * request writes the index (within its list) of the first clock <= R, or -1
+ * (= {undefined, _}), and is_first (1 if that index is 0 / list empty). */
+int agn_select_base(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_req,
+                    const uint64_t *cache_off, const uint64_t *clocks,
+                    const uint64_t *clock_mask, const uint64_t *R,
+                    const uint64_t *R_mask, int32_t *out_idx,
+                    uint8_t *out_is_first, void *stream);
+
+/* ---- global stable time ------------------------------------------------
+ * stable_time_functions:get_min_time/1 (src/stable_time_functions.erl:51-85)
+ * over P partition clocks [n_epochs][P][D] (device).  Absent DC entries are
+ * UINT64_MAX; defined[n_epochs*P] = 0 marks an `undefined` partition
+ * (NULL: all defined).  Output out[n_epochs][D+1]: per-DC min (UINT64_MAX =
+ * DC absent from every partition), word D = 1 if every partition was defined
+ * else 0.  agn_gst_finalize applies the "undefined => 0" rule (:78-84). */
+int agn_gst_min(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_parts, uint64_t n_epochs,
+                const uint64_t *clocks, const uint8_t *defined, uint64_t *out,
+                void *stream);
+/* In place on [n_epochs][D+1]: if word D == 0, every present DC becomes 0. */
+int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec,
+                     void *stream);
+
+/* meta_data_sender:update_stable/3 with stable_time_functions:update_func_min/2
+ * (src/meta_data_sender.erl:341-356, src/stable_time_functions.erl:42-48),
+ * host pointers: last[D] is updated in place from new_[D]; UINT64_MAX = absent.
+ * *changed = 1 if any DC was stored. */
+int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *new_,
+                      int *changed);
+
+/* ---- multi-GPU: the one collective -------------------------------------
+ * The meta_data_sender exchange (src/meta_data_sender.erl:230-255: local min,
+ * cast to every node, min again) is one RCCL allreduce(ncclUint64, ncclMin)
+ * over xGMI.  The unique id (128 bytes) is produced by rank 0 and
+ * distributed by the caller (torch.distributed / the Erlang cluster). */
+#define AGN_UNIQUE_ID_BYTES 128
+int agn_comm_unique_id(uint8_t *out_id /* [AGN_UNIQUE_ID_BYTES] */);
+int agn_comm_init(agn_ctx *ctx, int nranks, int rank, const uint8_t *id);
+int agn_comm_destroy(agn_ctx *ctx);
+int agn_gst_allreduce(agn_ctx *ctx, uint64_t *dev_vec, uint64_t n_words, void *stream);
+
+/* ---- synthetic op logs (BASELINE.md §3 / SURVEY.md §8(d) generator) -----
+ * Deterministic SplitMix64 streams, one per key (global key index
+ * key_base + i * key_stride, seed cfg->seed); identical output on host and
+ * device.  Used by bench.py and the parity tests only.  The library owns the
+ * arrays it fills into *log / *req (host: malloc, device: HBM); release them
+ * with the matching agn_gen_free_*.  The request holds one read per key:
+ * R = "random snapshot VC" (max OpSSCommit of a random prefix, jittered),
+ * SCT = ignore (cold) or, with warm = 1, the max OpSSCommit of a shorter
+ * random prefix; base = Type:new(). */
+typedef struct agn_gen_cfg {
+    uint32_t crdt_type;
+    uint32_t n_dcs;
+    uint64_t n_keys;
+    uint32_t ops_per_key;
+    uint32_t n_elems;      /* set_aw elements / register_mv values per key */
+    uint64_t seed;
+    uint64_t key_base;     /* global index of local key 0 */
+    uint64_t key_stride;   /* global key = key_base + i * key_stride (sharding) */
+    uint32_t warm;
+    uint32_t _pad;
+} agn_gen_cfg;
+
+int agn_gen_host(const agn_gen_cfg *cfg, agn_log *log, agn_read *req);
+int agn_gen_free_host(agn_log *log, agn_read *req);
+int agn_gen_dev(agn_ctx *ctx, const agn_gen_cfg *cfg, agn_log *log, agn_read *req,
+                void *stream);
+int agn_gen_free_dev(agn_ctx *ctx, agn_log *log, agn_read *req);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ANTIDOTE_GPU_H */

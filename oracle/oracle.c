@@ -1,0 +1,383 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * A deliberately literal, sequential restatement of the reference Erlang
+ * code, one key at a time, in the reference's own visiting order:
+ *
+ *   materialize/4              src/clocksi_materializer.erl:89-101
+ *   materialize_intern(_perform) src/clocksi_materializer.erl:157-197
+ *   is_op_in_snapshot/7        src/clocksi_materializer.erl:216-268
+ *   belongs_to_snapshot_op/3   src/materializer.erl:101-106
+ *   apply_operations/4         src/clocksi_materializer.erl:113-121
+ *   update_snapshot/3          src/materializer.erl:51-58
+ *   antidote_crdt_*:update/2   (antidote_crdt 0.1.2, restated in SURVEY.md §8(a) a5.1-a5.3)
+ *   get_min_time/1             src/stable_time_functions.erl:51-85
+ *   update_stable/3            src/meta_data_sender.erl:341-356
+ *   get_smaller/2              src/vector_orddict.erl:74-87
+ *
+ * Vector clocks are Erlang dicts in the reference; here a clock is a dense
+ * row of D words plus a presence bitmask (NULL = every DC present).  The
+ * vectorclock 0.1.0 predicates read a missing entry as 0.
+ *
+ * CRDT state for set_aw / register_mv is folded SEQUENTIALLY, effect after
+ * effect, exactly as apply_operations does; the HIP kernels instead resolve
+ * tags order-aware in parallel, and parity proves the two agree.
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define W_OF(d) (((d) + 63u) / 64u)
+
+static inline int present(const uint64_t *mask, uint32_t d) {
+    return mask == NULL || ((mask[d >> 6] >> (d & 63)) & 1u);
+}
+static inline uint64_t get_clock(const uint64_t *v, const uint64_t *m, uint32_t d) {
+    return present(m, d) ? v[d] : 0; /* vectorclock:get_clock_of_dc: missing = 0 */
+}
+
+/* vectorclock:le(A, B): for all d in keys(A) U keys(B): A[d] <= B[d] (missing = 0).
+ * DCs only in B compare 0 <= B[d], always true. */
+int oracle_vc_le(uint32_t D, const uint64_t *a, const uint64_t *am, const uint64_t *b,
+                 const uint64_t *bm) {
+    for (uint32_t d = 0; d < D; ++d)
+        if (present(am, d) && a[d] > get_clock(b, bm, d)) return 0;
+    return 1;
+}
+
+/* vectorclock:all_dots_greater(A, B): for all d in keys(A) U keys(B): A[d] > B[d]. */
+int oracle_vc_all_dots_greater(uint32_t D, const uint64_t *a, const uint64_t *am,
+                               const uint64_t *b, const uint64_t *bm) {
+    for (uint32_t d = 0; d < D; ++d) {
+        if (!present(am, d) && !present(bm, d)) continue;
+        if (!(get_clock(a, am, d) > get_clock(b, bm, d))) return 0;
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* CRDT states for the sequential fold                                       */
+
+typedef struct {
+    uint32_t tag;     /* elem (set_aw) / value (register_mv) */
+    uint64_t tok;
+} pair_t;
+
+typedef struct {
+    pair_t *v;
+    size_t n, cap;
+} pairvec;
+
+static void pv_push(pairvec *p, uint32_t tag, uint64_t tok) {
+    if (p->n == p->cap) {
+        p->cap = p->cap ? p->cap * 2 : 16;
+        p->v = (pair_t *)realloc(p->v, p->cap * sizeof(pair_t));
+    }
+    p->v[p->n].tag = tag;
+    p->v[p->n].tok = tok;
+    p->n++;
+}
+static void pv_insert_at(pairvec *p, size_t at, uint32_t tag, uint64_t tok) {
+    pv_push(p, 0, 0);
+    memmove(p->v + at + 1, p->v + at, (p->n - 1 - at) * sizeof(pair_t));
+    p->v[at].tag = tag;
+    p->v[at].tok = tok;
+}
+
+static int tok_in(const uint64_t *list, uint32_t n, uint64_t t) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (list[i] == t) return 1;
+    return 0;
+}
+
+/* antidote_crdt_set_aw:update/2 for one effect entry {Elem, AddTokens, RemoveTokens}.
+ * The state is the orddict [{Elem, [Token]}] flattened to pairs grouped by
+ * elem (elems ascending, tokens in list order).  Per elem:
+ * Tokens := (Tokens -- Remove) ++ Add; the elem disappears when empty. */
+static void set_aw_apply(pairvec *st, uint32_t elem, uint64_t add_tok,
+                         const uint64_t *rem, uint32_t n_rem) {
+    size_t w = 0, insert_at = (size_t)-1;
+    for (size_t r = 0; r < st->n; ++r) {
+        pair_t p = st->v[r];
+        if (p.tag == elem && tok_in(rem, n_rem, p.tok)) continue; /* Tokens -- Remove */
+        st->v[w++] = p;
+    }
+    st->n = w;
+    if (add_tok == 0) return;
+    /* ++ Add: append after the elem's surviving tokens (or create the elem
+     * at its sorted position). */
+    for (size_t r = 0; r < st->n; ++r) {
+        if (st->v[r].tag == elem) insert_at = r + 1;
+        else if (st->v[r].tag > elem && insert_at == (size_t)-1) { insert_at = r; break; }
+        else if (st->v[r].tag > elem) break;
+    }
+    if (insert_at == (size_t)-1) insert_at = st->n;
+    pv_insert_at(st, insert_at, elem, add_tok);
+}
+
+/* antidote_crdt_register_mv:update/2: {Value, Token, Overridden} drops the
+ * overridden tokens then insert_sorted({Value, Token}); {reset, Overridden}
+ * only drops.  The list stays sorted by (value, token). */
+static void register_mv_apply(pairvec *st, uint32_t value, uint64_t add_tok,
+                              const uint64_t *ovr, uint32_t n_ovr) {
+    size_t w = 0;
+    for (size_t r = 0; r < st->n; ++r) {
+        pair_t p = st->v[r];
+        if (tok_in(ovr, n_ovr, p.tok)) continue;
+        st->v[w++] = p;
+    }
+    st->n = w;
+    if (add_tok == 0) return; /* reset */
+    size_t at = 0;
+    while (at < st->n && (st->v[at].tag < value ||
+                          (st->v[at].tag == value && st->v[at].tok < add_tok)))
+        ++at;
+    pv_insert_at(st, at, value, add_tok);
+}
+
+/* ------------------------------------------------------------------------ */
+
+static void materialize_one(const agn_log *log, const agn_read *req, agn_result *out,
+                            uint64_t i, uint32_t *incl_buf) {
+    const uint32_t D = log->n_dcs, W = W_OF(D);
+    const uint64_t key = req->keys ? req->keys[i] : i;
+    const uint64_t off = log->key_off[key], n = log->key_off[key + 1] - off;
+    const uint64_t *R = req->R + i * D;
+    const uint64_t *Rm = req->R_mask ? req->R_mask + i * W : NULL;
+    int sct_ign = (req->sct == NULL) || (req->sct_ignore && req->sct_ignore[i]);
+    const uint64_t *sct = sct_ign ? NULL : req->sct + i * D;
+    const uint64_t *sctm = (sct_ign || !req->sct_mask) ? NULL : req->sct_mask + i * W;
+    const uint64_t txid = req->txid ? req->txid[i] : 0;
+    uint32_t flags = 0;
+
+    /* materialize_intern_perform raises erlang:error(corrupted_ops_cache) on
+     * the first visited op whose type differs (:174,190-191).  All ops are
+     * visited, so this is "any op of the key has another type". */
+    if (n > 0) {
+        uint8_t kt = log->key_type ? log->key_type[key] : (uint8_t)log->crdt_type;
+        if (kt != (uint8_t)req->req_type) {
+            out->flags[i] = AGN_F_ERR_CORRUPTED;
+            out->err_pos[i] = UINT32_MAX;
+            return;
+        }
+    }
+
+    /* LastOpCt starts as SnapshotCommitTime (materialize/4 passes it twice, :94-95). */
+    uint64_t ct[256], ctm[4];
+    int ct_ignore = sct_ign;
+    if (!ct_ignore) {
+        for (uint32_t d = 0; d < D; ++d) ct[d] = sct[d];
+        for (uint32_t w = 0; w < W; ++w) ctm[w] = sctm ? sctm[w] : ~0ull;
+    }
+    /* FirstHole = get_first_id(Ops): id of the newest op, 0 if none (:49-63). */
+    int64_t hole = n ? (int64_t)log->op_id[off + n - 1] : 0;
+    int new_ss = 0;
+    uint64_t n_incl = 0;
+
+    /* newest -> oldest (tuple form: element(?FIRST_OP+Length-1-Location), :163-171) */
+    for (uint64_t pos = n; pos-- > 0;) {
+        const uint64_t e = off + pos;
+        const uint64_t *oc = log->oc + e * D;
+        const uint64_t *ocm = log->oc_mask ? log->oc_mask + e * W : NULL;
+        /* belongs_to_snapshot_op(LastSnapshot, ...) or (TxId == op.txid)  (:219-220) */
+        int not_in_prev = sct_ign ? 1 : !oracle_vc_le(D, oc, ocm, sct, sctm);
+        if (txid != 0 && log->txid && log->txid[e] == txid) not_in_prev = 1;
+        if (!not_in_prev) continue; /* {false, true, _}: already in the base snapshot */
+        /* dict:fold over OpSSCommit (:235-258): every DC of the op must be in
+         * the read snapshot with TimeSS >= TimeOp. */
+        int result = 1;
+        for (uint32_t d = 0; d < D; ++d) {
+            if (!present(ocm, d)) continue;
+            if (!present(Rm, d)) { result = 0; continue; } /* logger:error, false (:245-247) */
+            if (R[d] < oc[d]) result = 0;
+        }
+        if (result) {
+            /* NewTime: PrevTime2 (= OpSSCommit when PrevTime is ignore) with
+             * every DC of the op max-merged in (dict:update, :249-256). */
+            if (ct_ignore) {
+                for (uint32_t d = 0; d < D; ++d) ct[d] = present(ocm, d) ? oc[d] : 0;
+                for (uint32_t w = 0; w < W; ++w) ctm[w] = ocm ? ocm[w] : ~0ull;
+                ct_ignore = 0;
+            } else {
+                for (uint32_t d = 0; d < D; ++d) {
+                    if (!present(ocm, d)) continue;
+                    int had = (ctm[d >> 6] >> (d & 63)) & 1u;
+                    if (!had) { ct[d] = oc[d]; ctm[d >> 6] |= 1ull << (d & 63); }
+                    else if (oc[d] > ct[d]) ct[d] = oc[d];
+                }
+            }
+            new_ss = 1;
+            incl_buf[n_incl++] = (uint32_t)pos; /* [Op | OpList]: ends oldest-first */
+        } else {
+            hole = (int64_t)log->op_id[e] - 1; /* {ok, OpList, LastOpCt, NewSS, OpId-1} */
+        }
+    }
+
+    /* apply_operations over OpList, oldest first (:113-121). */
+    uint32_t count = 0;
+    uint32_t err = UINT32_MAX;
+    if (log->crdt_type == AGN_COUNTER_PN) {
+        int64_t v = req->base_value ? req->base_value[i] : 0;
+        for (uint64_t j = n_incl; j-- > 0;) {
+            const uint64_t e = off + incl_buf[j];
+            if (log->eff[e] == AGN_EFFECT_INVALID) { err = (uint32_t)e; break; }
+            v = (int64_t)((uint64_t)v + (uint64_t)log->eff[e]); /* S + E */
+            ++count;
+        }
+        if (out->value) out->value[i] = v;
+    } else {
+        pairvec st = {0};
+        if (req->base_off)
+            for (uint64_t b = req->base_off[i]; b < req->base_off[i + 1]; ++b)
+                pv_push(&st, req->base_tag[b], req->base_tok[b]);
+        for (uint64_t j = n_incl; j-- > 0;) {
+            const uint64_t e = off + incl_buf[j];
+            const uint32_t *ro = log->rem_off;
+            if (log->tag[e] == AGN_TAG_INVALID) { err = (uint32_t)e; break; }
+            if (log->crdt_type == AGN_SET_AW)
+                set_aw_apply(&st, log->tag[e], log->add_tok[e], log->rem_tok + ro[e],
+                             ro[e + 1] - ro[e]);
+            else
+                register_mv_apply(&st, log->tag[e], log->add_tok[e], log->rem_tok + ro[e],
+                                  ro[e + 1] - ro[e]);
+            /* one Op may span several entries (same op_id): count it once */
+            if (incl_buf[j] == 0 || log->op_id[e - 1] != log->op_id[e]) ++count;
+        }
+        if (err == UINT32_MAX) {
+            uint64_t o = out->out_off[i], cap = out->out_off[i + 1] - o;
+            if (st.n > cap) {
+                flags |= AGN_F_ERR_CAPACITY;
+            } else {
+                for (size_t r = 0; r < st.n; ++r) {
+                    out->out_tag[o + r] = st.v[r].tag;
+                    out->out_tok[o + r] = st.v[r].tok;
+                }
+            }
+            out->out_n[i] = (uint32_t)st.n;
+        }
+        free(st.v);
+    }
+
+    if (err != UINT32_MAX) flags |= AGN_F_ERR_UNEXPECTED;
+    if (new_ss) flags |= AGN_F_NEWSS;
+    if (ct_ignore) flags |= AGN_F_CT_IGNORE;
+    out->flags[i] = flags;
+    out->err_pos[i] = err;
+    out->count[i] = count;
+    out->hole[i] = hole;
+    uint64_t *oct = out->lastct + i * D;
+    for (uint32_t d = 0; d < D; ++d)
+        oct[d] = ct_ignore ? 0 : (((ctm[d >> 6] >> (d & 63)) & 1u) ? ct[d] : 0);
+    if (out->lastct_mask) {
+        uint64_t *om = out->lastct_mask + i * W;
+        for (uint32_t w = 0; w < W; ++w) om[w] = ct_ignore ? 0 : ctm[w];
+    }
+}
+
+typedef struct {
+    const agn_log *log;
+    const agn_read *req;
+    agn_result *out;
+    uint64_t lo, hi;
+    uint64_t max_n;
+} job_t;
+
+static void *run_job(void *arg) {
+    job_t *j = (job_t *)arg;
+    uint32_t *buf = (uint32_t *)malloc((j->max_n + 1) * sizeof(uint32_t));
+    for (uint64_t i = j->lo; i < j->hi; ++i) materialize_one(j->log, j->req, j->out, i, buf);
+    free(buf);
+    return NULL;
+}
+
+int oracle_materialize(const agn_log *log, const agn_read *req, agn_result *out,
+                       int n_threads) {
+    if (!log || !req || !out || log->n_dcs == 0 || log->n_dcs > 256) return AGN_EINVAL;
+    if (!req->keys && req->n_req != log->n_keys) return AGN_EINVAL;
+    uint64_t max_n = 0;
+    for (uint64_t k = 0; k < log->n_keys; ++k) {
+        uint64_t n = log->key_off[k + 1] - log->key_off[k];
+        if (n > max_n) max_n = n;
+    }
+    if (n_threads < 1) n_threads = 1;
+    if ((uint64_t)n_threads > req->n_req) n_threads = req->n_req ? (int)req->n_req : 1;
+    job_t *jobs = (job_t *)calloc((size_t)n_threads, sizeof(job_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    uint64_t per = (req->n_req + n_threads - 1) / n_threads;
+    for (int t = 0; t < n_threads; ++t) {
+        jobs[t].log = log;
+        jobs[t].req = req;
+        jobs[t].out = out;
+        jobs[t].lo = per * t < req->n_req ? per * t : req->n_req;
+        jobs[t].hi = per * (t + 1) < req->n_req ? per * (t + 1) : req->n_req;
+        jobs[t].max_n = max_n;
+        if (n_threads == 1) run_job(&jobs[t]);
+        else pthread_create(&th[t], NULL, run_job, &jobs[t]);
+    }
+    if (n_threads > 1)
+        for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
+    free(jobs);
+    free(th);
+    return AGN_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* get_min_time/1 (src/stable_time_functions.erl:51-85): per DC, the min over
+ * the partitions whose dict contains it; an `undefined` partition makes
+ * every output DC 0.  Absent = UINT64_MAX, output word D = "all defined". */
+int oracle_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
+                   const uint8_t *defined, uint64_t *out, int finalize) {
+    for (uint64_t e = 0; e < E; ++e) {
+        uint64_t *o = out + e * (D + 1);
+        for (uint32_t d = 0; d < D; ++d) o[d] = UINT64_MAX;
+        o[D] = 1;
+        for (uint64_t p = 0; p < P; ++p) {
+            if (defined && !defined[e * P + p]) { o[D] = 0; continue; }
+            const uint64_t *c = clocks + (e * P + p) * D;
+            for (uint32_t d = 0; d < D; ++d)
+                if (c[d] < o[d]) o[d] = c[d]; /* PrevTime >= Time -> store Time */
+        }
+        if (finalize && o[D] == 0)
+            for (uint32_t d = 0; d < D; ++d)
+                if (o[d] != UINT64_MAX) o[d] = 0; /* FoundUndefined (:78-82) */
+    }
+    return AGN_OK;
+}
+
+/* update_stable/3 with update_func_min/2: store Time iff Last is undefined
+ * or Time >= Last; DCs absent from NewDict keep their last value. */
+int oracle_update_stable(uint32_t D, uint64_t *last, const uint64_t *nw, int *changed) {
+    int c = 0;
+    for (uint32_t d = 0; d < D; ++d) {
+        if (nw[d] == UINT64_MAX) continue;
+        if (last[d] == UINT64_MAX || nw[d] >= last[d]) { last[d] = nw[d]; c = 1; }
+    }
+    if (changed) *changed = c;
+    return AGN_OK;
+}
+
+/* get_smaller/2: first (newest) entry whose clock is le the read clock;
+ * IsFirst is true until the walk moves past the head (:78-87). */
+int oracle_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,
+                       const uint64_t *clocks, const uint64_t *clock_mask,
+                       const uint64_t *R, const uint64_t *R_mask, int32_t *out_idx,
+                       uint8_t *out_is_first) {
+    const uint32_t W = W_OF(D);
+    for (uint64_t i = 0; i < n_req; ++i) {
+        int32_t idx = -1;
+        uint8_t first = 1;
+        for (uint64_t c = cache_off[i]; c < cache_off[i + 1]; ++c) {
+            if (oracle_vc_le(D, clocks + c * D, clock_mask ? clock_mask + c * W : NULL,
+                             R + i * D, R_mask ? R_mask + i * W : NULL)) {
+                idx = (int32_t)(c - cache_off[i]);
+                break;
+            }
+            first = 0;
+        }
+        out_idx[i] = idx;
+        out_is_first[i] = first;
+    }
+    return AGN_OK;
+}

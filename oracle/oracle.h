@@ -1,0 +1,52 @@
+/*
+ * oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of AntidoteDB's materialization path, used as the parity
+ * checker for the HIP engine.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product library never links
+ * it (antidote_amd fails loudly instead of falling back to it).
+ *
+ * Parity is pinned against the reference's own EUnit known answers,
+ * transcribed to tests/golden/kats.json (see tests/test_oracle_kats.py).
+ * set_aw / register_mv concurrency semantics are only partially pinned
+ * (antidote_crdt 0.1.2 is not vendored in the reference).
+ */
+#ifndef AGN_ORACLE_H
+#define AGN_ORACLE_H
+
+#include "../include/antidote_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* clocksi_materializer:materialize/4 for every request (host pointers). */
+int oracle_materialize(const agn_log *log, const agn_read *req, agn_result *out,
+                       int n_threads);
+
+/* stable_time_functions:get_min_time/1 over [n_epochs][P][D] -> [n_epochs][D+1]
+ * (same encoding as agn_gst_min), followed by the finalize rule. */
+int oracle_gst_min(uint32_t n_dcs, uint64_t n_parts, uint64_t n_epochs,
+                   const uint64_t *clocks, const uint8_t *defined, uint64_t *out,
+                   int finalize);
+
+/* meta_data_sender:update_stable/3 */
+int oracle_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *new_,
+                         int *changed);
+
+/* vector_orddict:get_smaller/2 */
+int oracle_select_base(uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off,
+                       const uint64_t *clocks, const uint64_t *clock_mask,
+                       const uint64_t *R, const uint64_t *R_mask,
+                       int32_t *out_idx, uint8_t *out_is_first);
+
+/* vectorclock 0.1.0 predicates on single clocks (missing entry = 0). */
+int oracle_vc_le(uint32_t n_dcs, const uint64_t *a, const uint64_t *am,
+                 const uint64_t *b, const uint64_t *bm);
+int oracle_vc_all_dots_greater(uint32_t n_dcs, const uint64_t *a, const uint64_t *am,
+                               const uint64_t *b, const uint64_t *bm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
