@@ -1,0 +1,666 @@
+// api.hip — the C ABI of include/antidote_gpu.h: context, descriptor
+// validation, host-staged materialize (the per-key NIF entry), the GST
+// collective over RCCL, and the synthetic op-log generator.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+#include "gen.hpp"
+
+struct agn_ctx {
+    int device = 0;
+    std::mutex comm_mu;
+    ncclComm_t comm = nullptr;
+};
+
+namespace agn {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+static int use_device(agn_ctx *ctx) {
+    if (!ctx) return fail(AGN_EINVAL, "null context");
+    AGN_HIP(hipSetDevice(ctx->device));
+    return AGN_OK;
+}
+
+static bool is_tag_type(uint32_t t) { return t == AGN_SET_AW || t == AGN_REGISTER_MV; }
+
+static int validate(const agn_log *log, const agn_read *req, const agn_result *out) {
+    if (!log || !req || !out) return fail(AGN_EINVAL, "null descriptor");
+    if (log->n_dcs == 0 || log->n_dcs > 256) return fail(AGN_EINVAL, "n_dcs=%u not in [1,256]", log->n_dcs);
+    if (log->crdt_type != AGN_COUNTER_PN && !is_tag_type(log->crdt_type))
+        return fail(AGN_EINVAL, "unknown crdt_type %u", log->crdt_type);
+    if (req->n_req == 0) return AGN_OK;
+    if (!log->key_off || !log->op_id) return fail(AGN_EINVAL, "log: key_off/op_id required");
+    if (log->n_entries && !log->oc) return fail(AGN_EINVAL, "log: oc required");
+    if (!req->keys && req->n_req != log->n_keys)
+        return fail(AGN_EINVAL, "identity key map needs n_req == n_keys");
+    if (!req->R) return fail(AGN_EINVAL, "read: R required");
+    if (!out->hole || !out->lastct || !out->count || !out->flags || !out->err_pos)
+        return fail(AGN_EINVAL, "result: hole/lastct/count/flags/err_pos required");
+    if (log->crdt_type == AGN_COUNTER_PN) {
+        if (log->n_entries && !log->eff) return fail(AGN_EINVAL, "counter_pn log needs eff");
+        if (!out->value) return fail(AGN_EINVAL, "counter_pn result needs value");
+    } else {
+        if (log->n_entries && (!log->tag || !log->add_tok || !log->rem_off))
+            return fail(AGN_EINVAL, "set/register log needs tag/add_tok/rem_off");
+        if (!out->out_off || !out->out_n || !out->out_tag || !out->out_tok)
+            return fail(AGN_EINVAL, "set/register result needs out_off/out_n/out_tag/out_tok");
+        if (req->base_off && (!req->base_tag || !req->base_tok))
+            return fail(AGN_EINVAL, "base state needs base_tag/base_tok");
+    }
+    return AGN_OK;
+}
+
+}  // namespace agn
+
+using namespace agn;
+
+extern "C" {
+
+int agn_abi_version(void) { return AGN_ABI_VERSION; }
+
+const char *agn_last_error(void) { return g_err; }
+
+const char *agn_strerror(int code) {
+    switch (code) {
+        case AGN_OK: return "ok";
+        case AGN_EINVAL: return "invalid argument";
+        case AGN_EHIP: return "HIP runtime error";
+        case AGN_ENOMEM: return "out of memory";
+        case AGN_ECAPACITY: return "device table capacity exceeded";
+        case AGN_ENOTSUP: return "not supported";
+        case AGN_ERCCL: return "RCCL error";
+        case AGN_ENODEV: return "no device";
+        default: return "unknown error";
+    }
+}
+
+int agn_device_count(int *out) {
+    if (!out) return fail(AGN_EINVAL, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return AGN_OK;
+}
+
+int agn_open(int device, agn_ctx **out) {
+    if (!out) return fail(AGN_EINVAL, "null out");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(AGN_ENODEV, "no HIP device");
+    if (device < 0 || device >= n) return fail(AGN_EINVAL, "device %d of %d", device, n);
+    AGN_HIP(hipSetDevice(device));
+    hipDeviceProp_t p;
+    AGN_HIP(hipGetDeviceProperties(&p, device));
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+        return fail(AGN_ENOTSUP, "built for gfx950, device is %s", p.gcnArchName);
+    agn_ctx *c = new (std::nothrow) agn_ctx;
+    if (!c) return fail(AGN_ENOMEM, "ctx");
+    c->device = device;
+    *out = c;
+    return AGN_OK;
+}
+
+int agn_close(agn_ctx *ctx) {
+    if (!ctx) return AGN_OK;
+    agn_comm_destroy(ctx);
+    delete ctx;
+    return AGN_OK;
+}
+
+int agn_dev_alloc(agn_ctx *ctx, size_t bytes, void **out) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (!out) return fail(AGN_EINVAL, "null out");
+    *out = nullptr;
+    if (bytes == 0) return AGN_OK;
+    if (hipMalloc(out, bytes) != hipSuccess) return fail(AGN_ENOMEM, "hipMalloc(%zu)", bytes);
+    return AGN_OK;
+}
+
+int agn_dev_free(agn_ctx *ctx, void *ptr) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (ptr) AGN_HIP(hipFree(ptr));
+    return AGN_OK;
+}
+
+int agn_memcpy_h2d(agn_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (bytes) AGN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return AGN_OK;
+}
+
+int agn_memcpy_d2h(agn_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (bytes) AGN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return AGN_OK;
+}
+
+int agn_memset_d(agn_ctx *ctx, void *dst, int value, size_t bytes, void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (bytes) AGN_HIP(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));
+    return AGN_OK;
+}
+
+int agn_stream_sync(agn_ctx *ctx, void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    AGN_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return AGN_OK;
+}
+
+int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out,
+                    void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    rc = validate(log, req, out);
+    if (rc) return rc;
+    if (req->n_req == 0) return AGN_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (log->crdt_type == AGN_COUNTER_PN) return launch_counter(*log, *req, *out, s);
+    return launch_tags(*log, *req, *out, s);
+}
+
+int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_off) {
+    if (!log || !req || !cap_off) return fail(AGN_EINVAL, "null argument");
+    cap_off[0] = 0;
+    for (uint64_t i = 0; i < req->n_req; ++i) {
+        const uint64_t k = req->keys ? req->keys[i] : i;
+        uint64_t c = 0;
+        if (log->add_tok)
+            for (uint64_t e = log->key_off[k]; e < log->key_off[k + 1]; ++e) c += log->add_tok[e] != 0;
+        if (req->base_off) c += req->base_off[i + 1] - req->base_off[i];
+        cap_off[i + 1] = cap_off[i] + c;
+    }
+    return AGN_OK;
+}
+
+}  // extern "C"
+
+// ---- host-staged materialize --------------------------------------------------
+namespace {
+struct Staging {
+    std::vector<void *> bufs;
+    int err = AGN_OK;
+    template <class T>
+    T *up(const T *h, size_t n) {
+        if (!h || n == 0 || err) return nullptr;
+        void *d = nullptr;
+        if (hipMalloc(&d, n * sizeof(T)) != hipSuccess) { err = fail(AGN_ENOMEM, "staging"); return nullptr; }
+        bufs.push_back(d);
+        if (hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) {
+            err = fail(AGN_EHIP, "staging copy");
+            return nullptr;
+        }
+        return (T *)d;
+    }
+    template <class T>
+    T *alloc(const T *h, size_t n) {
+        if (!h || n == 0 || err) return nullptr;
+        void *d = nullptr;
+        if (hipMalloc(&d, n * sizeof(T)) != hipSuccess) { err = fail(AGN_ENOMEM, "staging"); return nullptr; }
+        bufs.push_back(d);
+        return (T *)d;
+    }
+    template <class T>
+    void down(T *h, const T *d, size_t n) {
+        if (!h || !d || n == 0 || err) return;
+        if (hipMemcpy(h, d, n * sizeof(T), hipMemcpyDeviceToHost) != hipSuccess)
+            err = fail(AGN_EHIP, "staging copy back");
+    }
+    ~Staging() {
+        for (void *p : bufs) (void)hipFree(p);
+    }
+};
+}  // namespace
+
+extern "C" {
+
+int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    rc = validate(log, req, out);
+    if (rc) return rc;
+    if (req->n_req == 0) return AGN_OK;
+    const uint32_t D = log->n_dcs, W = n_words(D);
+    const uint64_t E = log->n_entries, K = log->n_keys, Q = req->n_req;
+    Staging st;
+    agn_log dl = *log;
+    dl.key_off = st.up(log->key_off, K + 1);
+    dl.key_type = st.up(log->key_type, K);
+    dl.oc = st.up(log->oc, E * D);
+    dl.oc_mask = st.up(log->oc_mask, E * W);
+    dl.op_id = st.up(log->op_id, E);
+    dl.txid = st.up(log->txid, E);
+    dl.eff = st.up(log->eff, E);
+    dl.tag = st.up(log->tag, E);
+    dl.add_tok = st.up(log->add_tok, E);
+    dl.rem_off = st.up(log->rem_off, log->rem_off ? E + 1 : 0);
+    const uint64_t n_rem = log->rem_off ? log->rem_off[E] : 0;
+    dl.rem_tok = st.up(log->rem_tok, n_rem);
+    agn_read dr = *req;
+    dr.keys = st.up(req->keys, Q);
+    dr.R = st.up(req->R, Q * D);
+    dr.R_mask = st.up(req->R_mask, Q * W);
+    dr.sct = st.up(req->sct, Q * D);
+    dr.sct_mask = st.up(req->sct_mask, Q * W);
+    dr.sct_ignore = st.up(req->sct_ignore, Q);
+    dr.txid = st.up(req->txid, Q);
+    dr.base_value = st.up(req->base_value, Q);
+    dr.base_off = st.up(req->base_off, req->base_off ? Q + 1 : 0);
+    const uint64_t n_base = req->base_off ? req->base_off[Q] : 0;
+    dr.base_tag = st.up(req->base_tag, n_base);
+    dr.base_tok = st.up(req->base_tok, n_base);
+    agn_result dout = *out;
+    dout.value = st.alloc(out->value, Q);
+    dout.hole = st.alloc(out->hole, Q);
+    dout.lastct = st.alloc(out->lastct, Q * D);
+    dout.lastct_mask = st.alloc(out->lastct_mask, Q * W);
+    dout.count = st.alloc(out->count, Q);
+    dout.flags = st.alloc(out->flags, Q);
+    dout.err_pos = st.alloc(out->err_pos, Q);
+    const uint64_t n_out = out->out_off ? out->out_off[Q] : 0;
+    dout.out_off = st.up(out->out_off, out->out_off ? Q + 1 : 0);
+    dout.out_n = st.alloc(out->out_n, Q);
+    dout.out_tag = st.alloc(out->out_tag, n_out ? n_out : 1);
+    dout.out_tok = st.alloc(out->out_tok, n_out ? n_out : 1);
+    if (st.err) return st.err;
+    rc = agn_materialize(ctx, &dl, &dr, &dout, nullptr);
+    if (rc) return rc;
+    AGN_HIP(hipDeviceSynchronize());
+    st.down(out->value, dout.value, Q);
+    st.down(out->hole, dout.hole, Q);
+    st.down(out->lastct, dout.lastct, Q * D);
+    st.down(out->lastct_mask, dout.lastct_mask, Q * W);
+    st.down(out->count, dout.count, Q);
+    st.down(out->flags, dout.flags, Q);
+    st.down(out->err_pos, dout.err_pos, Q);
+    st.down(out->out_n, dout.out_n, Q);
+    st.down(out->out_tag, dout.out_tag, n_out);
+    st.down(out->out_tok, dout.out_tok, n_out);
+    return st.err;
+}
+
+// ---- base selection / GST ---------------------------------------------------------
+int agn_select_base(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off,
+                    const uint64_t *clocks, const uint64_t *clock_mask, const uint64_t *R,
+                    const uint64_t *R_mask, int32_t *out_idx, uint8_t *out_is_first,
+                    void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (n_dcs == 0 || !cache_off || !R || !out_idx || !out_is_first)
+        return fail(AGN_EINVAL, "select_base: bad arguments");
+    return launch_select_base(n_dcs, n_req, cache_off, clocks, clock_mask, R, R_mask, out_idx,
+                              out_is_first, (hipStream_t)stream);
+}
+
+int agn_gst_min(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_parts, uint64_t n_epochs,
+                const uint64_t *clocks, const uint8_t *defined, uint64_t *out, void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (!out || (n_parts && n_epochs && !clocks)) return fail(AGN_EINVAL, "gst: null buffer");
+    return launch_gst_min(n_dcs, n_parts, n_epochs, clocks, defined, out, (hipStream_t)stream);
+}
+
+int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec,
+                     void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (!vec) return fail(AGN_EINVAL, "gst: null buffer");
+    return launch_gst_finalize(n_dcs, n_epochs, vec, (hipStream_t)stream);
+}
+
+int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *nw, int *changed) {
+    if (!last || !nw) return fail(AGN_EINVAL, "null clock");
+    int c = 0;
+    for (uint32_t d = 0; d < n_dcs; ++d) {
+        if (nw[d] == UINT64_MAX) continue;  // DC absent from NewDict: keep Last
+        if (last[d] == UINT64_MAX || nw[d] >= last[d]) {  // update_func_min/2
+            last[d] = nw[d];
+            c = 1;
+        }
+    }
+    if (changed) *changed = c;
+    return AGN_OK;
+}
+
+// ---- RCCL ------------------------------------------------------------------------
+int agn_comm_unique_id(uint8_t *out_id) {
+    static_assert(sizeof(ncclUniqueId) <= AGN_UNIQUE_ID_BYTES, "unique id size");
+    if (!out_id) return fail(AGN_EINVAL, "null id");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(AGN_ERCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+    std::memset(out_id, 0, AGN_UNIQUE_ID_BYTES);
+    std::memcpy(out_id, &id, sizeof id);
+    return AGN_OK;
+}
+
+int agn_comm_init(agn_ctx *ctx, int nranks, int rank, const uint8_t *id) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(AGN_EINVAL, "comm args");
+    std::lock_guard<std::mutex> g(ctx->comm_mu);
+    if (ctx->comm) return fail(AGN_EINVAL, "communicator already initialised");
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        ctx->comm = nullptr;
+        return fail(AGN_ERCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    return AGN_OK;
+}
+
+int agn_comm_destroy(agn_ctx *ctx) {
+    if (!ctx) return AGN_OK;
+    std::lock_guard<std::mutex> g(ctx->comm_mu);
+    if (ctx->comm) {
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    return AGN_OK;
+}
+
+int agn_gst_allreduce(agn_ctx *ctx, uint64_t *dev_vec, uint64_t n_words_, void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(ctx->comm_mu);
+    if (!ctx->comm) return fail(AGN_EINVAL, "no communicator (agn_comm_init)");
+    ncclResult_t r = ncclAllReduce(dev_vec, dev_vec, n_words_, ncclUint64, ncclMin, ctx->comm,
+                                   (hipStream_t)stream);
+    if (r != ncclSuccess) return fail(AGN_ERCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    return AGN_OK;
+}
+
+}  // extern "C"
+
+// ---- synthetic generator ------------------------------------------------------------
+namespace agn {
+namespace {
+
+uint32_t gen_live_lists(const agn_gen_cfg &c) {
+    return c.crdt_type == AGN_SET_AW ? (c.n_elems ? c.n_elems : 1) : 1;
+}
+
+int check_cfg(const agn_gen_cfg *c) {
+    if (!c) return fail(AGN_EINVAL, "null cfg");
+    if (c->n_dcs == 0 || c->n_dcs > 256) return fail(AGN_EINVAL, "gen: n_dcs");
+    if (c->ops_per_key >= (1u << 24) - 1) return fail(AGN_EINVAL, "gen: ops_per_key");
+    if (c->crdt_type != AGN_COUNTER_PN && !is_tag_type(c->crdt_type))
+        return fail(AGN_EINVAL, "gen: crdt_type");
+    return AGN_OK;
+}
+
+__global__ void k_gen(agn_gen_cfg cfg, agn_log log, agn_read req, int pass, uint64_t *scratch,
+                      uint32_t *rem_cnt) {
+    const uint32_t D = cfg.n_dcs, N = cfg.ops_per_key;
+    const uint32_t nl = cfg.crdt_type == AGN_SET_AW ? (cfg.n_elems ? cfg.n_elems : 1) : 1;
+    const uint64_t per = (uint64_t)D + (uint64_t)nl * GEN_MAX_LIVE + nl;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t *my = scratch + tid * per;
+    for (uint64_t k = tid; k < cfg.n_keys; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e0 = k * N;
+        GenOut o{};
+        o.clk = my;
+        o.live = my + D;
+        o.live_n = (uint32_t *)(my + D + (uint64_t)nl * GEN_MAX_LIVE);
+        if (pass == 0) {
+            o.rem_cnt = rem_cnt + e0;
+        } else {
+            o.oc = (uint64_t *)log.oc + e0 * D;
+            o.op_id = (uint32_t *)log.op_id + e0;
+            o.eff = (int64_t *)log.eff + (log.eff ? e0 : 0);
+            o.tag = (uint32_t *)log.tag + (log.tag ? e0 : 0);
+            o.add_tok = (uint64_t *)log.add_tok + (log.add_tok ? e0 : 0);
+            o.rem_off = log.rem_off ? log.rem_off + e0 : nullptr;
+            o.rem_tok = (uint64_t *)log.rem_tok;
+            o.R = (uint64_t *)req.R + k * D;
+            o.sct = req.sct ? (uint64_t *)req.sct + k * D : nullptr;
+            o.sct_ignore = req.sct_ignore ? (uint8_t *)req.sct_ignore + k : nullptr;
+        }
+        gen_key(cfg, k, o);
+        if (pass == 1 && k == 0) ((uint64_t *)log.key_off)[0] = 0;
+        if (pass == 1) ((uint64_t *)log.key_off)[k + 1] = (k + 1) * (uint64_t)N;
+    }
+}
+
+template <class T>
+T *dmalloc(uint64_t n, int &err) {
+    if (err || n == 0) return nullptr;
+    void *p = nullptr;
+    if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) {
+        err = fail(AGN_ENOMEM, "gen: hipMalloc(%llu)", (unsigned long long)(n * sizeof(T)));
+        return nullptr;
+    }
+    return (T *)p;
+}
+
+}  // namespace
+}  // namespace agn
+
+extern "C" {
+
+int agn_gen_dev(agn_ctx *ctx, const agn_gen_cfg *cfg, agn_log *log, agn_read *req,
+                void *stream) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (!log || !req) return fail(AGN_EINVAL, "null out");
+    std::memset(log, 0, sizeof *log);
+    std::memset(req, 0, sizeof *req);
+    hipStream_t s = (hipStream_t)stream;
+    const agn_gen_cfg c = *cfg;
+    const uint32_t D = c.n_dcs;
+    const uint64_t K = c.n_keys, E = K * c.ops_per_key;
+    const bool tags = is_tag_type(c.crdt_type);
+    int err = AGN_OK;
+    log->crdt_type = c.crdt_type;
+    log->n_dcs = D;
+    log->n_keys = K;
+    log->n_entries = E;
+    log->key_off = dmalloc<uint64_t>(K + 1, err);
+    log->oc = dmalloc<uint64_t>(E * D, err);
+    log->op_id = dmalloc<uint32_t>(E, err);
+    if (!tags) {
+        log->eff = dmalloc<int64_t>(E, err);
+    } else {
+        log->tag = dmalloc<uint32_t>(E, err);
+        log->add_tok = dmalloc<uint64_t>(E, err);
+        log->rem_off = dmalloc<uint32_t>(E + 1, err);
+    }
+    req->n_req = K;
+    req->req_type = c.crdt_type;
+    req->R = dmalloc<uint64_t>(K * D, err);
+    if (c.warm) {
+        req->sct = dmalloc<uint64_t>(K * D, err);
+        req->sct_ignore = dmalloc<uint8_t>(K, err);
+    }
+    const uint32_t nl = gen_live_lists(c);
+    const uint64_t threads = std::min<uint64_t>(std::max<uint64_t>(K, 1), 256ull * 1024ull);
+    const uint64_t per = (uint64_t)D + (uint64_t)nl * GEN_MAX_LIVE + nl;
+    uint64_t *scratch = dmalloc<uint64_t>(threads * per, err);
+    if (err) { agn_gen_free_dev(ctx, log, req); if (scratch) (void)hipFree(scratch); return err; }
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    if (tags && E) {
+        // pass 0: removal counts into rem_off[1..E], inclusive scan, rem_off[0] = 0
+        uint32_t *ro = (uint32_t *)log->rem_off;
+        hipLaunchKernelGGL(k_gen, dim3(blocks), dim3(256), 0, s, c, *log, *req, 0, scratch, ro + 1);
+        size_t tmp_bytes = 0;
+        hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, ro + 1, ro + 1, (int)E, s);
+        void *tmp = dmalloc<uint8_t>(tmp_bytes ? tmp_bytes : 1, err);
+        if (!err) hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, ro + 1, ro + 1, (int)E, s);
+        if (!err) (void)hipMemsetAsync(ro, 0, sizeof(uint32_t), s);
+        uint32_t total = 0;
+        if (!err) (void)hipMemcpyAsync(&total, ro + E, sizeof total, hipMemcpyDeviceToHost, s);
+        if (!err) (void)hipStreamSynchronize(s);
+        if (tmp) (void)hipFree(tmp);
+        log->rem_tok = dmalloc<uint64_t>(total ? total : 1, err);
+    } else if (tags) {
+        (void)hipMemsetAsync((void *)log->rem_off, 0, sizeof(uint32_t), s);
+        log->rem_tok = dmalloc<uint64_t>(1, err);
+    }
+    if (err) { (void)hipFree(scratch); agn_gen_free_dev(ctx, log, req); return err; }
+    if (K == 0) (void)hipMemsetAsync((void *)log->key_off, 0, sizeof(uint64_t), s);
+    hipLaunchKernelGGL(k_gen, dim3(blocks), dim3(256), 0, s, c, *log, *req, 1, scratch, nullptr);
+    hipError_t he = hipGetLastError();
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(scratch);
+    if (he != hipSuccess) return fail(AGN_EHIP, "k_gen: %s", hipGetErrorString(he));
+    return AGN_OK;
+}
+
+int agn_gen_free_dev(agn_ctx *ctx, agn_log *log, agn_read *req) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    const void *ptrs[] = {log ? log->key_off : nullptr, log ? log->key_type : nullptr,
+                          log ? log->oc : nullptr, log ? log->oc_mask : nullptr,
+                          log ? log->op_id : nullptr, log ? log->txid : nullptr,
+                          log ? log->eff : nullptr, log ? log->tag : nullptr,
+                          log ? log->add_tok : nullptr, log ? log->rem_off : nullptr,
+                          log ? log->rem_tok : nullptr, req ? req->keys : nullptr,
+                          req ? req->R : nullptr, req ? req->R_mask : nullptr,
+                          req ? req->sct : nullptr, req ? req->sct_mask : nullptr,
+                          req ? req->sct_ignore : nullptr, req ? req->txid : nullptr,
+                          req ? req->base_value : nullptr, req ? req->base_off : nullptr,
+                          req ? req->base_tag : nullptr, req ? req->base_tok : nullptr};
+    for (const void *p : ptrs)
+        if (p) (void)hipFree((void *)p);
+    if (log) std::memset(log, 0, sizeof *log);
+    if (req) std::memset(req, 0, sizeof *req);
+    return AGN_OK;
+}
+
+int agn_gen_host(const agn_gen_cfg *cfg, agn_log *log, agn_read *req) {
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (!log || !req) return fail(AGN_EINVAL, "null out");
+    std::memset(log, 0, sizeof *log);
+    std::memset(req, 0, sizeof *req);
+    const agn_gen_cfg c = *cfg;
+    const uint32_t D = c.n_dcs, N = c.ops_per_key;
+    const uint64_t K = c.n_keys, E = K * N;
+    const bool tags = is_tag_type(c.crdt_type);
+    auto hm = [](uint64_t bytes) { return std::calloc(bytes ? bytes : 1, 1); };
+    log->crdt_type = c.crdt_type;
+    log->n_dcs = D;
+    log->n_keys = K;
+    log->n_entries = E;
+    uint64_t *key_off = (uint64_t *)hm((K + 1) * 8);
+    for (uint64_t k = 0; k <= K; ++k) key_off[k] = k * N;
+    log->key_off = key_off;
+    log->oc = (uint64_t *)hm(E * D * 8);
+    log->op_id = (uint32_t *)hm(E * 4);
+    if (!tags) log->eff = (int64_t *)hm(E * 8);
+    else {
+        log->tag = (uint32_t *)hm(E * 4);
+        log->add_tok = (uint64_t *)hm(E * 8);
+        log->rem_off = (uint32_t *)hm((E + 1) * 4);
+    }
+    req->n_req = K;
+    req->req_type = c.crdt_type;
+    req->R = (uint64_t *)hm(K * D * 8);
+    if (c.warm) {
+        req->sct = (uint64_t *)hm(K * D * 8);
+        req->sct_ignore = (uint8_t *)hm(K);
+    }
+    const uint32_t nl = gen_live_lists(c);
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt < 1) nt = 1;
+    if (nt > 32) nt = 32;
+    if ((uint64_t)nt > K) nt = K ? (unsigned)K : 1;
+    auto run = [&](int pass, unsigned t) {
+        std::vector<uint64_t> clk(D), live((size_t)nl * GEN_MAX_LIVE);
+        std::vector<uint32_t> live_n(nl);
+        for (uint64_t k = t; k < K; k += nt) {
+            const uint64_t e0 = k * N;
+            GenOut o{};
+            o.clk = clk.data();
+            o.live = live.data();
+            o.live_n = live_n.data();
+            if (pass == 0) {
+                o.rem_cnt = (uint32_t *)log->rem_off + 1 + e0;
+            } else {
+                o.oc = (uint64_t *)log->oc + e0 * D;
+                o.op_id = (uint32_t *)log->op_id + e0;
+                o.eff = log->eff ? (int64_t *)log->eff + e0 : nullptr;
+                o.tag = log->tag ? (uint32_t *)log->tag + e0 : nullptr;
+                o.add_tok = log->add_tok ? (uint64_t *)log->add_tok + e0 : nullptr;
+                o.rem_off = log->rem_off ? log->rem_off + e0 : nullptr;
+                o.rem_tok = (uint64_t *)log->rem_tok;
+                o.R = (uint64_t *)req->R + k * D;
+                o.sct = req->sct ? (uint64_t *)req->sct + k * D : nullptr;
+                o.sct_ignore = req->sct_ignore ? (uint8_t *)req->sct_ignore + k : nullptr;
+            }
+            gen_key(c, k, o);
+        }
+    };
+    auto par = [&](int pass) {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t) th.emplace_back(run, pass, t);
+        for (auto &x : th) x.join();
+    };
+    if (tags) {
+        par(0);
+        uint32_t *ro = (uint32_t *)log->rem_off;
+        ro[0] = 0;
+        for (uint64_t e = 0; e < E; ++e) ro[e + 1] += ro[e];
+        log->rem_tok = (uint64_t *)hm((uint64_t)ro[E] * 8);
+    }
+    par(1);
+    return AGN_OK;
+}
+
+int agn_gen_free_host(agn_log *log, agn_read *req) {
+    if (log) {
+        std::free((void *)log->key_off); std::free((void *)log->key_type);
+        std::free((void *)log->oc); std::free((void *)log->oc_mask);
+        std::free((void *)log->op_id); std::free((void *)log->txid);
+        std::free((void *)log->eff); std::free((void *)log->tag);
+        std::free((void *)log->add_tok); std::free((void *)log->rem_off);
+        std::free((void *)log->rem_tok);
+        std::memset(log, 0, sizeof *log);
+    }
+    if (req) {
+        std::free((void *)req->keys); std::free((void *)req->R); std::free((void *)req->R_mask);
+        std::free((void *)req->sct); std::free((void *)req->sct_mask);
+        std::free((void *)req->sct_ignore); std::free((void *)req->txid);
+        std::free((void *)req->base_value); std::free((void *)req->base_off);
+        std::free((void *)req->base_tag); std::free((void *)req->base_tok);
+        std::memset(req, 0, sizeof *req);
+    }
+    return AGN_OK;
+}
+
+}  // extern "C"

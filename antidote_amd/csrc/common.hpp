@@ -1,0 +1,75 @@
+// common.hpp — shared device/host helpers for the gfx950 engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/antidote_gpu.h"
+
+#define AGN_WAVE 64
+
+namespace agn {
+
+// Thread-local last-error message (agn_last_error).
+void set_error(const char *fmt, ...);
+int fail(int code, const char *fmt, ...);
+
+#define AGN_HIP(call)                                                              \
+    do {                                                                           \
+        hipError_t e_ = (call);                                                    \
+        if (e_ != hipSuccess)                                                      \
+            return ::agn::fail(AGN_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #call, \
+                               hipGetErrorString(e_));                             \
+    } while (0)
+
+__host__ __device__ inline uint32_t n_words(uint32_t d) { return (d + 63u) / 64u; }
+
+// ---- wave-level helpers (wave64) ------------------------------------------
+__device__ inline uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ inline int lane_id() { return threadIdx.x & (AGN_WAVE - 1); }
+
+__device__ inline uint64_t shfl_xor_u64(uint64_t v, int m) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = __shfl_xor(lo, m, AGN_WAVE);
+    hi = __shfl_xor(hi, m, AGN_WAVE);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ inline int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += (int64_t)shfl_xor_u64((uint64_t)v, m);
+    return v;
+}
+
+__device__ inline uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// Scalar (wave-uniform) value: lets hipcc keep it in an SGPR.
+__device__ inline uint64_t uniform_u64(uint64_t v) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Grid sizing for the streaming kernels: enough waves to fill 256 CUs.
+inline unsigned grid_for(uint64_t work_items, unsigned items_per_block, unsigned max_blocks) {
+    uint64_t b = (work_items + items_per_block - 1) / items_per_block;
+    if (b < 1) b = 1;
+    if (b > max_blocks) b = max_blocks;
+    return (unsigned)b;
+}
+
+// Launchers (defined in the .hip files).
+int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
+                   hipStream_t s);
+int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
+                hipStream_t s);
+int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
+                   const uint8_t *defined, uint64_t *out, hipStream_t s);
+int launch_gst_finalize(uint32_t D, uint64_t E, uint64_t *vec, hipStream_t s);
+int launch_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,
+                       const uint64_t *clocks, const uint64_t *clock_mask,
+                       const uint64_t *R, const uint64_t *R_mask, int32_t *out_idx,
+                       uint8_t *out_is_first, hipStream_t s);
+
+}  // namespace agn

@@ -1,0 +1,159 @@
+// gst.hip — global stable time and base-snapshot selection on gfx950.
+//
+// get_min_time/1 (src/stable_time_functions.erl:51-85): per DC, the min of
+// the partition clocks that contain it; an `undefined` partition zeroes every
+// output DC.  Layout [E epochs][P partitions][D] u64, absent = UINT64_MAX, so
+// the dict "union of keys" survives an elementwise min; the extra word D of
+// each output row carries "every partition defined" (min of 1/0), which is
+// also what the RCCL ncclMin allreduce across GPUs combines
+// (meta_data_sender merge, src/meta_data_sender.erl:230-255).
+//
+// k_gst_min: each block reduces a band of partition rows of one epoch into an
+// LDS column-min (ds_min_u64), then one global atomicMin per column.  HBM bytes
+// per epoch: 8*P*D + P (defined) + 8*(D+1).
+//
+// k_select_base: vector_orddict:get_smaller/2 (src/vector_orddict.erl:74-87):
+// first cached clock (newest first) that is le the read clock.
+#include "common.hpp"
+
+namespace agn {
+namespace {
+
+__global__ void k_gst_init(uint64_t *out, uint32_t D, uint64_t E) {
+    const uint64_t n = E * (uint64_t)(D + 1);
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (uint64_t)gridDim.x * blockDim.x)
+        out[x] = ((x % (D + 1)) == D) ? 1ull : ~0ull;
+}
+
+constexpr int GST_THREADS = 256;
+constexpr uint32_t GST_MAX_LDS_D = 4096;
+
+__global__ __launch_bounds__(GST_THREADS) void k_gst_min(const uint64_t *__restrict__ clocks,
+                                                         const uint8_t *__restrict__ defined,
+                                                         uint64_t *out, uint32_t D, uint64_t P,
+                                                         uint64_t rows_per_block,
+                                                         uint64_t bands) {
+    __shared__ uint64_t colmin[GST_MAX_LDS_D];
+    __shared__ int all_def;
+    const uint64_t e = blockIdx.x / bands;
+    const uint64_t band = blockIdx.x % bands;
+    const uint64_t p0 = band * rows_per_block;
+    const uint64_t p1 = p0 + rows_per_block < P ? p0 + rows_per_block : P;
+    for (uint32_t d = threadIdx.x; d < D; d += GST_THREADS) colmin[d] = ~0ull;
+    if (threadIdx.x == 0) all_def = 1;
+    __syncthreads();
+
+    // undefined partitions contribute no clock, only the flag
+    if (defined) {
+        for (uint64_t p = p0 + threadIdx.x; p < p1; p += GST_THREADS)
+            if (!defined[e * P + p]) all_def = 0;
+    }
+    __syncthreads();
+    const uint64_t *base = clocks + (e * P + p0) * D;
+    const uint64_t n = (p1 - p0) * D;
+    // flat walk of the band; consecutive threads read consecutive words
+    uint64_t acc = ~0ull;
+    uint32_t acc_d = 0xffffffffu;
+    for (uint64_t x = threadIdx.x; x < n; x += GST_THREADS) {
+        const uint64_t p = p0 + x / D;
+        const uint32_t d = (uint32_t)(x % D);
+        if (defined && !defined[e * P + p]) continue;
+        const uint64_t v = base[x];
+        if (d == acc_d) {
+            acc = v < acc ? v : acc;
+        } else {
+            if (acc_d != 0xffffffffu) atomicMin((unsigned long long *)&colmin[acc_d], acc);
+            acc_d = d;
+            acc = v;
+        }
+    }
+    if (acc_d != 0xffffffffu) atomicMin((unsigned long long *)&colmin[acc_d], acc);
+    __syncthreads();
+    uint64_t *o = out + e * (uint64_t)(D + 1);
+    for (uint32_t d = threadIdx.x; d < D; d += GST_THREADS)
+        if (colmin[d] != ~0ull) atomicMin((unsigned long long *)&o[d], colmin[d]);
+    if (threadIdx.x == 0 && !all_def) atomicMin((unsigned long long *)&o[D], 0ull);
+}
+
+__global__ void k_gst_finalize(uint64_t *vec, uint32_t D, uint64_t E) {
+    const uint64_t n = E * (uint64_t)D;
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = x / D, d = x % D;
+        uint64_t *row = vec + e * (uint64_t)(D + 1);
+        if (row[D] == 0ull && row[d] != ~0ull) row[d] = 0ull;  // FoundUndefined (:78-82)
+    }
+}
+
+__global__ void k_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,
+                              const uint64_t *clocks, const uint64_t *clock_mask,
+                              const uint64_t *R, const uint64_t *R_mask, int32_t *out_idx,
+                              uint8_t *out_is_first) {
+    const uint32_t W = n_words(D);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_req;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        int32_t idx = -1;
+        uint8_t first = 1;
+        const uint64_t c0 = cache_off[i], c1 = cache_off[i + 1];
+        for (uint64_t c = c0; c < c1; ++c) {
+            bool le = true;  // vectorclock:le(Clock, R): missing entries read 0
+            for (uint32_t d = 0; d < D && le; ++d) {
+                const bool pa = !clock_mask || ((clock_mask[c * W + (d >> 6)] >> (d & 63)) & 1ull);
+                if (!pa) continue;
+                const bool pb = !R_mask || ((R_mask[i * W + (d >> 6)] >> (d & 63)) & 1ull);
+                const uint64_t b = pb ? R[i * D + d] : 0ull;
+                le = clocks[c * D + d] <= b;
+            }
+            if (le) {
+                idx = (int32_t)(c - c0);
+                break;
+            }
+            first = 0;
+        }
+        out_idx[i] = idx;
+        out_is_first[i] = first;
+    }
+}
+
+}  // namespace
+
+int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
+                   const uint8_t *defined, uint64_t *out, hipStream_t s) {
+    if (D == 0 || D > GST_MAX_LDS_D) return fail(AGN_ENOTSUP, "gst: D=%u unsupported", D);
+    hipLaunchKernelGGL(k_gst_init, dim3(grid_for(E * (D + 1), 256, 1024)), dim3(256), 0, s,
+                       out, D, E);
+    AGN_HIP(hipGetLastError());
+    if (P == 0 || E == 0) return AGN_OK;
+    // ~16 KB of clocks per block; at least 1 row
+    uint64_t rows = (16384 / 8) / D;
+    if (rows < 1) rows = 1;
+    const uint64_t bands = (P + rows - 1) / rows;
+    const uint64_t blocks = E * bands;
+    if (blocks > 0x7fffffffull) return fail(AGN_ENOTSUP, "gst: grid too large");
+    hipLaunchKernelGGL(k_gst_min, dim3((unsigned)blocks), dim3(GST_THREADS), 0, s, clocks,
+                       defined, out, D, P, rows, bands);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+int launch_gst_finalize(uint32_t D, uint64_t E, uint64_t *vec, hipStream_t s) {
+    if (E == 0 || D == 0) return AGN_OK;
+    hipLaunchKernelGGL(k_gst_finalize, dim3(grid_for(E * D, 256, 1024)), dim3(256), 0, s, vec,
+                       D, E);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+int launch_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,
+                       const uint64_t *clocks, const uint64_t *clock_mask, const uint64_t *R,
+                       const uint64_t *R_mask, int32_t *out_idx, uint8_t *out_is_first,
+                       hipStream_t s) {
+    if (n_req == 0) return AGN_OK;
+    hipLaunchKernelGGL(k_select_base, dim3(grid_for(n_req, 256, 4096)), dim3(256), 0, s, D,
+                       n_req, cache_off, clocks, clock_mask, R, R_mask, out_idx, out_is_first);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+}  // namespace agn

@@ -1,0 +1,224 @@
+"""Thin object wrapper over the C ABI: a device context, device buffers,
+device-resident op logs / read batches / results, and the batched entry
+points.  Everything numeric happens in libantidote_gpu.so."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from ._lib import EngineUnavailable, check, load
+from .encode import (EncodedLog, EncodedRead, ResultArrays, alloc_result, log_struct, n_words,
+                     read_struct, result_struct)
+
+
+class DevBuf:
+    """HBM allocation owned by an Engine (agn_dev_alloc)."""
+
+    def __init__(self, eng: "Engine", nbytes: int):
+        self.eng, self.nbytes = eng, int(nbytes)
+        p = C.c_void_p()
+        check(eng.lib.agn_dev_alloc(eng.ctx, self.nbytes, C.byref(p)), "agn_dev_alloc")
+        self.ptr = p.value or 0
+        eng._bufs.add(self)
+
+    def free(self):
+        if self.ptr:
+            self.eng.lib.agn_dev_free(self.eng.ctx, self.ptr)
+            self.ptr = 0
+        self.eng._bufs.discard(self)
+
+
+@dataclass
+class DeviceArrays:
+    """Device copies of an Encoded* / Result structure (same field names)."""
+    struct: object
+    bufs: dict = field(default_factory=dict)
+    shapes: dict = field(default_factory=dict)
+
+
+class Engine:
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.ctx = C.c_void_p()
+        rc = self.lib.agn_open(device, C.byref(self.ctx))
+        if rc in (_abi.ENODEV, _abi.ENOTSUP):
+            raise EngineUnavailable(self.lib.agn_last_error().decode())
+        check(rc, "agn_open")
+        self.device = device
+        self._bufs: set = set()
+
+    # ---------------------------------------------------------------- memory
+    def close(self):
+        for b in list(self._bufs):
+            b.free()
+        if self.ctx:
+            self.lib.agn_close(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def upload(self, arr: np.ndarray | None) -> DevBuf | None:
+        if arr is None:
+            return None
+        arr = np.ascontiguousarray(arr)
+        b = DevBuf(self, max(arr.nbytes, 8))
+        if arr.nbytes:
+            check(self.lib.agn_memcpy_h2d(self.ctx, b.ptr, arr.ctypes.data, arr.nbytes, None))
+        return b
+
+    def empty(self, nbytes: int) -> DevBuf:
+        return DevBuf(self, max(int(nbytes), 8))
+
+    def download(self, buf: DevBuf, dtype, shape, stream=None) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        if out.nbytes:
+            check(self.lib.agn_memcpy_d2h(self.ctx, out.ctypes.data, buf.ptr, out.nbytes, stream))
+            check(self.lib.agn_stream_sync(self.ctx, stream))
+        return out
+
+    def sync(self, stream=None):
+        check(self.lib.agn_stream_sync(self.ctx, stream))
+
+    # ---------------------------------------------------------------- materialize
+    def materialize_host(self, log: EncodedLog, req: EncodedRead, sparse: bool = True,
+                         cap_off=None) -> ResultArrays:
+        """Host arrays in, host arrays out (agn_materialize_host)."""
+        res = alloc_result(req.n_req, log.n_dcs, sparse=sparse, cap_off=cap_off)
+        ls, rs, os_ = log_struct(log), read_struct(req, sparse=sparse), result_struct(res)
+        if not sparse:
+            ls.oc_mask = None
+        check(self.lib.agn_materialize_host(self.ctx, C.byref(ls), C.byref(rs), C.byref(os_)),
+              "agn_materialize_host")
+        return res
+
+    def upload_log(self, log: EncodedLog) -> DeviceArrays:
+        s = log_struct(log)
+        d = DeviceArrays(s)
+        for name in ("key_off", "key_type", "oc", "oc_mask", "op_id", "txid", "eff", "tag",
+                     "add_tok", "rem_off", "rem_tok"):
+            a = getattr(log, name)
+            if a is None or (isinstance(a, np.ndarray) and a.size == 0 and name != "rem_tok"):
+                setattr(s, name, None)
+                continue
+            b = self.upload(a)
+            d.bufs[name] = b
+            setattr(s, name, b.ptr)
+        return d
+
+    def upload_read(self, req: EncodedRead, sparse: bool = True) -> DeviceArrays:
+        s = read_struct(req, sparse=sparse)
+        d = DeviceArrays(s)
+        names = ["keys", "R", "sct", "sct_ignore", "txid", "base_value", "base_off", "base_tag",
+                 "base_tok"] + (["R_mask", "sct_mask"] if sparse else [])
+        for name in names:
+            if getattr(s, name) is None:
+                continue
+            b = self.upload(getattr(req, name))
+            d.bufs[name] = b
+            setattr(s, name, b.ptr)
+        return d
+
+    def alloc_result(self, n_req: int, n_dcs: int, sparse: bool, cap_off=None) -> DeviceArrays:
+        s = _abi.AgnResult()
+        d = DeviceArrays(s)
+        W = n_words(n_dcs)
+        spec = {"value": (np.int64, (n_req,)), "hole": (np.int64, (n_req,)),
+                "lastct": (np.uint64, (n_req, n_dcs)), "count": (np.uint32, (n_req,)),
+                "flags": (np.uint32, (n_req,)), "err_pos": (np.uint32, (n_req,))}
+        if sparse:
+            spec["lastct_mask"] = (np.uint64, (n_req, W))
+        if cap_off is not None:
+            total = max(int(cap_off[-1]), 1)
+            spec.update({"out_n": (np.uint32, (n_req,)), "out_tag": (np.uint32, (total,)),
+                         "out_tok": (np.uint64, (total,))})
+            b = self.upload(np.ascontiguousarray(cap_off, np.uint64))
+            d.bufs["out_off"] = b
+            d.shapes["out_off"] = (np.uint64, (n_req + 1,))
+            s.out_off = b.ptr
+        for name, (dt, shape) in spec.items():
+            b = self.empty(int(np.prod(shape)) * np.dtype(dt).itemsize)
+            d.bufs[name] = b
+            d.shapes[name] = (dt, shape)
+            setattr(s, name, b.ptr)
+        return d
+
+    def fetch_result(self, d: DeviceArrays, stream=None) -> ResultArrays:
+        get = {n: self.download(d.bufs[n], *d.shapes[n], stream=stream) for n in d.shapes}
+        return ResultArrays(value=get["value"], hole=get["hole"], lastct=get["lastct"],
+                            lastct_mask=get.get("lastct_mask"), count=get["count"],
+                            flags=get["flags"], err_pos=get["err_pos"], out_off=get.get("out_off"),
+                            out_n=get.get("out_n"), out_tag=get.get("out_tag"),
+                            out_tok=get.get("out_tok"))
+
+    def materialize(self, dlog, dreq, dres, stream=None):
+        ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
+        rs = dreq.struct if isinstance(dreq, DeviceArrays) else dreq
+        os_ = dres.struct if isinstance(dres, DeviceArrays) else dres
+        check(self.lib.agn_materialize(self.ctx, C.byref(ls), C.byref(rs), C.byref(os_), stream),
+              "agn_materialize")
+
+    # ---------------------------------------------------------------- generator
+    def gen_dev(self, cfg: _abi.AgnGenCfg, stream=None):
+        log, req = _abi.AgnLog(), _abi.AgnRead()
+        check(self.lib.agn_gen_dev(self.ctx, C.byref(cfg), C.byref(log), C.byref(req), stream),
+              "agn_gen_dev")
+        return log, req
+
+    def free_gen(self, log, req):
+        check(self.lib.agn_gen_free_dev(self.ctx, C.byref(log), C.byref(req)))
+
+    # ---------------------------------------------------------------- GST
+    def gst_min(self, n_dcs, n_parts, n_epochs, clocks_ptr, defined_ptr, out_ptr, stream=None):
+        check(self.lib.agn_gst_min(self.ctx, n_dcs, n_parts, n_epochs, clocks_ptr, defined_ptr,
+                                   out_ptr, stream), "agn_gst_min")
+
+    def gst_finalize(self, n_dcs, n_epochs, vec_ptr, stream=None):
+        check(self.lib.agn_gst_finalize(self.ctx, n_dcs, n_epochs, vec_ptr, stream),
+              "agn_gst_finalize")
+
+    def select_base(self, n_dcs, n_req, off_ptr, clocks_ptr, cmask_ptr, R_ptr, Rmask_ptr,
+                    idx_ptr, first_ptr, stream=None):
+        check(self.lib.agn_select_base(self.ctx, n_dcs, n_req, off_ptr, clocks_ptr, cmask_ptr,
+                                       R_ptr, Rmask_ptr, idx_ptr, first_ptr, stream),
+              "agn_select_base")
+
+    # ---------------------------------------------------------------- RCCL
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load()
+        buf = (C.c_uint8 * _abi.UNIQUE_ID_BYTES)()
+        check(lib.agn_comm_unique_id(buf), "agn_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = (C.c_uint8 * _abi.UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        check(self.lib.agn_comm_init(self.ctx, nranks, rank, buf), "agn_comm_init")
+
+    def gst_allreduce(self, vec_ptr, n_words_, stream=None):
+        check(self.lib.agn_gst_allreduce(self.ctx, vec_ptr, n_words_, stream), "agn_gst_allreduce")
+
+
+def gen_host(cfg: _abi.AgnGenCfg):
+    """Host-generated synthetic log (library-owned arrays) as numpy views."""
+    lib = load()
+    log, req = _abi.AgnLog(), _abi.AgnRead()
+    check(lib.agn_gen_host(C.byref(cfg), C.byref(log), C.byref(req)), "agn_gen_host")
+    return log, req
+
+
+def free_gen_host(log, req):
+    load().agn_gen_free_host(C.byref(log), C.byref(req))
+
+
+def host_view(ptr, dtype, n):
+    if not ptr or n == 0:
+        return np.zeros(0, dtype)
+    ct = np.ctypeslib.as_ctypes_type(np.dtype(dtype))
+    return np.ctypeslib.as_array((ct * int(n)).from_address(ptr))

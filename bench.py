@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""bench.py — materialized ops/s (+ VC compares/s) of the MI355X engine.
+
+One step = one agn_materialize pass over the whole device-resident batch: for
+every key of this GPU's vnode partitions, the VC snapshot filter + CRDT effect
+fold of clocksi_materializer:materialize/4.  Inputs (op log, read clocks) are
+generated on the device before the timed region (synthetic, SplitMix64,
+BASELINE.md §3); nothing is cached between steps — every step re-reads the
+whole log from HBM and rewrites every output.
+
+Sharding (weak scaling): key k lives in partition p = k mod 64 and on GPU
+g = p mod G (src/log_utilities.erl:65-70); with G | 64 each rank owns keys
+k = rank + G*i, i < keys_per_gpu.  Materialize has no collective.
+
+Default (no flags): N=1, BASELINE cfg2 = counter_pn, 10M keys x 64 ops/key,
+8-DC clocks, random snapshot VCs.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+CONFIGS = {
+    2: dict(name="cfg2 counter_pn materialize: 10M keys x 64 ops/key, 8-DC clocks, "
+                 "random snapshot VCs", crdt_type=1, n_dcs=8, n_keys=10_000_000,
+            ops_per_key=64, n_elems=0, seed=20250112 + 1),
+    3: dict(name="cfg3 set_aw materialize: 1M keys x 256 add/remove ops, 16-DC clocks, "
+                 "32 elems/key, order-aware tag resolution", crdt_type=2, n_dcs=16,
+            n_keys=1_000_000, ops_per_key=256, n_elems=32, seed=20250112 + 2),
+    4: dict(name="cfg4 register_mv materialize: 1M keys x 100 ops (100M ops total over G GPUs), "
+                 "64-DC clocks, concurrent-write pruning", crdt_type=3, n_dcs=64,
+            n_keys=1_000_000, ops_per_key=100, n_elems=16, seed=20250112 + 3, strong=True),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
+    ap.add_argument("--cpu-keys", type=int, default=-1,
+                    help="CPU-baseline sample size in keys (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="extra multi-thread CPU run")
+    ap.add_argument("--gst", action="store_true", help="also time a GST epoch + RCCL min-allreduce")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0):
+    """HBM bytes one materialize launch must move."""
+    D, N = cfg["n_dcs"], cfg["ops_per_key"]
+    ops = n_keys * N
+    if cfg["crdt_type"] == 1:
+        per_op = 8 * D + 8                    # OpSSCommit row + effect
+        per_key = 8 + 8 * D + 8 * D + 32      # key_off, R, LastOpCt, value/hole/count/flags/err/op_id
+        return ops * per_op + n_keys * per_key
+    per_op = 8 * D + 4 + 4 + 8 + 4            # oc, op_id, tag, add_tok, rem_off
+    per_key = 8 + 8 * D + 8 * D + 24 + 8 + 4  # key_off, R, LastOpCt, hole/count/flags/err, out_off, out_n
+    return ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key
+
+
+def cpu_baseline(cfg, n_keys, threads):
+    """The C oracle (oracle/liboracle.so, a restatement of the Erlang path) on a
+    bounded host-generated sample of the same workload."""
+    from antidote_amd import _abi
+    from antidote_amd.encode import alloc_result, result_struct
+    from antidote_amd.engine import free_gen_host, gen_host
+    lib = _abi.bind(C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so")), _abi.ORACLE_PROTOTYPES)
+    chunk = min(n_keys, 500_000 if cfg["n_dcs"] <= 16 else 100_000)
+    out = {}
+    for nt in ([1] + ([threads] if threads > 1 else [])):
+        done, secs = 0, 0.0
+        while done < n_keys:
+            k = min(chunk, n_keys - done)
+            g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=cfg["n_dcs"], n_keys=k,
+                               ops_per_key=cfg["ops_per_key"], n_elems=cfg["n_elems"],
+                               seed=cfg["seed"], key_base=done, key_stride=1, warm=0)
+            hl, hr = gen_host(g)
+            cap = (np.arange(k + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
+                   if cfg["crdt_type"] != 1 else None)
+            res = alloc_result(k, cfg["n_dcs"], sparse=False, cap_off=cap)
+            os_ = result_struct(res)
+            t0 = time.perf_counter()
+            rc = lib.oracle_materialize(C.byref(hl), C.byref(hr), C.byref(os_), nt)
+            secs += time.perf_counter() - t0
+            free_gen_host(hl, hr)
+            assert rc == 0
+            done += k
+        out[nt] = n_keys * cfg["ops_per_key"] / secs
+    return out
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(a.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from antidote_amd import _abi
+    from antidote_amd.engine import Engine
+
+    cfg = dict(CONFIGS[a.config])
+    n_keys = a.keys or cfg["n_keys"]
+    if cfg.get("strong") and not a.keys:
+        n_keys = cfg["n_keys"] // world      # cfg4 is quoted as a fixed total
+    gcfg = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=cfg["n_dcs"], n_keys=n_keys,
+                          ops_per_key=cfg["ops_per_key"], n_elems=cfg["n_elems"],
+                          seed=cfg["seed"], key_base=rank, key_stride=world, warm=0)
+    eng = Engine(local)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    t_gen = time.perf_counter()
+    dl, dr = eng.gen_dev(gcfg)
+    t_gen = time.perf_counter() - t_gen
+    cap = None
+    if cfg["crdt_type"] != 1:
+        cap = np.arange(n_keys + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
+    res = eng.alloc_result(n_keys, cfg["n_dcs"], sparse=False, cap_off=cap)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        eng.materialize(dl, dr, res, stream=sp)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s in range(a.steps):
+        ev[s][0].record(stream)
+        eng.materialize(dl, dr, res, stream=sp)
+        ev[s][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    # sanity: outputs exist and no error flags
+    flags = eng.download(res.bufs["flags"], np.uint32, (n_keys,))
+    count = eng.download(res.bufs["count"], np.uint32, (n_keys,))
+    err_keys = int((flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED |
+                             _abi.F_ERR_CAPACITY)).astype(bool).sum())
+    n_rem = n_live = 0
+    if cfg["crdt_type"] != 1:
+        E = n_keys * cfg["ops_per_key"]
+        n_rem = int(eng.download(type("B", (), {"ptr": dl.rem_off})(), np.uint32, (E + 1,))[-1])
+        n_live = int(eng.download(res.bufs["out_n"], np.uint64 if False else np.uint32,
+                                  (n_keys,)).astype(np.int64).sum())
+
+    ops_step = n_keys * cfg["ops_per_key"] * world
+    value = ops_step * a.steps / elapsed
+    bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+
+    gst = None
+    if a.gst:
+        gst = gst_bench(eng, torch, dist, world, rank, sp)
+
+    if rank == 0:
+        cpu = None
+        n_cpu = a.cpu_keys if a.cpu_keys >= 0 else (2_000_000 if cfg["n_dcs"] <= 16 else 200_000)
+        if world == 1 and n_cpu > 0:
+            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+            rates = cpu_baseline(cfg, min(n_cpu, n_keys), thr)
+            cpu = {"value": rates[1], "unit": "ops/s", "cores": 1, "kind": "port",
+                   "sample": f"{min(n_cpu, n_keys)} keys x {cfg['ops_per_key']} ops of the same "
+                             f"workload (host-generated, same SplitMix64 streams), "
+                             f"oracle/oracle.c -O3, 1 thread",
+                   "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
+                   "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_cfg{a.config}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                p = json.load(f)
+            if p.get("n_keys") == n_keys:
+                traffic = p.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "materialized ops/sec + VC compares/sec (1/2/4/8 GPU), % of HBM roofline",
+            "value": value, "unit": "ops/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong" if cfg.get("strong") else "weak",
+            "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (device SplitMix64 generator, BASELINE.md §3)",
+            "vc_compares_per_s": value,  # SCT = ignore: one D-wide compare per op
+            "config": {"workload": cfg["name"], "keys_per_gpu": n_keys,
+                       "ops_per_key": cfg["ops_per_key"], "n_dcs": cfg["n_dcs"],
+                       "partitioning": "vnode p = key mod 64, gpu = p mod G; no collective",
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch},
+            "cpu_baseline": cpu,
+            "error_keys": err_keys, "mean_included_ops": float(count.mean()),
+            "gen_s": t_gen,
+        }
+        if gst:
+            line["gst"] = gst
+        print(json.dumps(line), flush=True)
+
+    eng.free_gen(dl, dr)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def gst_bench(eng, torch, dist, world, rank, sp):
+    """cfg5: P=4096 partitions x D=256, local min over this GPU's partitions +
+    RCCL ncclMin allreduce; single-epoch latency and batched 256-epoch rate."""
+    from antidote_amd import _abi
+    from antidote_amd.engine import Engine
+    D, P, E = 256, 4096, 256
+    Pl = P // world
+    rng = np.random.default_rng(7 + rank)
+    clocks = (1_700_000_000_000_000 + rng.integers(0, 10 ** 9, (E, Pl, D))).astype(np.uint64)
+    dc = eng.upload(clocks)
+    out = eng.empty(E * (D + 1) * 8)
+    if world > 1:
+        uid = [Engine.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+    def one():
+        eng.gst_min(D, Pl, 1, dc.ptr, None, out.ptr, sp)
+        if world > 1:
+            eng.gst_allreduce(out.ptr, D + 1, sp)
+        eng.gst_finalize(D, 1, out.ptr, sp)
+    for _ in range(5):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(50):
+        one()
+    torch.cuda.synchronize()
+    lat = (time.perf_counter() - t0) / 50
+    b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    eng.gst_min(D, Pl, E, dc.ptr, None, out.ptr, sp)
+    b.record()
+    for _ in range(5):
+        eng.gst_min(D, Pl, E, dc.ptr, None, out.ptr, sp)
+    e.record()
+    torch.cuda.synchronize()
+    ms = b.elapsed_time(e) / 5
+    byts = E * Pl * D * 8 + E * (D + 1) * 8
+    dc.free()
+    out.free()
+    return {"epoch_latency_us": lat * 1e6, "batched_epochs": E, "batched_ms": ms,
+            "batched_GBps": byts / (ms * 1e-3) / 1e9, "partitions_per_gpu": Pl, "n_dcs": D}
+
+
+if __name__ == "__main__":
+    main()

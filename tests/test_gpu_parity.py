@@ -1,0 +1,315 @@
+"""Parity of the HIP engine with the C oracle (and, through it, with the
+reference's known answers).  Bit-exact on every output: value / state pairs,
+NewLastOp, LastOpCt (+ presence), Count, IsNewSS, error kind and position."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from antidote_amd import _abi
+from antidote_amd.encode import alloc_result, log_struct, read_struct, result_struct
+from antidote_amd.engine import Engine, free_gen_host, gen_host, host_view
+from kat_util import TYPES, OneKeyRun, kats, oracle_fn, py_ops, to_vc
+from synth import compare, random_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def gpu_fn(eng):
+    def fn(ls, rs, os_):
+        return eng.lib.agn_materialize_host(eng.ctx, C.byref(ls), C.byref(rs), C.byref(os_))
+    return fn
+
+
+# ------------------------------------------------------------------ KATs on the GPU
+MAT = kats({"materialize", "materialize_chain"})
+
+
+@pytest.mark.parametrize("c", MAT, ids=[c["name"] for c in MAT])
+def test_kat_materialize_gpu(eng, oracle_lib, c):
+    from test_oracle_kats import c_materialize_case, check_expect
+    r = c_materialize_case(gpu_fn(eng), c)
+    check_expect(r, c["expect"])
+    assert r == c_materialize_case(oracle_fn(oracle_lib), c)
+
+
+SYS = kats({"system_seq"})
+
+
+@pytest.mark.parametrize("c", SYS, ids=[c["name"] for c in SYS])
+def test_kat_system_seq_gpu(eng, c):
+    from kat_util import system_seq_log
+    from oracle import py_oracle as po
+    typ = TYPES[c["type"]]
+    ops, reads, _ = system_seq_log(c)
+    for i in range(len(reads)):
+        run = OneKeyRun(c["type"], ops, 1)
+        run.add_read(reads[i])
+        _, res = run.run(gpu_fn(eng))
+        g = run.decode(res, 0)
+        want = po.materialize(typ, po.IGNORE, reads[i], po.SnapshotGetResponse(
+            ops, len(ops), po.MaterializedSnapshot(0, po.crdt_new(typ)), po.IGNORE, True))
+        assert g == want
+
+
+# ------------------------------------------------------------------ randomised differential
+DIFF = []
+for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
+    for D in (1, 2, 3, 5, 8, 12, 16, 17, 33, 64, 100, 256):
+        for sparse in (False, True):
+            DIFF.append((crdt, D, sparse))
+
+
+@pytest.mark.parametrize("crdt,D,sparse", DIFF)
+def test_random_vs_oracle(eng, oracle_lib, crdt, D, sparse):
+    K = 300 if D <= 64 else 120
+    nmax = 150 if D <= 16 else 70
+    log, req, cap = random_case(7919 * crdt + 31 * D + sparse, crdt, K, D, nmax, sparse=sparse,
+                                warm=0.4, txid=0.3, invalid=0.02, corrupt=0.03,
+                                multi=0.15 if crdt == _abi.SET_AW else 0.0, base=0.4,
+                                identity=(D % 2 == 0))
+    res_g = eng.materialize_host(log, req, sparse=sparse, cap_off=cap)
+    res_o = alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)
+    ls, rs, os_ = log_struct(log), read_struct(req, sparse=sparse), result_struct(res_o)
+    if not sparse:
+        ls.oc_mask = None
+    assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
+    bad = compare(crdt, D, res_g, res_o, sparse, req.n_req)
+    assert not bad, bad[:10]
+
+
+def test_long_keys_vs_oracle(eng, oracle_lib):
+    """Keys far longer than a wave (1000+ ops, like large_list_test) and
+    set_aw state that forces table compaction."""
+    for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
+        log, req, cap = random_case(99 + crdt, crdt, 24, 8, 1500, warm=0.3, base=0.3,
+                                    n_elems=40, empty=0.0)
+        res_g = eng.materialize_host(log, req, sparse=False, cap_off=cap)
+        res_o = alloc_result(req.n_req, 8, sparse=False, cap_off=cap)
+        ls, rs, os_ = log_struct(log), read_struct(req, sparse=False), result_struct(res_o)
+        ls.oc_mask = None
+        oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4)
+        assert not compare(crdt, 8, res_g, res_o, False, req.n_req)
+
+
+def test_empty_batch_and_empty_log(eng):
+    log, req, cap = random_case(5, _abi.COUNTER_PN, 10, 4, 0, empty=1.0)
+    res = eng.materialize_host(log, req, sparse=False)
+    assert (res.count == 0).all() and (res.hole == 0).all()
+    assert ((res.flags & _abi.F_CT_IGNORE) > 0).sum() == int((req.sct_ignore == 1).sum())
+
+
+# ------------------------------------------------------------------ generator
+def _arrays(log, req, cfg, dev, eng):
+    D, K, N = cfg.n_dcs, cfg.n_keys, cfg.ops_per_key
+    E = K * N
+    if dev:
+        g = lambda p, dt, n: eng.download(type("B", (), {"ptr": p})(), dt, (n,))  # noqa: E731
+    else:
+        g = lambda p, dt, n: host_view(p, dt, n).copy()  # noqa: E731
+    out = {"key_off": g(log.key_off, np.uint64, K + 1), "oc": g(log.oc, np.uint64, E * D),
+           "op_id": g(log.op_id, np.uint32, E), "R": g(req.R, np.uint64, K * D)}
+    if cfg.crdt_type == _abi.COUNTER_PN:
+        out["eff"] = g(log.eff, np.int64, E)
+    else:
+        out["tag"] = g(log.tag, np.uint32, E)
+        out["add_tok"] = g(log.add_tok, np.uint64, E)
+        ro = g(log.rem_off, np.uint32, E + 1)
+        out["rem_off"] = ro
+        out["rem_tok"] = g(log.rem_tok, np.uint64, int(ro[-1]))
+    if cfg.warm:
+        out["sct"] = g(req.sct, np.uint64, K * D)
+    return out
+
+
+@pytest.mark.parametrize("crdt,D,N,warm", [(1, 8, 64, 0), (1, 3, 100, 1), (2, 16, 256, 0),
+                                           (3, 64, 100, 1)])
+def test_device_generator_matches_host(eng, crdt, D, N, warm):
+    cfg = _abi.AgnGenCfg(crdt_type=crdt, n_dcs=D, n_keys=777, ops_per_key=N, n_elems=32 if
+                         crdt == 2 else 16, seed=20250112 + crdt, key_base=5, key_stride=3,
+                         warm=warm)
+    dl, dr = eng.gen_dev(cfg)
+    hl, hr = gen_host(cfg)
+    try:
+        a = _arrays(dl, dr, cfg, True, eng)
+        b = _arrays(hl, hr, cfg, False, eng)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+    finally:
+        eng.free_gen(dl, dr)
+        free_gen_host(hl, hr)
+
+
+# ------------------------------------------------------------------ full-size configs
+def _run_dev(eng, cfg):
+    """Generate on device, materialize on device, return (log, req, device result)."""
+    dl, dr = eng.gen_dev(cfg)
+    K, D = cfg.n_keys, cfg.n_dcs
+    cap = None
+    if cfg.crdt_type != _abi.COUNTER_PN:
+        # capacity = adds per key + 0 base: bound by ops_per_key
+        cap = np.arange(K + 1, dtype=np.uint64) * np.uint64(cfg.ops_per_key)
+    res = eng.alloc_result(K, D, sparse=False, cap_off=cap)
+    eng.materialize(dl, dr, res)
+    eng.sync()
+    return dl, dr, res
+
+
+def _sampled_oracle(oracle_lib, cfg, keys, cap_per_key):
+    """Host-generate only the sampled keys (same SplitMix64 streams) and run
+    the oracle on them."""
+    outs = []
+    for k in keys:
+        c1 = _abi.AgnGenCfg(crdt_type=cfg.crdt_type, n_dcs=cfg.n_dcs, n_keys=1,
+                            ops_per_key=cfg.ops_per_key, n_elems=cfg.n_elems, seed=cfg.seed,
+                            key_base=cfg.key_base + int(k) * cfg.key_stride,
+                            key_stride=cfg.key_stride, warm=cfg.warm)
+        hl, hr = gen_host(c1)
+        capo = np.array([0, cap_per_key], np.uint64) if cap_per_key else None
+        r = alloc_result(1, cfg.n_dcs, sparse=False, cap_off=capo)
+        os_ = result_struct(r)
+        assert oracle_lib.oracle_materialize(C.byref(hl), C.byref(hr), C.byref(os_), 1) == 0
+        free_gen_host(hl, hr)
+        outs.append(r)
+    return outs
+
+
+FULL = [
+    # BASELINE cfg2: counter_pn 10M keys x 64 ops, D=8
+    dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0, seed=20250113),
+    # BASELINE cfg3: set_aw 1M keys x 256 ops, D=16, 32 elems
+    dict(crdt_type=2, n_dcs=16, n_keys=1_000_000, ops_per_key=256, n_elems=32, seed=20250114),
+    # BASELINE cfg4 (one GPU's shard at G=8): register_mv 125k keys x 100 ops, D=64
+    dict(crdt_type=3, n_dcs=64, n_keys=125_000, ops_per_key=100, n_elems=16, seed=20250115,
+         key_stride=8),
+]
+
+
+@pytest.mark.parametrize("spec", FULL, ids=["cfg2_counter", "cfg3_set_aw", "cfg4_register_mv"])
+def test_full_size_sampled_parity(eng, oracle_lib, spec):
+    cfg = _abi.AgnGenCfg(key_base=0, key_stride=1, warm=0, **{k: v for k, v in spec.items()})
+    if "key_stride" in spec:
+        cfg.key_stride = spec["key_stride"]
+    dl, dr, res = _run_dev(eng, cfg)
+    try:
+        K, D = cfg.n_keys, cfg.n_dcs
+        flags = eng.download(res.bufs["flags"], np.uint32, (K,))
+        count = eng.download(res.bufs["count"], np.uint32, (K,))
+        # size-independent properties over every key
+        assert not (flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED |
+                             _abi.F_ERR_CAPACITY)).any()
+        assert (count <= cfg.ops_per_key).all()
+        assert (((flags & _abi.F_NEWSS) > 0) == (count > 0)).all()
+        inc = count.mean() / cfg.ops_per_key
+        assert 0.2 < inc < 0.8, inc  # "random snapshot VCs": neither all nor none
+        # bit-exact on a random sample of keys
+        rng = np.random.default_rng(cfg.seed)
+        sample = np.sort(rng.choice(K, 64, replace=False))
+        sample[0], sample[-1] = 0, K - 1
+        cap = cfg.ops_per_key if cfg.crdt_type != 1 else 0
+        want = _sampled_oracle(oracle_lib, cfg, sample, cap)
+        full = eng.fetch_result(res)
+        for j, k in enumerate(sample):
+            w = want[j]
+            assert int(full.flags[k]) == int(w.flags[0])
+            assert int(full.hole[k]) == int(w.hole[0])
+            assert int(full.count[k]) == int(w.count[0])
+            assert np.array_equal(full.lastct[k], w.lastct[0])
+            if cfg.crdt_type == 1:
+                assert int(full.value[k]) == int(w.value[0])
+            else:
+                n = int(full.out_n[k])
+                o = int(full.out_off[k])
+                assert n == int(w.out_n[0])
+                assert np.array_equal(full.out_tag[o:o + n], w.out_tag[:n])
+                assert np.array_equal(full.out_tok[o:o + n], w.out_tok[:n])
+    finally:
+        eng.free_gen(dl, dr)
+        for b in res.bufs.values():
+            b.free()
+
+
+# ------------------------------------------------------------------ GST / base selection
+@pytest.mark.parametrize("D,P,E,p_undef,p_absent", [(2, 3, 1, 0.0, 0.0), (8, 64, 4, 0.05, 0.1),
+                                                    (256, 4096, 2, 0.0, 0.0),
+                                                    (256, 4096, 3, 0.001, 0.02),
+                                                    (5, 1000, 7, 0.01, 0.3), (300, 17, 2, 0.1, 0.5)])
+def test_gst_vs_oracle(eng, oracle_lib, D, P, E, p_undef, p_absent):
+    rng = np.random.default_rng(D * 7 + P)
+    clocks = (1_700_000_000_000_000 + rng.integers(0, 10 ** 9, (E, P, D))).astype(np.uint64)
+    clocks[rng.random((E, P, D)) < p_absent] = np.uint64(_abi.U64_MAX)
+    defined = (rng.random((E, P)) >= p_undef).astype(np.uint8)
+    want = np.zeros((E, D + 1), np.uint64)
+    oracle_lib.oracle_gst_min(D, P, E, clocks.ctypes.data, defined.ctypes.data, want.ctypes.data, 1)
+    dc, dd = eng.upload(clocks), eng.upload(defined)
+    out = eng.empty(E * (D + 1) * 8)
+    eng.gst_min(D, P, E, dc.ptr, dd.ptr, out.ptr)
+    eng.gst_finalize(D, E, out.ptr)
+    got = eng.download(out, np.uint64, (E, D + 1))
+    assert np.array_equal(got, want)
+    for b in (dc, dd, out):
+        b.free()
+
+
+def test_gst_kats_gpu(eng):
+    from oracle import py_oracle as po
+    for c in kats({"gst"}):
+        parts = {p: (po.UNDEFINED if v == "undefined" else to_vc(v)) for p, v in c["parts"].items()}
+        dcs = sorted({d for v in parts.values() if v != po.UNDEFINED for d in v}) or ["dc1"]
+        D, P = len(dcs), len(parts)
+        clocks = np.full((P, D), _abi.U64_MAX, np.uint64)
+        defined = np.ones(P, np.uint8)
+        for i, v in enumerate(parts.values()):
+            if v == po.UNDEFINED:
+                defined[i] = 0
+            else:
+                for j, d in enumerate(dcs):
+                    if d in v:
+                        clocks[i, j] = v[d]
+        dc, dd, out = eng.upload(clocks), eng.upload(defined), eng.empty((D + 1) * 8)
+        eng.gst_min(D, P, 1, dc.ptr, dd.ptr, out.ptr)
+        eng.gst_finalize(D, 1, out.ptr)
+        got = eng.download(out, np.uint64, (D + 1,))
+        res = {d: int(got[j]) for j, d in enumerate(dcs) if int(got[j]) != _abi.U64_MAX}
+        assert res == to_vc(c["expect"]), c["name"]
+
+
+def test_select_base_vs_oracle(eng, oracle_lib):
+    rng = np.random.default_rng(3)
+    for D in (2, 8, 64, 130):
+        n = 500
+        lens = rng.integers(0, 11, n)
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum(lens)
+        M = int(off[-1])
+        clocks = rng.integers(0, 100, (max(M, 1), D)).astype(np.uint64)
+        W = (D + 63) // 64
+        cm = rng.integers(0, 2 ** 62, (max(M, 1), W)).astype(np.uint64)
+        R = rng.integers(50, 150, (n, D)).astype(np.uint64)
+        Rm = rng.integers(0, 2 ** 62, (n, W)).astype(np.uint64) | np.uint64(0x5555)
+        wi, wf = np.zeros(n, np.int32), np.zeros(n, np.uint8)
+        oracle_lib.oracle_select_base(D, n, off.ctypes.data, clocks.ctypes.data, cm.ctypes.data,
+                                      R.ctypes.data, Rm.ctypes.data, wi.ctypes.data,
+                                      wf.ctypes.data)
+        bufs = [eng.upload(x) for x in (off, clocks, cm, R, Rm)]
+        oi, of = eng.empty(n * 4), eng.empty(n)
+        eng.select_base(D, n, *[b.ptr for b in bufs], oi.ptr, of.ptr)
+        assert np.array_equal(eng.download(oi, np.int32, (n,)), wi)
+        assert np.array_equal(eng.download(of, np.uint8, (n,)), wf)
+
+
+def test_rccl_single_rank_min_allreduce(eng):
+    uid = Engine.unique_id()
+    eng.comm_init(1, 0, uid)
+    v = np.array([5, 3, _abi.U64_MAX, 1], np.uint64)
+    b = eng.upload(v)
+    eng.gst_allreduce(b.ptr, 4)
+    eng.sync()
+    assert np.array_equal(eng.download(b, np.uint64, (4,)), v)

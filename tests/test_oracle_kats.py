@@ -46,7 +46,8 @@ def test_py_oracle_materialize(c):
     check_expect(py_materialize_case(c), c["expect"])
 
 
-def c_materialize_case(lib, c):
+def c_materialize_case(fn, c):
+    """fn(log_struct, read_struct, result_struct) -> rc (C oracle or engine)."""
     ops = py_ops(c)
     clocks = [p.snapshot_time for _, p in ops] + [to_vc(c["R"])]
     n_dcs = max(2, len({d for ck in clocks for d in ck} | {p.commit_time[0] for _, p in ops}))
@@ -54,20 +55,20 @@ def c_materialize_case(lib, c):
     if c["kind"] == "materialize_chain":
         f = c["first"]
         run.add_read(to_vc(f["R"]), to_vc(f["sct"]), base=f["base"][1])
-        _, res = run.run(oracle_fn(lib))
+        _, res = run.run(fn)
         _, v1, hole1, ct1, _, _ = run.decode(res, 0)
         run2 = OneKeyRun(c["type"], ops, n_dcs)
         run2.add_read(to_vc(c["R"]), ct1, base=v1)
-        _, res2 = run2.run(oracle_fn(lib))
+        _, res2 = run2.run(fn)
         return run2.decode(res2, 0)
     run.add_read(to_vc(c["R"]), to_vc(c["sct"]), base=c["base"][1])
-    _, res = run.run(oracle_fn(lib))
+    _, res = run.run(fn)
     return run.decode(res, 0)
 
 
 @pytest.mark.parametrize("c", MAT, ids=[c["name"] for c in MAT])
 def test_c_oracle_materialize(oracle_lib, c):
-    r = c_materialize_case(oracle_lib, c)
+    r = c_materialize_case(oracle_fn(oracle_lib), c)
     check_expect(r, c["expect"])
     # the two restatements agree on every field, asserted or not
     py = py_materialize_case(c)
