@@ -56,8 +56,9 @@ static int validate(const agn_log *log, const agn_read *req, const agn_result *o
     if (log->crdt_type != AGN_COUNTER_PN && !is_tag_type(log->crdt_type))
         return fail(AGN_EINVAL, "unknown crdt_type %u", log->crdt_type);
     if (req->n_req == 0) return AGN_OK;
-    if (!log->key_off || !log->op_id) return fail(AGN_EINVAL, "log: key_off/op_id required");
-    if (log->n_entries && !log->oc) return fail(AGN_EINVAL, "log: oc required");
+    if (!log->key_off) return fail(AGN_EINVAL, "log: key_off required");
+    if (log->n_entries && (!log->oc || !log->op_id))
+        return fail(AGN_EINVAL, "log: oc/op_id required");
     if (!req->keys && req->n_req != log->n_keys)
         return fail(AGN_EINVAL, "identity key map needs n_req == n_keys");
     if (!req->R) return fail(AGN_EINVAL, "read: R required");
@@ -71,8 +72,6 @@ static int validate(const agn_log *log, const agn_read *req, const agn_result *o
             return fail(AGN_EINVAL, "set/register log needs tag/add_tok/rem_off");
         if (!out->out_off || !out->out_n || !out->out_tag || !out->out_tok)
             return fail(AGN_EINVAL, "set/register result needs out_off/out_n/out_tag/out_tok");
-        if (req->base_off && (!req->base_tag || !req->base_tok))
-            return fail(AGN_EINVAL, "base state needs base_tag/base_tok");
     }
     return AGN_OK;
 }
@@ -181,9 +180,9 @@ int agn_stream_sync(agn_ctx *ctx, void *stream) {
 
 int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out,
                     void *stream) {
-    int rc = use_device(ctx);
+    int rc = validate(log, req, out);  // descriptors first: checkable without a GPU
     if (rc) return rc;
-    rc = validate(log, req, out);
+    rc = use_device(ctx);
     if (rc) return rc;
     if (req->n_req == 0) return AGN_OK;
     hipStream_t s = (hipStream_t)stream;
@@ -247,9 +246,9 @@ struct Staging {
 extern "C" {
 
 int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out) {
-    int rc = use_device(ctx);
+    int rc = validate(log, req, out);
     if (rc) return rc;
-    rc = validate(log, req, out);
+    rc = use_device(ctx);
     if (rc) return rc;
     if (req->n_req == 0) return AGN_OK;
     const uint32_t D = log->n_dcs, W = n_words(D);

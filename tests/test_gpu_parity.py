@@ -194,9 +194,7 @@ FULL = [
 
 @pytest.mark.parametrize("spec", FULL, ids=["cfg2_counter", "cfg3_set_aw", "cfg4_register_mv"])
 def test_full_size_sampled_parity(eng, oracle_lib, spec):
-    cfg = _abi.AgnGenCfg(key_base=0, key_stride=1, warm=0, **{k: v for k, v in spec.items()})
-    if "key_stride" in spec:
-        cfg.key_stride = spec["key_stride"]
+    cfg = _abi.AgnGenCfg(**{"key_base": 0, "key_stride": 1, "warm": 0, **spec})
     dl, dr, res = _run_dev(eng, cfg)
     try:
         K, D = cfg.n_keys, cfg.n_dcs
