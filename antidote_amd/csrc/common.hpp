@@ -62,6 +62,8 @@ inline unsigned grid_for(uint64_t work_items, unsigned items_per_block, unsigned
 // Launchers (defined in the .hip files).
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t s);
+int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
+                         hipStream_t s);
 int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
                 hipStream_t s);
 int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,

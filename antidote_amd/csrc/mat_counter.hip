@@ -12,6 +12,8 @@
 // (src/materializer.erl:53-58).
 // HBM bytes per op: 8*D (OpSSCommit) + 8 (effect); per key: 16 (key_off pair)
 // + 8*D (R) + 8*D (LastOpCt) + 32 (value, hole, count, flags, err_pos).
+#include <cstdlib>
+
 #include "filter.hpp"
 
 namespace agn {
@@ -102,6 +104,15 @@ int dispatch(const agn_log &log, const agn_read &req, const agn_result &out, hip
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t st) {
     if (req.n_req == 0) return AGN_OK;
+    // AGN_COUNTER_IMPL=general forces the general kernel (A/B and tests)
+    const bool force_general = [] {
+        const char *v = getenv("AGN_COUNTER_IMPL");
+        return v && v[0] == 'g';
+    }();
+    if (!force_general) {
+        const int rc = launch_counter_dense(log, req, out, st);
+        if (rc != AGN_ENOTSUP) return rc;
+    }
     const bool sparse = log.oc_mask || req.R_mask || req.sct_mask || out.lastct_mask;
     return sparse ? dispatch<true>(log, req, out, st) : dispatch<false>(log, req, out, st);
 }

@@ -1,0 +1,250 @@
+// mat_counter_dense.hip — the counter_pn fast path for dense clocks, D <= 8
+// (BASELINE cfg1/cfg2 shapes): the same semantics as k_counter (filter.hpp +
+// mat_counter.hip), specialised where the general kernel pays for
+// generality:
+//   * the read clock R and SCT are wave-uniform: explicit noalias kernel
+//     arguments + readfirstlane keep them in SGPRs (s_load, no VGPRs);
+//   * no presence masks (every DC present), so "+1 encoding" and per-DC
+//     branches disappear; each OpSSCommit row is loaded with 16-byte loads;
+//   * cold (SCT = ignore) and warm reads run separate loop bodies, so the
+//     cold body does one D-wide compare per op, exactly the reference's
+//     VC compare count;
+//   * the i64 effect sum is reduced with DPP row ops + 4 readlanes.
+// HBM bytes per op: 8*D + 8; per key: 8 + 16*D + 32.
+#include "common.hpp"
+
+namespace agn {
+namespace {
+
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v, int ctrl_id) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    switch (ctrl_id) {
+        case 0:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0xB1, 0xF, 0xF, false);
+            break;
+        case 1:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0x4E, 0xF, 0xF, false);
+            break;
+        case 2:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0x141, 0xF, 0xF, false);  // row_half_mirror
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0x141, 0xF, 0xF, false);
+            break;
+        default:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0x140, 0xF, 0xF, false);  // row_mirror
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0x140, 0xF, 0xF, false);
+            break;
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Full-wave i64 sum: 4 DPP steps make every 16-lane row uniform, then the 4
+// row totals are read into SGPRs.
+__device__ __forceinline__ int64_t wave_sum_dpp(int64_t x) {
+    uint64_t v = (uint64_t)x;
+    v += dpp_u64(v, 0);
+    v += dpp_u64(v, 1);
+    v += dpp_u64(v, 2);
+    v += dpp_u64(v, 3);
+    uint64_t t = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, r * 16);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), r * 16);
+        t += ((uint64_t)hi << 32) | lo;
+    }
+    return (int64_t)t;
+}
+
+template <int D>
+__device__ __forceinline__ void load_row(const uint64_t *__restrict__ p, uint64_t (&o)[D]) {
+    if constexpr (D % 2 == 0) {
+        const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(p);
+#pragma unroll
+        for (int j = 0; j < D / 2; ++j) {
+            const ulonglong2 x = q[j];
+            o[2 * j] = x.x;
+            o[2 * j + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) o[j] = p[j];
+    }
+}
+
+struct DenseArgs {
+    uint64_t n_req;
+    uint32_t req_type;
+    uint32_t _pad;
+};
+
+template <int D, bool WARM>
+__device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
+                                         const int64_t *__restrict__ eff,
+                                         const uint64_t *__restrict__ txid, uint64_t txr,
+                                         uint64_t off, uint64_t n, const uint64_t (&r)[D],
+                                         const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum,
+                                         uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+    const int lane = lane_id();
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        const uint64_t pos = b + (uint64_t)lane;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);  // in-bounds for idle lanes
+        uint64_t o[D];
+        load_row<D>(oc + e * D, o);
+        const int64_t ev = eff[e];
+        bool okR = true, leS = true;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            okR = okR && (o[j] <= r[j]);
+            if (WARM) leS = leS && (o[j] <= s[j]);
+        }
+        bool nip = WARM ? !leS : true;  // belongs_to_snapshot_op (ignore -> true)
+        if (txid != nullptr) nip = nip || (txid[e] == txr);
+        const bool incl = valid && nip && okR;
+        const bool excl = valid && nip && !okR;
+        if (first_excl < 0) {
+            const uint64_t bx = ballot(excl);
+            if (bx) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(bx);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) ct[j] = (incl && o[j] > ct[j]) ? o[j] : ct[j];
+        const bool bad = incl && ev == AGN_EFFECT_INVALID;
+        cnt += (uint32_t)__builtin_popcountll(ballot(incl));
+        if (first_err < 0) {
+            const uint64_t be = ballot(bad);
+            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+        }
+        sum += (incl && !bad) ? ev : 0;
+    }
+}
+
+// ANY_WARM = false when the batch has no SCT at all (cold reads): the SCT
+// registers and the warm loop body are compiled out (SGPR pressure).
+template <int D, bool ANY_WARM>
+__global__ __launch_bounds__(256) void k_counter_dense(
+    DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
+    const uint8_t *__restrict__ key_type, const uint64_t *__restrict__ oc,
+    const uint32_t *__restrict__ op_id, const int64_t *__restrict__ eff,
+    const uint64_t *__restrict__ log_txid, const uint64_t *__restrict__ R,
+    const uint64_t *__restrict__ sct, const uint8_t *__restrict__ sct_ignore,
+    const uint64_t *__restrict__ req_txid, const int64_t *__restrict__ base_value,
+    int64_t *__restrict__ o_value, int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
+    uint32_t *__restrict__ o_err) {
+    constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
+    constexpr int V = DCP;                                          // op slots per lane
+    __shared__ uint64_t stage[4][DCP][AGN_WAVE];
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint64_t nw = (uint64_t)gridDim.x * 4u;
+
+    for (uint64_t ii = (uint64_t)blockIdx.x * 4u + (uint64_t)w; ii < a.n_req; ii += nw) {
+        const uint64_t i = uniform_u64(ii);
+        const uint64_t key = keys ? uniform_u64(keys[i]) : i;
+        const uint64_t off = uniform_u64(key_off[key]);
+        const uint64_t n = uniform_u64(key_off[key + 1]) - off;
+        if (n != 0 && key_type != nullptr && key_type[key] != (uint8_t)a.req_type) {
+            if (lane == 0) {  // erlang:error(corrupted_ops_cache)
+                o_flags[i] = AGN_F_ERR_CORRUPTED;
+                o_err[i] = 0xffffffffu;
+            }
+            continue;
+        }
+        uint64_t r[D], s[D], ct[D];
+        const bool sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sct_ignore[i]);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            r[j] = uniform_u64(R[i * D + j]);
+            s[j] = sct_ign ? 0ull : uniform_u64(sct[i * D + j]);
+            ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
+        }
+        const uint64_t txr = req_txid ? uniform_u64(req_txid[i]) : 0ull;
+        const uint64_t *tx = (txr != 0ull) ? log_txid : nullptr;
+        int64_t sum = 0, first_excl = -1, first_err = -1;
+        uint32_t cnt = 0;
+        if (!ANY_WARM || sct_ign)
+            scan_key<D, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl, first_err);
+        else
+            scan_key<D, ANY_WARM>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                  first_err);
+
+        const int64_t total = wave_sum_dpp(sum);
+        // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots
+        // of one DC -> xor-shuffle across the 64/DCP lanes that share it
+#pragma unroll
+        for (int j = 0; j < D; ++j) stage[w][j][lane] = ct[j];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int c = lane % DCP, g = lane / DCP;
+        uint64_t m = 0;
+        if (c < D) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) m = umax64(m, stage[w][c][g * V + v]);
+        }
+#pragma unroll
+        for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
+        const bool ct_ign = sct_ign && cnt == 0u;
+        if (g == 0 && c < D) o_lastct[i * D + (uint64_t)c] = ct_ign ? 0ull : m;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+
+        if (lane == 0) {
+            int64_t hole;
+            if (first_excl >= 0) hole = (int64_t)op_id[off + (uint64_t)first_excl] - 1;
+            else hole = n ? (int64_t)op_id[off + n - 1] : 0;  // get_first_id (:49-63)
+            uint32_t fl = 0;
+            if (cnt) fl |= AGN_F_NEWSS;
+            if (ct_ign) fl |= AGN_F_CT_IGNORE;
+            if (first_err >= 0) fl |= AGN_F_ERR_UNEXPECTED;
+            const int64_t base = base_value ? base_value[i] : 0;
+            o_value[i] = (int64_t)((uint64_t)base + (uint64_t)total);
+            o_hole[i] = hole;
+            o_count[i] = cnt;
+            o_flags[i] = fl;
+            o_err[i] = first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
+        }
+    }
+}
+
+template <int D>
+int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
+                 hipStream_t st) {
+    DenseArgs a{req.n_req, req.req_type, 0};
+    const unsigned blocks = grid_for(req.n_req, 4, 256u * 16u);
+    if (req.sct)
+        hipLaunchKernelGGL((k_counter_dense<D, true>), dim3(blocks), dim3(256), 0, st, a,
+                           req.keys, log.key_off, log.key_type, log.oc, log.op_id, log.eff,
+                           log.txid, req.R, req.sct, req.sct_ignore, req.txid, req.base_value,
+                           out.value, out.hole, out.lastct, out.count, out.flags, out.err_pos);
+    else
+        hipLaunchKernelGGL((k_counter_dense<D, false>), dim3(blocks), dim3(256), 0, st, a,
+                           req.keys, log.key_off, log.key_type, log.oc, log.op_id, log.eff,
+                           log.txid, req.R, req.sct, req.sct_ignore, req.txid, req.base_value,
+                           out.value, out.hole, out.lastct, out.count, out.flags, out.err_pos);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+}  // namespace
+
+// Dense fast path applies when every clock is dense and D <= 8; returns
+// AGN_ENOTSUP otherwise so the caller uses the general kernel.
+int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
+                         hipStream_t st) {
+    if (log.oc_mask || req.R_mask || req.sct_mask || out.lastct_mask) return AGN_ENOTSUP;
+    switch (log.n_dcs) {
+        case 1: return launch_dense<1>(log, req, out, st);
+        case 2: return launch_dense<2>(log, req, out, st);
+        case 3: return launch_dense<3>(log, req, out, st);
+        case 4: return launch_dense<4>(log, req, out, st);
+        case 5: return launch_dense<5>(log, req, out, st);
+        case 6: return launch_dense<6>(log, req, out, st);
+        case 7: return launch_dense<7>(log, req, out, st);
+        case 8: return launch_dense<8>(log, req, out, st);
+        default: return AGN_ENOTSUP;
+    }
+}
+
+}  // namespace agn

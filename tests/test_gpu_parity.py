@@ -67,8 +67,20 @@ for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
             DIFF.append((crdt, D, sparse))
 
 
+@pytest.fixture(params=["auto", "general"])
+def counter_impl(request, monkeypatch):
+    """Run counter cases through the dense fast path (auto) and the general kernel."""
+    if request.param == "general":
+        monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
+    else:
+        monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("crdt,D,sparse", DIFF)
-def test_random_vs_oracle(eng, oracle_lib, crdt, D, sparse):
+def test_random_vs_oracle(eng, oracle_lib, crdt, D, sparse, counter_impl):
+    if crdt != _abi.COUNTER_PN and counter_impl == "general":
+        pytest.skip("impl switch only applies to counter_pn")
     K = 300 if D <= 64 else 120
     nmax = 150 if D <= 16 else 70
     log, req, cap = random_case(7919 * crdt + 31 * D + sparse, crdt, K, D, nmax, sparse=sparse,
@@ -85,7 +97,7 @@ def test_random_vs_oracle(eng, oracle_lib, crdt, D, sparse):
     assert not bad, bad[:10]
 
 
-def test_long_keys_vs_oracle(eng, oracle_lib):
+def test_long_keys_vs_oracle(eng, oracle_lib, counter_impl):
     """Keys far longer than a wave (1000+ ops, like large_list_test) and
     set_aw state that forces table compaction."""
     for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
