@@ -11,6 +11,8 @@
 //     VC compare count;
 //   * the i64 effect sum is reduced with DPP row ops + 4 readlanes.
 // HBM bytes per op: 8*D + 8; per key: 8 + 16*D + 32.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace agn {
@@ -57,19 +59,29 @@ __device__ __forceinline__ int64_t wave_sum_dpp(int64_t x) {
     return (int64_t)t;
 }
 
-template <int D>
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT, class T>
+__device__ __forceinline__ T ld(const T *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// One OpSSCommit row; 16-byte loads when the row is 16-byte aligned (D even).
+// NT: non-temporal (streamed once; keeps the log from thrashing L2/MALL).
+template <int D, bool NT>
 __device__ __forceinline__ void load_row(const uint64_t *__restrict__ p, uint64_t (&o)[D]) {
     if constexpr (D % 2 == 0) {
-        const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(p);
+        const u64x2 *q = reinterpret_cast<const u64x2 *>(p);
 #pragma unroll
         for (int j = 0; j < D / 2; ++j) {
-            const ulonglong2 x = q[j];
+            const u64x2 x = ld<NT>(q + j);
             o[2 * j] = x.x;
             o[2 * j + 1] = x.y;
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < D; ++j) o[j] = p[j];
+        for (int j = 0; j < D; ++j) o[j] = ld<NT>(p + j);
     }
 }
 
@@ -79,21 +91,32 @@ struct DenseArgs {
     uint32_t _pad;
 };
 
-template <int D, bool WARM>
+// Process the key's ops in chunks of 64 (lane = op).  `pre` holds the first
+// chunk's row + effect when the caller prefetched them (software pipelining
+// across keys); later chunks are loaded here.
+template <int D, bool WARM, bool NT>
 __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
                                          const int64_t *__restrict__ eff,
                                          const uint64_t *__restrict__ txid, uint64_t txr,
                                          uint64_t off, uint64_t n, const uint64_t (&r)[D],
                                          const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum,
-                                         uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+                                         uint32_t &cnt, int64_t &first_excl, int64_t &first_err,
+                                         const uint64_t (*pre_o)[D], int64_t pre_ev) {
     const int lane = lane_id();
     for (uint64_t b = 0; b < n; b += AGN_WAVE) {
         const uint64_t pos = b + (uint64_t)lane;
         const bool valid = pos < n;
         const uint64_t e = off + (valid ? pos : 0ull);  // in-bounds for idle lanes
         uint64_t o[D];
-        load_row<D>(oc + e * D, o);
-        const int64_t ev = eff[e];
+        int64_t ev;
+        if (b == 0 && pre_o != nullptr) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) o[j] = (*pre_o)[j];
+            ev = pre_ev;
+        } else {
+            load_row<D, NT>(oc + e * D, o);
+            ev = ld<NT>(eff + e);
+        }
         bool okR = true, leS = true;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
@@ -122,7 +145,10 @@ __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
 
 // ANY_WARM = false when the batch has no SCT at all (cold reads): the SCT
 // registers and the warm loop body are compiled out (SGPR pressure).
-template <int D, bool ANY_WARM>
+// VAR: 0 = plain; 1 = prefetch the next key's first 64 rows + effects before
+// reducing the current key (keeps HBM requests in flight across the per-key
+// reduction); 2 = 1 + non-temporal streaming loads.
+template <int D, bool ANY_WARM, int VAR>
 __global__ __launch_bounds__(256) void k_counter_dense(
     DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
     const uint8_t *__restrict__ key_type, const uint64_t *__restrict__ oc,
@@ -133,6 +159,7 @@ __global__ __launch_bounds__(256) void k_counter_dense(
     int64_t *__restrict__ o_value, int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
     uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
     uint32_t *__restrict__ o_err) {
+    constexpr bool PF = VAR >= 1, NT = VAR >= 2;
     constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
     constexpr int V = DCP;                                          // op slots per lane
     __shared__ uint64_t stage[4][DCP][AGN_WAVE];
@@ -140,12 +167,40 @@ __global__ __launch_bounds__(256) void k_counter_dense(
     const int w = threadIdx.x >> 6;
     const uint64_t nw = (uint64_t)gridDim.x * 4u;
 
-    for (uint64_t ii = (uint64_t)blockIdx.x * 4u + (uint64_t)w; ii < a.n_req; ii += nw) {
-        const uint64_t i = uniform_u64(ii);
-        const uint64_t key = keys ? uniform_u64(keys[i]) : i;
-        const uint64_t off = uniform_u64(key_off[key]);
-        const uint64_t n = uniform_u64(key_off[key + 1]) - off;
-        if (n != 0 && key_type != nullptr && key_type[key] != (uint8_t)a.req_type) {
+    // key meta (uniform) + first-chunk rows of the key this wave handles next
+    auto meta = [&](uint64_t i, uint64_t &key, uint64_t &off, uint64_t &n) {
+        key = keys ? uniform_u64(keys[i]) : i;
+        off = uniform_u64(key_off[key]);
+        n = uniform_u64(key_off[key + 1]) - off;
+    };
+    uint64_t p_o[D];
+    int64_t p_ev = 0;
+    uint64_t i = uniform_u64((uint64_t)blockIdx.x * 4u + (uint64_t)w);
+    uint64_t key = 0, off = 0, n = 0;
+    if (i < a.n_req) {
+        meta(i, key, off, n);
+        if (PF && n) {
+            const uint64_t e = off + ((uint64_t)lane < n ? (uint64_t)lane : 0ull);
+            load_row<D, NT>(oc + e * D, p_o);
+            p_ev = ld<NT>(eff + e);
+        }
+    }
+    for (; i < a.n_req; i += nw) {
+        uint64_t c_o[D];
+        const int64_t c_ev = p_ev;
+#pragma unroll
+        for (int j = 0; j < D; ++j) c_o[j] = p_o[j];
+        const uint64_t c_key = key, c_off = off, c_n = n;
+        const uint64_t inext = i + nw;
+        if (inext < a.n_req) {
+            meta(inext, key, off, n);
+            if (PF && n) {
+                const uint64_t e = off + ((uint64_t)lane < n ? (uint64_t)lane : 0ull);
+                load_row<D, NT>(oc + e * D, p_o);
+                p_ev = ld<NT>(eff + e);
+            }
+        }
+        if (c_n != 0 && key_type != nullptr && key_type[c_key] != (uint8_t)a.req_type) {
             if (lane == 0) {  // erlang:error(corrupted_ops_cache)
                 o_flags[i] = AGN_F_ERR_CORRUPTED;
                 o_err[i] = 0xffffffffu;
@@ -164,11 +219,13 @@ __global__ __launch_bounds__(256) void k_counter_dense(
         const uint64_t *tx = (txr != 0ull) ? log_txid : nullptr;
         int64_t sum = 0, first_excl = -1, first_err = -1;
         uint32_t cnt = 0;
+        const uint64_t(*pre)[D] = PF ? &c_o : nullptr;
         if (!ANY_WARM || sct_ign)
-            scan_key<D, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl, first_err);
+            scan_key<D, false, NT>(oc, eff, tx, txr, c_off, c_n, r, s, ct, sum, cnt, first_excl,
+                                   first_err, pre, c_ev);
         else
-            scan_key<D, ANY_WARM>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                                  first_err);
+            scan_key<D, ANY_WARM, NT>(oc, eff, tx, txr, c_off, c_n, r, s, ct, sum, cnt,
+                                      first_excl, first_err, pre, c_ev);
 
         const int64_t total = wave_sum_dpp(sum);
         // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots
@@ -192,8 +249,8 @@ __global__ __launch_bounds__(256) void k_counter_dense(
 
         if (lane == 0) {
             int64_t hole;
-            if (first_excl >= 0) hole = (int64_t)op_id[off + (uint64_t)first_excl] - 1;
-            else hole = n ? (int64_t)op_id[off + n - 1] : 0;  // get_first_id (:49-63)
+            if (first_excl >= 0) hole = (int64_t)op_id[c_off + (uint64_t)first_excl] - 1;
+            else hole = c_n ? (int64_t)op_id[c_off + c_n - 1] : 0;  // get_first_id (:49-63)
             uint32_t fl = 0;
             if (cnt) fl |= AGN_F_NEWSS;
             if (ct_ign) fl |= AGN_F_CT_IGNORE;
@@ -203,28 +260,45 @@ __global__ __launch_bounds__(256) void k_counter_dense(
             o_hole[i] = hole;
             o_count[i] = cnt;
             o_flags[i] = fl;
-            o_err[i] = first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
+            o_err[i] = first_err >= 0 ? (uint32_t)(c_off + (uint64_t)first_err) : 0xffffffffu;
         }
     }
 }
 
-template <int D>
-int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
-                 hipStream_t st) {
+template <int D, int VAR>
+int launch_dense_var(const agn_log &log, const agn_read &req, const agn_result &out,
+                     hipStream_t st) {
     DenseArgs a{req.n_req, req.req_type, 0};
     const unsigned blocks = grid_for(req.n_req, 4, 256u * 16u);
     if (req.sct)
-        hipLaunchKernelGGL((k_counter_dense<D, true>), dim3(blocks), dim3(256), 0, st, a,
+        hipLaunchKernelGGL((k_counter_dense<D, true, VAR>), dim3(blocks), dim3(256), 0, st, a,
                            req.keys, log.key_off, log.key_type, log.oc, log.op_id, log.eff,
                            log.txid, req.R, req.sct, req.sct_ignore, req.txid, req.base_value,
                            out.value, out.hole, out.lastct, out.count, out.flags, out.err_pos);
     else
-        hipLaunchKernelGGL((k_counter_dense<D, false>), dim3(blocks), dim3(256), 0, st, a,
+        hipLaunchKernelGGL((k_counter_dense<D, false, VAR>), dim3(blocks), dim3(256), 0, st, a,
                            req.keys, log.key_off, log.key_type, log.oc, log.op_id, log.eff,
                            log.txid, req.R, req.sct, req.sct_ignore, req.txid, req.base_value,
                            out.value, out.hole, out.lastct, out.count, out.flags, out.err_pos);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
+}
+
+// AGN_COUNTER_VARIANT=0|1|2 selects the pipeline variant (A/B); default 1.
+int dense_variant() {
+    const char *v = getenv("AGN_COUNTER_VARIANT");
+    if (v && v[0] >= '0' && v[0] <= '2') return v[0] - '0';
+    return 1;
+}
+
+template <int D>
+int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
+                 hipStream_t st) {
+    switch (dense_variant()) {
+        case 0: return launch_dense_var<D, 0>(log, req, out, st);
+        case 2: return launch_dense_var<D, 2>(log, req, out, st);
+        default: return launch_dense_var<D, 1>(log, req, out, st);
+    }
 }
 
 }  // namespace

@@ -15,15 +15,18 @@ eng = Engine(0)
 cfg = _abi.AgnGenCfg(crdt_type=1, n_dcs=8, n_keys=keys, ops_per_key=64, n_elems=0,
                      seed=20250113, key_base=0, key_stride=1, warm=0)
 dl, dr = eng.gen_dev(cfg)
-res = {v: eng.alloc_result(keys, 8, sparse=False) for v in ("dense", "general")}
+VARS = {"v0": ("0", None), "v1_pf": ("1", None), "v2_pf_nt": ("2", None), "general": (None, "general")}
+res = {v: eng.alloc_result(keys, 8, sparse=False) for v in VARS}
 sp = torch.cuda.current_stream().cuda_stream
 times = {v: [] for v in res}
 for rnd in range(12):
     for v in res:
-        if v == "general":
-            os.environ["AGN_COUNTER_IMPL"] = "general"
-        else:
-            os.environ.pop("AGN_COUNTER_IMPL", None)
+        var, impl = VARS[v]
+        for k, x in (("AGN_COUNTER_VARIANT", var), ("AGN_COUNTER_IMPL", impl)):
+            if x is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = x
         b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b.record()
         eng.materialize(dl, dr, res[v], stream=sp)
@@ -32,9 +35,13 @@ for rnd in range(12):
         if rnd >= 2:
             times[v].append(b.elapsed_time(e))
 os.environ.pop("AGN_COUNTER_IMPL", None)
-a, g = eng.fetch_result(res["dense"]), eng.fetch_result(res["general"])
-same = all(np.array_equal(getattr(a, f), getattr(g, f)) for f in
-           ("value", "hole", "lastct", "count", "flags", "err_pos"))
+os.environ.pop("AGN_COUNTER_VARIANT", None)
+ref = eng.fetch_result(res["general"])
+same = {}
+for v in res:
+    got = eng.fetch_result(res[v])
+    same[v] = all(np.array_equal(getattr(got, f), getattr(ref, f)) for f in
+                  ("value", "hole", "lastct", "count", "flags", "err_pos"))
 byts = keys * 64 * 72 + keys * (8 + 16 * 8 + 32)
 for v, t in times.items():
     ms = float(np.median(t))
