@@ -6,19 +6,32 @@
 //   set_aw      entry {Elem, Add, Rem}: Tokens(Elem) := (Tokens -- Rem) ++ Add
 //   register_mv entry {V, Tok, Ovr}: drop tokens in Ovr, insert_sorted({V, Tok})
 //               entry {reset, Ovr}: drop tokens in Ovr
-// applied oldest first.  Sequentially, a token t added at position p (or
-// present in the base snapshot, p = -1) survives iff no INCLUDED op at a
-// position q > p removes it (within one entry the removal happens before the
-// add).  The kernel evaluates exactly that rule in one streaming pass, in
-// position order, with an LDS token table per wave:
-//   per iteration of OPI ops: (1) insert every included add as a candidate
-//   {tok, tag, ord = B + p}; (2) every included removal (t, q) kills the
-//   candidate t if q + B > ord (set_aw: and the elem matches).
-// Removals of tokens added later are ignored (q < p), which is what the
-// sequential fold does.  Dead candidates are tombstones; the table is
-// compacted when 3/4 full (the live state, not the log length, bounds it).
-// Output order: set_aw (elem, add order), register_mv (value, token) — the
-// order the sequential fold produces; bitonic-sorted in LDS per key.
+// applied oldest first.  Sequentially, the pair added at position p (or base
+// pair, p < 0) survives iff no INCLUDED entry at a position q > p removes its
+// token (set_aw: under the same elem); inside one entry the removal happens
+// before the add.  Every pair is judged on its own, so repeated tokens keep
+// the fold's multiset semantics.
+//
+// Kernel structure (one wave per key, 4 independent waves per block):
+//   * the key is processed in chunks of 64 log entries (lane = entry for the
+//     per-entry fields, LPO lanes x DPL DCs per op for the clock rows);
+//   * the snapshot filter streams the OpSSCommit rows through a two-deep
+//     register ring: the rows of sub-iteration j+1 (and the next chunk's side
+//     fields) are in flight while sub-iteration j is compared, and every
+//     prefetch is unconditional (clamped address) so the compiler's counted
+//     vmcnt waits stay exact;
+//   * per chunk, the entry fields (tag, add token, removal range, op id) and
+//     the chunk's removal tokens (up to RB*64, prefetched before the filter)
+//     are resolved against an LDS candidate list: included adds are appended
+//     in position order ({tok, tag, ord}), hashed into per-bucket chains; each
+//     included removal token then walks its chain and marks DEAD every
+//     candidate with that token (set_aw: and elem) whose ord is older;
+//   * the list is compacted in place when full; a key whose live state does
+//     not fit CAP - 64 slots is pushed to a worklist and redone by the same
+//     kernel with a 4096-slot table (one wave per block), which flags
+//     AGN_F_ERR_CAPACITY only beyond that;
+//   * live pairs are bitonic-sorted in LDS into the fold's order: set_aw
+//     (elem, add order), register_mv (value, token).
 //
 // HBM bytes per entry: 8*D (OpSSCommit) + 4 (op_id) + 4 (tag) + 8 (add_tok)
 // + 4 (rem_off) + 8 per removed token; plus 12 per live output pair.
@@ -28,83 +41,81 @@ namespace agn {
 namespace {
 
 constexpr uint32_t DEAD = 0x80000000u;
+constexpr uint32_t NIL = 0xffffffffu;
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 template <int CAP>
-struct TagLds {
+struct CandLds {
     uint64_t tok[CAP];
     uint32_t tag[CAP];
-    uint32_t ord[CAP];
-    // sort / compaction buffer; also aliased as the LastOpCt stage at the end
-    uint64_t btok[CAP];
-    uint32_t btag[CAP];
-    uint32_t bord[CAP];
+    uint32_t ord[CAP];   // B + position (base pairs: index < B); DEAD bit
+    uint32_t nxt[CAP];   // hash chain
+    uint32_t head[2 * CAP];
 };
 
 template <int CAP>
-__device__ __forceinline__ uint32_t hslot(uint64_t t) {
-    constexpr int LOG = __builtin_ctz(CAP);
+__device__ __forceinline__ uint32_t hbucket(uint64_t t) {
+    constexpr int LOG = __builtin_ctz(2 * CAP);
     return (uint32_t)((t * 0x9E3779B97F4A7C15ull) >> (64 - LOG));
 }
 
-template <int CAP>
-__device__ __forceinline__ void tab_insert(TagLds<CAP> &L, uint64_t t, uint32_t tag, uint32_t ord) {
-    uint32_t h = hslot<CAP>(t);
-    for (int probe = 0; probe < CAP; ++probe) {
-        const uint64_t prev = atomicCAS((unsigned long long *)&L.tok[h], 0ull,
-                                        (unsigned long long)t);
-        if (prev == 0ull || prev == t) {
-            L.tag[h] = tag;
-            L.ord[h] = ord;  // a repeated token: the later add wins
-            return;
-        }
-        h = (h + 1u) & (CAP - 1);
-    }
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint64_t lanes_below() {
+    const int lane = lane_id();
+    return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
 template <int CAP>
-__device__ __forceinline__ int tab_find(const TagLds<CAP> &L, uint64_t t) {
-    uint32_t h = hslot<CAP>(t);
-    for (int probe = 0; probe < CAP; ++probe) {
-        const uint64_t k = L.tok[h];
-        if (k == t) return (int)h;
-        if (k == 0ull) return -1;
-        h = (h + 1u) & (CAP - 1);
-    }
-    return -1;
+__device__ __forceinline__ void heads_clear(CandLds<CAP> &L) {
+    for (int s = lane_id(); s < 2 * CAP; s += AGN_WAVE) L.head[s] = NIL;
+    wave_sync();
 }
 
-// Gather live slots of the table into the buffer (stable in slot order);
-// returns the number gathered (wave-uniform).
 template <int CAP>
-__device__ __forceinline__ uint32_t gather_live(TagLds<CAP> &L, int lane) {
+__device__ __forceinline__ void link(CandLds<CAP> &L, uint32_t s, uint64_t t) {
+    const uint32_t prev = atomicExch(&L.head[hbucket<CAP>(t)], s);
+    L.nxt[s] = prev;
+}
+
+// Stable in-place compaction of the live candidates [0, used); returns the
+// live count.  With relink, the hash chains are rebuilt.
+template <int CAP>
+__device__ __forceinline__ uint32_t compact(CandLds<CAP> &L, uint32_t used, bool relink) {
+    const int lane = lane_id();
+    const uint64_t lt = lanes_below();
     uint32_t n = 0;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int s0 = 0; s0 < CAP; s0 += AGN_WAVE) {
-        const int s = s0 + lane;
-        const uint64_t k = L.tok[s];
-        const bool live = k != 0ull && !(L.ord[s] & DEAD);
+    for (uint32_t s0 = 0; s0 < used; s0 += AGN_WAVE) {
+        const uint32_t s = s0 + (uint32_t)lane;
+        uint64_t t = 0;
+        uint32_t g = 0, o = DEAD;
+        if (s < used) {
+            t = L.tok[s];
+            g = L.tag[s];
+            o = L.ord[s];
+        }
+        const bool live = !(o & DEAD);
         const uint64_t m = ballot(live);
+        wave_sync();  // every read of this chunk before any write
         if (live) {
-            const uint32_t at = n + (uint32_t)__builtin_popcountll(m & lt);
-            L.btok[at] = k;
-            L.btag[at] = L.tag[s];
-            L.bord[at] = L.ord[s];
+            const uint32_t d = n + (uint32_t)__builtin_popcountll(m & lt);
+            L.tok[d] = t;
+            L.tag[d] = g;
+            L.ord[d] = o;
         }
         n += (uint32_t)__builtin_popcountll(m);
+        wave_sync();
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    if (relink) {
+        heads_clear<CAP>(L);
+        for (uint32_t s = lane; s < n; s += AGN_WAVE) link<CAP>(L, s, L.tok[s]);
+        wave_sync();
+    }
     return n;
-}
-
-template <int CAP>
-__device__ __forceinline__ void tab_clear(TagLds<CAP> &L, int lane) {
-    for (int s = lane; s < CAP; s += AGN_WAVE) {
-        L.tok[s] = 0ull;
-        L.ord[s] = 0u;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
 }
 
 // (tag, ord) for set_aw, (tag, tok) for register_mv
@@ -117,55 +128,103 @@ __device__ __forceinline__ bool key_less(uint32_t ta, uint64_t ka, uint32_t oa, 
 }
 
 template <bool SET, int CAP>
-__device__ __forceinline__ void bitonic(TagLds<CAP> &L, uint32_t n, int lane) {
+__device__ __forceinline__ void bitonic(CandLds<CAP> &L, uint32_t n) {
+    const int lane = lane_id();
     uint32_t M = 1;
     while (M < n) M <<= 1;
     for (uint32_t s = n + lane; s < M; s += AGN_WAVE) {  // pad with +inf
-        L.btag[s] = 0xffffffffu;
-        L.btok[s] = ~0ull;
-        L.bord[s] = 0xffffffffu;
+        L.tag[s] = 0xffffffffu;
+        L.tok[s] = ~0ull;
+        L.ord[s] = 0xffffffffu;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     for (uint32_t k = 2; k <= M; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t t = lane; t < (M >> 1); t += AGN_WAVE) {
                 const uint32_t a = 2u * j * (t / j) + (t % j);
                 const uint32_t b = a + j;
                 const bool up = (a & k) == 0u;
-                const uint32_t ta = L.btag[a], tb = L.btag[b];
-                const uint64_t ka = L.btok[a], kb = L.btok[b];
-                const uint32_t oa = L.bord[a], ob = L.bord[b];
+                const uint32_t ta = L.tag[a], tb = L.tag[b];
+                const uint64_t ka = L.tok[a], kb = L.tok[b];
+                const uint32_t oa = L.ord[a], ob = L.ord[b];
                 const bool swap = up ? key_less<SET>(tb, kb, ob, ta, ka, oa)
                                      : key_less<SET>(ta, ka, oa, tb, kb, ob);
                 if (swap) {
-                    L.btag[a] = tb; L.btok[a] = kb; L.bord[a] = ob;
-                    L.btag[b] = ta; L.btok[b] = ka; L.bord[b] = oa;
+                    L.tag[a] = tb; L.tok[a] = kb; L.ord[a] = ob;
+                    L.tag[b] = ta; L.tok[b] = ka; L.ord[b] = oa;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            wave_sync();
         }
     }
 }
 
-template <int DPL, int LPO, bool SPARSE, bool SET, int CAP>
-__global__ __launch_bounds__(64) void k_tags(agn_log log, agn_read req, agn_result out) {
-    using F = KeyFilter<DPL, LPO, SPARSE>;
-    static_assert(sizeof(uint64_t) * DPL * AGN_WAVE <= sizeof(uint64_t) * CAP * 2,
-                  "stage must fit the sort buffer");
-    __shared__ TagLds<CAP> L;
-    const int lane = lane_id();
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    constexpr uint32_t HIGH = (uint32_t)(CAP * 3 / 4);
+// One sub-iteration's OpSSCommit slice: DPL DCs of one op per lane.
+template <int DPL, bool SPARSE, bool FULL>
+__device__ __forceinline__ void load_rows(const agn_log &log, uint64_t e, int d0, uint32_t D,
+                                          uint32_t W, uint64_t (&v)[DPL], uint32_t &bits) {
+    if constexpr (FULL) {
+        const u64x2 *q = reinterpret_cast<const u64x2 *>(log.oc + e * D + (uint32_t)d0);
+#pragma unroll
+        for (int j = 0; j < DPL / 2; ++j) {
+            const u64x2 x = q[j];
+            v[2 * j] = x.x;
+            v[2 * j + 1] = x.y;
+        }
+        bits = (1u << DPL) - 1u;
+    } else {
+        bits = chunk_bits<DPL, SPARSE>(log.oc_mask, e, W, d0, D);
+#pragma unroll
+        for (int j = 0; j < DPL; ++j)
+            v[j] = ((bits >> j) & 1u) ? log.oc[e * D + (uint32_t)(d0 + j)] : 0ull;
+    }
+}
 
-    for (uint64_t i = blockIdx.x; i < req.n_req; i += gridDim.x) {
+// Per-entry fields of one 64-entry chunk (lane = entry).
+struct Side {
+    uint32_t tag, ro0, ro1, id, id_prev;
+    uint64_t add;
+};
+
+__device__ __forceinline__ Side load_side(const agn_log &log, uint64_t off, uint64_t n,
+                                          uint64_t c0) {
+    const uint64_t pos = c0 + (uint64_t)lane_id();
+    const uint64_t p = pos < n ? pos : n - 1;  // clamped: unconditional loads
+    const uint64_t e = off + p;
+    Side s;
+    s.tag = log.tag[e];
+    s.add = log.add_tok[e];
+    s.ro0 = log.rem_off[e];
+    s.ro1 = log.rem_off[e + 1];
+    s.id = log.op_id[e];
+    s.id_prev = log.op_id[p ? e - 1 : e];
+    return s;
+}
+
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, int CAP, int WPB, int RB,
+          bool WARM, bool SLOW>
+__global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, agn_result out,
+                                                   uint32_t *wl, uint32_t *wl_n) {
+    using S = Shape<DPL, LPO>;
+    constexpr int OPI = S::OPI;
+    __shared__ CandLds<CAP> Lall[WPB];
+    const int w = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
+    CandLds<CAP> &L = Lall[w];
+    const int lane = lane_id();
+    const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
+    const uint32_t D = log.n_dcs, W = n_words(D);
+    const uint64_t lt = lanes_below();
+    const uint64_t n_items = SLOW ? (uint64_t)uniform_u64(*wl_n) : req.n_req;
+    const uint64_t nw = (uint64_t)gridDim.x * WPB;
+
+    for (uint64_t it = (uint64_t)blockIdx.x * WPB + (uint64_t)w; it < n_items; it += nw) {
+        const uint64_t i = SLOW ? (uint64_t)__builtin_amdgcn_readfirstlane(wl[it]) : it;
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
         const uint64_t off = uniform_u64(log.key_off[key]);
         const uint64_t n = uniform_u64(log.key_off[key + 1]) - off;
 
         if (n != 0 && log.key_type != nullptr && log.key_type[key] != (uint8_t)req.req_type) {
-            if (lane == 0) {
+            if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
                 out.flags[i] = AGN_F_ERR_CORRUPTED;
                 out.err_pos[i] = 0xffffffffu;
                 out.out_n[i] = 0;
@@ -173,106 +232,263 @@ __global__ __launch_bounds__(64) void k_tags(agn_log log, agn_read req, agn_resu
             continue;
         }
 
-        F f;
-        f.init(log, req, i);
-        tab_clear<CAP>(L, lane);
-        bool overflow = false;
+        // ---- read snapshot R, base snapshot time SCT, LastOpCt seed
+        const bool sct_ign = !WARM || req.sct == nullptr || (req.sct_ignore && req.sct_ignore[i]);
+        const uint32_t rbits = chunk_bits<DPL, SPARSE>(req.R_mask, i, W, d0, D);
+        const uint32_t sbits = sct_ign ? 0u : chunk_bits<DPL, SPARSE>(req.sct_mask, i, W, d0, D);
+        uint64_t r[DPL], s[DPL], ct[DPL];
+#pragma unroll
+        for (int j = 0; j < DPL; ++j) {
+            const uint32_t d = (uint32_t)(d0 + j);
+            r[j] = (d < D) ? req.R[i * D + d] : 0ull;
+            s[j] = ((sbits >> j) & 1u) ? req.sct[i * D + d] : 0ull;
+            // LastOpCt starts as SnapshotCommitTime (materialize/4 :94-95);
+            // "+1 encoded" in sparse mode (0 = DC absent from the dict)
+            ct[j] = ((sbits >> j) & 1u) ? (SPARSE ? s[j] + 1ull : s[j]) : 0ull;
+        }
+        const uint64_t txr = req.txid ? uniform_u64(req.txid[i]) : 0ull;
+        const bool use_tx = txr != 0ull && log.txid != nullptr;
 
-        // base snapshot state: candidates with ord = index (< B)
+        // ---- base snapshot state: candidates with ord = index (< B)
+        heads_clear<CAP>(L);
         const uint64_t b0 = req.base_off ? req.base_off[i] : 0ull;
         const uint32_t B = req.base_off ? (uint32_t)(req.base_off[i + 1] - b0) : 0u;
-        if (B > (uint32_t)(CAP / 2)) overflow = true;
-        uint32_t used = overflow ? 0u : B;
-        for (uint32_t x = lane; !overflow && x < B; x += AGN_WAVE)
-            tab_insert<CAP>(L, req.base_tok[b0 + x], req.base_tag[b0 + x], x);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        bool overflow = B > (uint32_t)(CAP - AGN_WAVE);
+        uint32_t used = 0;
+        if (!overflow) {
+            for (uint32_t x = lane; x < B; x += AGN_WAVE) {
+                const uint64_t t = req.base_tok[b0 + x];
+                L.tok[x] = t;
+                L.tag[x] = req.base_tag[b0 + x];
+                L.ord[x] = x;
+                link<CAP>(L, x, t);
+            }
+            used = B;
+        }
+        wave_sync();
 
+        int64_t first_excl = -1, first_err = -1;
         uint32_t cnt = 0;
-        int64_t first_err = -1;
-        for (uint64_t b = 0; b < n; b += F::S::OPI) {
-            bool valid;
-            const bool incl = f.step(log, off, n, b, valid);
-            if (overflow) continue;  // keep the filter outputs exact; state is lost
-            const uint64_t pos = b + (uint64_t)f.slot;
-            const uint64_t e = off + pos;
-            const bool lead = incl && f.sub == 0;
-            uint32_t tag = 0;
-            uint64_t add = 0;
-            bool opstart = false;
-            if (lead) {
-                tag = log.tag[e];
-                add = log.add_tok[e];
-                opstart = (pos == 0) || (log.op_id[e - 1] != log.op_id[e]);
-            }
-            const bool bad = lead && tag == AGN_TAG_INVALID;
-            cnt += (uint32_t)__builtin_popcountll(ballot(lead && opstart));
-            if (first_err < 0) {
-                const uint64_t be = ballot(bad);
-                if (be) first_err = (int64_t)b + (int64_t)(__builtin_ctzll(be) / LPO);
-            }
-            if (first_err >= 0) continue;  // {error, ...}: the state is not returned
 
-            const bool adds = lead && add != 0ull;
-            const uint32_t n_add = (uint32_t)__builtin_popcountll(ballot(adds));
-            if (used + n_add > HIGH) {  // compact: drop tombstones
-                const uint32_t live = gather_live<CAP>(L, lane);
-                tab_clear<CAP>(L, lane);
-                if (live > (uint32_t)(CAP / 2)) {
-                    overflow = true;
-                    continue;
-                }
-                for (uint32_t x = lane; x < live; x += AGN_WAVE)
-                    tab_insert<CAP>(L, L.btok[x], L.btag[x], L.bord[x]);
-                used = live;
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
+        if (n != 0) {
+            Side side = load_side(log, off, n, 0);
+            uint64_t nx[DPL];
+            uint32_t nxbits;
+            {
+                const uint64_t p = (uint64_t)slot < n ? (uint64_t)slot : n - 1;
+                load_rows<DPL, SPARSE, FULL>(log, off + p, d0, D, W, nx, nxbits);
             }
-            // (1) candidates: included adds of this iteration
-            if (adds) tab_insert<CAP>(L, add, tag, B + (uint32_t)pos);
-            used += n_add;
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            // (2) removals (set_aw: Rem of the entry's elem; register_mv: Overridden)
-            if (lead) {
-                const uint32_t r0 = log.rem_off[e], r1 = log.rem_off[e + 1];
-                const uint32_t q = B + (uint32_t)pos;
-                for (uint32_t k = r0; k < r1; ++k) {
-                    const int h = tab_find<CAP>(L, log.rem_tok[k]);
-                    if (h >= 0 && (!SET || L.tag[h] == tag) && q > (L.ord[h] & ~DEAD))
-                        atomicOr(&L.ord[h], DEAD);
+            for (uint64_t c0 = 0; c0 < n; c0 += AGN_WAVE) {
+                const uint64_t left = n - c0;
+                const uint32_t nvalid = left < AGN_WAVE ? (uint32_t)left : (uint32_t)AGN_WAVE;
+                const Side cs = side;
+                // the chunk's removal tokens, first RB*64 of them
+                const uint32_t K0 = __builtin_amdgcn_readfirstlane(cs.ro0);
+                const uint32_t K1 = __builtin_amdgcn_readlane(cs.ro1, nvalid - 1);
+                uint64_t rt[RB];
+#pragma unroll
+                for (int q = 0; q < RB; ++q) rt[q] = 0ull;
+                if (K1 > K0) {  // rem_tok may be empty (NULL) for a log without removals
+#pragma unroll
+                    for (int q = 0; q < RB; ++q) {
+                        const uint32_t k = K0 + (uint32_t)(q * AGN_WAVE + lane);
+                        rt[q] = log.rem_tok[k < K1 ? k : K1 - 1u];
+                    }
                 }
+
+                // ---- snapshot filter over the chunk's sub-iterations
+                const uint32_t nsub = (nvalid + OPI - 1) / OPI;
+                bool incl_e = false;
+                for (uint32_t j = 0; j < nsub; ++j) {
+                    uint64_t o[DPL];
+                    const uint32_t obits0 = nxbits;
+#pragma unroll
+                    for (int x = 0; x < DPL; ++x) o[x] = nx[x];
+                    const uint64_t b = c0 + (uint64_t)j * OPI;
+                    const uint64_t nb = (j + 1 < nsub) ? b + OPI : c0 + AGN_WAVE;
+                    if (j + 1 == nsub) side = load_side(log, off, n, nb < n ? nb : c0);
+                    {
+                        const uint64_t p = nb + (uint64_t)slot;
+                        load_rows<DPL, SPARSE, FULL>(log, off + (p < n ? p : n - 1), d0, D, W,
+                                                     nx, nxbits);
+                    }
+                    const uint64_t pos = b + (uint64_t)slot;
+                    const bool valid = pos < n;
+                    const uint32_t obits = valid ? obits0 : 0u;
+                    bool okR = true, leS = true;
+#pragma unroll
+                    for (int x = 0; x < DPL; ++x) {
+                        if ((obits >> x) & 1u) {
+                            const bool inR = SPARSE ? (((rbits >> x) & 1u) != 0u) : true;
+                            okR = okR && inR && (o[x] <= r[x]);  // DC missing in R -> false
+                            if (WARM) leS = leS && (o[x] <= s[x]);
+                        }
+                    }
+                    if (LPO > 1) {
+                        const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
+                        okR = (ballot(!okR) & grp) == 0ull;
+                        if (WARM) leS = (ballot(!leS) & grp) == 0ull;
+                    }
+                    // belongs_to_snapshot_op(SCT, ...) or (TxId == op.txid)  (:219-220)
+                    bool nip = sct_ign || !leS;
+                    if (use_tx) {
+                        bool txm = valid && sub == 0 && log.txid[off + pos] == txr;
+                        if (LPO > 1) txm = (ballot(txm) >> (slot * LPO)) & 1ull;
+                        nip = nip || txm;
+                    }
+                    const bool incl = valid && nip && okR;
+                    const bool excl = valid && nip && !okR;
+                    if (first_excl < 0) {
+                        const uint64_t bx = ballot(excl && sub == 0);
+                        if (bx) first_excl = (int64_t)b + (int64_t)(__builtin_ctzll(bx) / LPO);
+                    }
+                    if (incl) {
+#pragma unroll
+                        for (int x = 0; x < DPL; ++x)
+                            if ((obits >> x) & 1u)
+                                ct[x] = umax64(ct[x], SPARSE ? o[x] + 1ull : o[x]);
+                    }
+                    // per-op verdict -> lane = entry
+                    const uint64_t bi = ballot(incl && sub == 0);
+                    if ((uint32_t)lane / (uint32_t)OPI == j)
+                        incl_e = (bi >> (((uint32_t)lane % (uint32_t)OPI) * LPO)) & 1ull;
+                }
+
+                // ---- chunk resolution (lane = entry c0 + lane)
+                const uint64_t pos = c0 + (uint64_t)lane;
+                const bool opstart = pos == 0 || cs.id_prev != cs.id;
+                cnt += (uint32_t)__builtin_popcountll(ballot(incl_e && opstart));
+                if (first_err < 0) {
+                    const uint64_t be = ballot(incl_e && cs.tag == AGN_TAG_INVALID);
+                    if (be) first_err = (int64_t)c0 + (int64_t)__builtin_ctzll(be);
+                }
+                if (first_err >= 0 || overflow) continue;  // {error,..} / no state kept
+
+                // (1) candidates: the chunk's included adds, in position order
+                const bool adds = incl_e && cs.add != 0ull;
+                const uint64_t am = ballot(adds);
+                const uint32_t n_add = (uint32_t)__builtin_popcountll(am);
+                if (used + n_add > (uint32_t)CAP) {
+                    used = compact<CAP>(L, used, true);
+                    if (used + n_add > (uint32_t)CAP) {
+                        overflow = true;
+                        continue;
+                    }
+                }
+                if (adds) {
+                    const uint32_t sl = used + (uint32_t)__builtin_popcountll(am & lt);
+                    L.tok[sl] = cs.add;
+                    L.tag[sl] = cs.tag;
+                    L.ord[sl] = B + (uint32_t)pos;
+                    link<CAP>(L, sl, cs.add);
+                }
+                used += n_add;
+                wave_sync();
+
+                // (2) removals: lane = removal token; owner entry by binary
+                // search over the chunk's removal offsets
+                const uint64_t im = ballot(incl_e);
+                for (uint32_t k0 = K0, q = 0; k0 < K1; k0 += AGN_WAVE, ++q) {
+                    const uint32_t k = k0 + (uint32_t)lane;
+                    const bool has = k < K1;
+                    uint64_t t;
+                    if (q < (uint32_t)RB) {
+                        t = rt[0];
+#pragma unroll
+                        for (int z = 1; z < RB; ++z)
+                            if (q == (uint32_t)z) t = rt[z];
+                    } else {
+                        t = has ? log.rem_tok[k] : 0ull;
+                    }
+                    uint32_t sidx = 0;
+#pragma unroll
+                    for (uint32_t st = AGN_WAVE / 2; st > 0; st >>= 1) {
+                        const uint32_t c = sidx + st;
+                        const uint32_t v = (uint32_t)__shfl((int)cs.ro0, (int)(c & 63u));
+                        if (c < nvalid && v <= k) sidx = c;
+                    }
+                    const uint32_t etag = (uint32_t)__shfl((int)cs.tag, (int)sidx);
+                    const bool einc = (im >> sidx) & 1ull;
+                    if (has && einc) {
+                        const uint32_t qpos = B + (uint32_t)(c0 + sidx);
+                        for (uint32_t x = L.head[hbucket<CAP>(t)]; x != NIL; x = L.nxt[x]) {
+                            if (L.tok[x] != t) continue;
+                            if (SET && L.tag[x] != etag) continue;
+                            const uint32_t o = L.ord[x];
+                            if (qpos > (o & ~DEAD)) L.ord[x] = o | DEAD;
+                        }
+                    }
+                }
+                wave_sync();
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
         }
 
-        // live state -> sorted pairs
+        // ---- fast path overflow: hand the key to the 4096-slot pass
+        if (!SLOW && overflow && first_err < 0) {
+            if (lane == 0) {
+                const uint32_t at = atomicAdd(wl_n, 1u);
+                wl[at] = (uint32_t)i;
+            }
+            continue;
+        }
+
+        // ---- live state -> sorted pairs
         uint32_t n_live = 0;
         bool cap_err = overflow;
         const uint64_t o = out.out_off[i];
         if (!overflow && first_err < 0) {
-            n_live = gather_live<CAP>(L, lane);
+            n_live = compact<CAP>(L, used, false);
             if ((uint64_t)n_live > out.out_off[i + 1] - o) {
                 cap_err = true;
             } else {
-                bitonic<SET, CAP>(L, n_live, lane);
+                bitonic<SET, CAP>(L, n_live);
                 for (uint32_t x = lane; x < n_live; x += AGN_WAVE) {
-                    out.out_tag[o + x] = L.btag[x];
-                    out.out_tok[o + x] = L.btok[x];
+                    out.out_tag[o + x] = L.tag[x];
+                    out.out_tok[o + x] = L.tok[x];
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();
 
-        const bool ct_ign = f.sct_ign && cnt == 0u;
-        f.write_ct(reinterpret_cast<uint64_t(*)[AGN_WAVE]>(L.btok), out, i, ct_ign);
+        // ---- LastOpCt: max over the lanes that hold the same DC slice
+#pragma unroll
+        for (int x = LPO; x < AGN_WAVE; x <<= 1) {
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) ct[j] = umax64(ct[j], shfl_xor_u64(ct[j], x));
+        }
+        const bool ct_ign = sct_ign && cnt == 0u;
+        if (slot == 0) {
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) {
+                const uint32_t d = (uint32_t)(d0 + j);
+                if (d < D) {
+                    uint64_t v = ct[j];
+                    if (SPARSE) v = (v && !ct_ign) ? v - 1ull : 0ull;
+                    else if (ct_ign) v = 0ull;
+                    out.lastct[i * D + d] = v;
+                }
+            }
+        }
+        if (SPARSE && out.lastct_mask != nullptr) {
+            uint64_t part = 0;
+            if (slot == 0 && !ct_ign) {
+#pragma unroll
+                for (int j = 0; j < DPL; ++j)
+                    if ((uint32_t)(d0 + j) < D && ct[j] != 0ull)
+                        part |= 1ull << ((uint32_t)(d0 + j) & 63u);
+            }
+            for (uint32_t wd = 0; wd < W; ++wd) {
+                uint64_t v = (((uint32_t)d0 >> 6) == wd) ? part : 0ull;
+#pragma unroll
+                for (int x = 1; x < AGN_WAVE; x <<= 1) v |= shfl_xor_u64(v, x);
+                if (lane == 0) out.lastct_mask[i * W + wd] = v;
+            }
+        }
 
         if (lane == 0) {
             int64_t hole;
-            if (f.first_excl >= 0) hole = (int64_t)log.op_id[off + (uint64_t)f.first_excl] - 1;
-            else hole = n ? (int64_t)log.op_id[off + n - 1] : 0;
+            if (first_excl >= 0) hole = (int64_t)log.op_id[off + (uint64_t)first_excl] - 1;
+            else hole = n ? (int64_t)log.op_id[off + n - 1] : 0;  // get_first_id (:49-63)
             uint32_t fl = 0;
             if (cnt) fl |= AGN_F_NEWSS;
             if (ct_ign) fl |= AGN_F_CT_IGNORE;
@@ -285,25 +501,60 @@ __global__ __launch_bounds__(64) void k_tags(agn_log log, agn_read req, agn_resu
                 first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
             out.out_n[i] = n_live;
         }
-        (void)lt;
     }
 }
 
-constexpr int TAG_CAP = 512;
+constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 4, RBATCH = 2;
 
-template <int DPL, int LPO, bool SPARSE, bool SET>
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM>
 int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
-    const unsigned blocks = grid_for(req.n_req, 1, 256u * 10u * 4u);
-    hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, SET, TAG_CAP>), dim3(blocks), dim3(64), 0,
-                       st, log, req, out);
-    AGN_HIP(hipGetLastError());
-    return AGN_OK;
+    // worklist of keys whose live state overflows the fast table: [0] = count
+    uint32_t *wl = nullptr;
+    AGN_HIP(hipMallocAsync((void **)&wl, (req.n_req + 1) * sizeof(uint32_t), st));
+    int rc = AGN_OK;
+    {
+        hipError_t e = hipMemsetAsync(wl, 0, sizeof(uint32_t), st);
+        const unsigned blocks = grid_for(req.n_req, FAST_WPB, 256u * 8u);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH,
+                                       WARM, false>),
+                               dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, wl + 1,
+                               wl);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM,
+                                       true>),
+                               dim3(256), dim3(64), 0, st, log, req, out, wl + 1, wl);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) rc = fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
+    }
+    const hipError_t ef = hipFreeAsync(wl, st);
+    if (rc == AGN_OK && ef != hipSuccess)
+        rc = fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
+    return rc;
+}
+
+template <int DPL, int LPO, bool SPARSE, bool SET>
+int launch_full(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    const bool warm = req.sct != nullptr;
+    // FULL: dense rows that split exactly into 16-byte loads
+    const bool full = !SPARSE && (DPL % 2 == 0) && log.n_dcs == (uint32_t)(DPL * LPO);
+    if constexpr (!SPARSE && DPL % 2 == 0) {
+        if (full)
+            return warm ? launch_shape<DPL, LPO, false, true, SET, true>(log, req, out, st)
+                        : launch_shape<DPL, LPO, false, true, SET, false>(log, req, out, st);
+    }
+    (void)full;
+    return warm ? launch_shape<DPL, LPO, SPARSE, false, SET, true>(log, req, out, st)
+                : launch_shape<DPL, LPO, SPARSE, false, SET, false>(log, req, out, st);
 }
 
 template <bool SPARSE, bool SET>
 int dispatch(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-#define AGN_L(DPL, LPO) launch_shape<DPL, LPO, SPARSE, SET>(log, req, out, st)
+#define AGN_L(DPL, LPO) launch_full<DPL, LPO, SPARSE, SET>(log, req, out, st)
     AGN_DISPATCH_SHAPES(log.n_dcs, AGN_L)
 #undef AGN_L
 }

@@ -111,6 +111,51 @@ def test_long_keys_vs_oracle(eng, oracle_lib, counter_impl):
         assert not compare(crdt, 8, res_g, res_o, False, req.n_req)
 
 
+def _oracle_vs_gpu(eng, oracle_lib, crdt, D, log, req, sparse=False):
+    from antidote_amd.encode import state_capacity
+    cap = state_capacity(log, req)
+    res_g = eng.materialize_host(log, req, sparse=sparse, cap_off=cap)
+    res_o = alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)
+    ls, rs, os_ = log_struct(log), read_struct(req, sparse=sparse), result_struct(res_o)
+    if not sparse:
+        ls.oc_mask = None
+    assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
+    return res_g, res_o, compare(crdt, D, res_g, res_o, sparse, req.n_req)
+
+
+@pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])
+@pytest.mark.parametrize("D", [8, 16, 64])
+def test_large_live_state_slow_path(eng, oracle_lib, crdt, D):
+    """Live state beyond the fast table (CAP - 64 = 192 pairs): the key is
+    handed to the 4096-slot pass through the device worklist."""
+    log, req, _ = random_case(4242 + crdt + D, crdt, 12, D, 1500, base=0.5, n_elems=600,
+                              empty=0.0, warm=0.3)
+    log.rem_off[:] = 0  # no removals: every included add stays live
+    log.rem_tok = np.zeros(1, np.uint64)
+    res_g, res_o, bad = _oracle_vs_gpu(eng, oracle_lib, crdt, D, log, req)
+    assert not bad, bad[:5]
+    assert int(res_o.out_n.max()) > 256  # the slow path really ran
+
+
+@pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_repeated_tokens(eng, oracle_lib, crdt, sparse):
+    """A token added twice stays twice in the sequential fold (set_aw appends,
+    register_mv insert_sorted); a removal kills every earlier copy only."""
+    D = 5
+    log, req, _ = random_case(77 + crdt + 2 * sparse, crdt, 200, D, 120, base=0.3, sparse=sparse,
+                              warm=0.3, n_elems=4)
+    rng = np.random.default_rng(9)
+    for k in range(len(log.key_off) - 1):
+        a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+        adds = [e for e in range(a, b) if log.add_tok[e] != 0]
+        for j, e in enumerate(adds[1:], 1):
+            if rng.random() < 0.3:
+                log.add_tok[e] = log.add_tok[adds[int(rng.integers(0, j))]]
+    _, _, bad = _oracle_vs_gpu(eng, oracle_lib, crdt, D, log, req, sparse=sparse)
+    assert not bad, bad[:5]
+
+
 def test_empty_batch_and_empty_log(eng):
     log, req, cap = random_case(5, _abi.COUNTER_PN, 10, 4, 0, empty=1.0)
     res = eng.materialize_host(log, req, sparse=False)
