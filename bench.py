@@ -182,6 +182,8 @@ def main():
     bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
+    probe = probe_read_gbs(eng, dl, n_keys * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
+
     gst = None
     if a.gst:
         gst = gst_bench(eng, torch, dist, world, rank, sp)
@@ -219,7 +221,9 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch},
+                         "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch,
+                         "probe_read_GBps": probe,
+                         "frac_of_probe": achieved / probe if probe else None},
             "cpu_baseline": cpu,
             "error_keys": err_keys, "mean_included_ops": float(count.mean()),
             "gen_s": t_gen,
@@ -232,6 +236,29 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def probe_read_gbs(eng, dl, nbytes, sp, torch):
+    """The box's practical HBM read ceiling: tools/libagn_probe.so streams the
+    OpSSCommit array (16-byte coalesced loads, every byte once) on the same
+    stream; reported beside the spec peak so box-to-box HBM variance can be
+    told apart from kernel changes."""
+    path = os.path.join(ROOT, "tools", "libagn_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    lib.agn_probe_read.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    scratch = eng.empty(64)
+    for _ in range(2):
+        lib.agn_probe_read(dl.oc, nbytes, scratch.ptr, sp)
+    b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b.record()
+    for _ in range(5):
+        lib.agn_probe_read(dl.oc, nbytes, scratch.ptr, sp)
+    e.record()
+    torch.cuda.synchronize()
+    scratch.free()
+    return nbytes / (b.elapsed_time(e) / 5 * 1e-3) / 1e9
 
 
 def gst_bench(eng, torch, dist, world, rank, sp):

@@ -15,14 +15,15 @@ eng = Engine(0)
 cfg = _abi.AgnGenCfg(crdt_type=1, n_dcs=8, n_keys=keys, ops_per_key=64, n_elems=0,
                      seed=20250113, key_base=0, key_stride=1, warm=0)
 dl, dr = eng.gen_dev(cfg)
-VARS = {"v0": ("0", None), "v1_pf": ("1", None), "v2_pf_nt": ("2", None), "general": (None, "general")}
+VARS = {"v0w8": ("0", "8", None), "v1w8": ("1", "8", None), "v2w8": ("2", "8", None), "v2w6": ("2", "6", None), "general": (None, None, "general")}
 res = {v: eng.alloc_result(keys, 8, sparse=False) for v in VARS}
 sp = torch.cuda.current_stream().cuda_stream
 times = {v: [] for v in res}
 for rnd in range(12):
     for v in res:
-        var, impl = VARS[v]
-        for k, x in (("AGN_COUNTER_VARIANT", var), ("AGN_COUNTER_IMPL", impl)):
+        var, minw, impl = VARS[v]
+        for k, x in (("AGN_COUNTER_VARIANT", var), ("AGN_COUNTER_MINW", minw),
+                     ("AGN_COUNTER_IMPL", impl)):
             if x is None:
                 os.environ.pop(k, None)
             else:
@@ -34,6 +35,10 @@ for rnd in range(12):
         torch.cuda.synchronize()
         if rnd >= 2:
             times[v].append(b.elapsed_time(e))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import probe_read_gbs  # noqa: E402
+pr = probe_read_gbs(eng, dl, keys * 64 * 8 * 8, sp, torch)
+print(f"probe read ceiling: {pr:.0f} GB/s")
 os.environ.pop("AGN_COUNTER_IMPL", None)
 os.environ.pop("AGN_COUNTER_VARIANT", None)
 ref = eng.fetch_result(res["general"])
@@ -46,5 +51,5 @@ byts = keys * 64 * 72 + keys * (8 + 16 * 8 + 32)
 for v, t in times.items():
     ms = float(np.median(t))
     print(f"{v:8s} median {ms:.3f} ms  min {min(t):.3f}  {byts / ms / 1e6:.0f} GB/s  "
-          f"{keys * 64 / ms / 1e6:.3e} ops/s")
+          f"{keys * 64 / ms / 1e6:.3e} ops/s  {byts / ms / 1e6 / pr:.3f} of probe")
 print("outputs identical:", same)
