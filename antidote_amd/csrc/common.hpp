@@ -59,6 +59,30 @@ inline unsigned grid_for(uint64_t work_items, unsigned items_per_block, unsigned
     return (unsigned)b;
 }
 
+// Grid of exactly one resident round of `kernel` (blocks per CU from the
+// occupancy API x CUs), capped by the work: the streaming kernels grid-stride,
+// so a grid of k.33 rounds would leave its last third of a round running at a
+// third of the chip.  Cached per kernel instantiation.
+template <class K>
+inline unsigned resident_grid(K kernel, unsigned threads, uint64_t work_blocks) {
+    static int per_cu = -1, cus = -1;
+    if (per_cu < 0) {
+        int dev = 0, nb = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, (int)threads, 0) !=
+                hipSuccess || nb < 1 || c < 1) {
+            nb = 2;
+            c = 256;
+        }
+        per_cu = nb;
+        cus = c;
+    }
+    uint64_t b = (uint64_t)per_cu * (uint64_t)cus;
+    if (work_blocks < b) b = work_blocks;
+    return (unsigned)(b < 1 ? 1 : b);
+}
+
 // Launchers (defined in the .hip files).
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t s);

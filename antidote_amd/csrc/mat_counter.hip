@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void k_counter(agn_log log, agn_read req, agn_
 template <int DPL, int LPO, bool SPARSE>
 int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
-    const unsigned blocks = grid_for(req.n_req, 4, 256u * 16u);
+    const unsigned blocks = grid_for(req.n_req, 4, 0x7fffffffu);  // one wave per request
     hipLaunchKernelGGL((k_counter<DPL, LPO, SPARSE>), dim3(blocks), dim3(256), 0, st, log,
                        req, out);
     AGN_HIP(hipGetLastError());

@@ -35,6 +35,8 @@
 //
 // HBM bytes per entry: 8*D (OpSSCommit) + 4 (op_id) + 4 (tag) + 8 (add_tok)
 // + 4 (rem_off) + 8 per removed token; plus 12 per live output pair.
+#include <cstdlib>
+
 #include "filter.hpp"
 
 namespace agn {
@@ -515,7 +517,10 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
     int rc = AGN_OK;
     {
         hipError_t e = hipMemsetAsync(wl, 0, sizeof(uint32_t), st);
-        const unsigned blocks = grid_for(req.n_req, FAST_WPB, 256u * 8u);
+        // one wave per key: the grid is the batch (the wave dispatcher then
+        // overlaps keys; AGN_TAGS_GRID=<blocks> caps it for A/B)
+        const char *ge = getenv("AGN_TAGS_GRID");
+        const unsigned blocks = grid_for(req.n_req, FAST_WPB, ge ? (unsigned)atoi(ge) : 0x7fffffffu);
         if (e == hipSuccess) {
             hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH,
                                        WARM, false>),

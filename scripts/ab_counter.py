@@ -15,14 +15,14 @@ eng = Engine(0)
 cfg = _abi.AgnGenCfg(crdt_type=1, n_dcs=8, n_keys=keys, ops_per_key=64, n_elems=0,
                      seed=20250113, key_base=0, key_stride=1, warm=0)
 dl, dr = eng.gen_dev(cfg)
-VARS = {"v0w8": ("0", "8", None), "v1w8": ("1", "8", None), "v2w8": ("2", "8", None), "v2w6": ("2", "6", None), "general": (None, None, "general")}
+VARS = {"key_w1": ("8", "1", None), "key_w2": ("8", "2", None), "key_w4": ("8", "4", None), "key_w8": ("8", "8", None), "v4g4": ("4", "4", None), "general": (None, None, "general")}
 res = {v: eng.alloc_result(keys, 8, sparse=False) for v in VARS}
 sp = torch.cuda.current_stream().cuda_stream
 times = {v: [] for v in res}
 for rnd in range(12):
     for v in res:
         var, minw, impl = VARS[v]
-        for k, x in (("AGN_COUNTER_VARIANT", var), ("AGN_COUNTER_MINW", minw),
+        for k, x in (("AGN_COUNTER_VARIANT", var), ("AGN_COUNTER_WPB", minw),
                      ("AGN_COUNTER_IMPL", impl)):
             if x is None:
                 os.environ.pop(k, None)
