@@ -76,6 +76,78 @@ __global__ __launch_bounds__(GST_THREADS) void k_gst_min(const uint64_t *__restr
     if (threadIdx.x == 0 && !all_def) atomicMin((unsigned long long *)&o[D], 0ull);
 }
 
+// Column-resident form for D | 512 (D a power of two <= 512, e.g. the cfg5
+// D = 256): thread t owns the DC pair c = 2t mod D of row offset 2t div D,
+// so its column never changes; it streams its band's rows with 16-byte loads
+// (4 rows in flight) into two running minima held in registers.  The
+// RG = 512 / D threads that share a column pair fold through LDS once, and
+// the block issues ONE global atomicMin per column (bands blocks per epoch).
+// Undefined partitions only clear word D (they contribute no clock).
+typedef unsigned long long u64x2g __attribute__((ext_vector_type(2)));
+
+template <bool DEF>
+__global__ __launch_bounds__(GST_THREADS) void k_gst_cols(const uint64_t *__restrict__ clocks,
+                                                          const uint8_t *__restrict__ defined,
+                                                          uint64_t *out, uint32_t D, uint64_t P,
+                                                          uint64_t rows_per_block,
+                                                          uint64_t bands) {
+    __shared__ uint64_t red[2 * GST_THREADS];
+    __shared__ int all_def;
+    const uint32_t t = threadIdx.x;
+    const uint32_t RG = (2u * GST_THREADS) / D;        // rows per block step
+    const uint32_t c = (2u * t) % D, r0 = (2u * t) / D;
+    const uint64_t e = blockIdx.x / bands, band = blockIdx.x % bands;
+    const uint64_t p0 = band * rows_per_block;
+    const uint64_t p1 = p0 + rows_per_block < P ? p0 + rows_per_block : P;
+    if (t == 0) all_def = 1;
+    __syncthreads();
+    uint64_t m0 = ~0ull, m1 = ~0ull;
+    const uint64_t *base = clocks + e * P * D + c;
+    uint64_t p = p0 + r0;
+    for (; p + 3 * RG < p1; p += 4 * RG) {
+        u64x2g v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = *reinterpret_cast<const u64x2g *>(base + (p + (uint64_t)k * RG) * D);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bool ok = true;
+            if (DEF) ok = defined[e * P + p + (uint64_t)k * RG] != 0;
+            if (ok) {
+                m0 = v[k].x < m0 ? v[k].x : m0;
+                m1 = v[k].y < m1 ? v[k].y : m1;
+            } else {
+                all_def = 0;
+            }
+        }
+    }
+    for (; p < p1; p += RG) {
+        const u64x2g v = *reinterpret_cast<const u64x2g *>(base + p * D);
+        if (!DEF || defined[e * P + p]) {
+            m0 = v.x < m0 ? v.x : m0;
+            m1 = v.y < m1 ? v.y : m1;
+        } else {
+            all_def = 0;
+        }
+    }
+    red[2 * t] = m0;
+    red[2 * t + 1] = m1;
+    __syncthreads();
+    uint64_t *o = out + e * (uint64_t)(D + 1);
+    for (uint32_t d = t; d < D; d += GST_THREADS) {
+        uint64_t m = ~0ull;
+        for (uint32_t r = 0; r < RG; ++r) {
+            const uint64_t v = red[r * D + d];
+            m = v < m ? v : m;
+        }
+        if (m != ~0ull) {
+            if (bands == 1) o[d] = m;
+            else atomicMin((unsigned long long *)&o[d], (unsigned long long)m);
+        }
+    }
+    if (t == 0 && !all_def) atomicMin((unsigned long long *)&o[D], 0ull);
+}
+
 __global__ void k_gst_finalize(uint64_t *vec, uint32_t D, uint64_t E) {
     const uint64_t n = E * (uint64_t)D;
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
@@ -125,7 +197,28 @@ int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
                        out, D, E);
     AGN_HIP(hipGetLastError());
     if (P == 0 || E == 0) return AGN_OK;
-    // ~16 KB of clocks per block; at least 1 row
+    if (D <= 2u * GST_THREADS && ((2u * GST_THREADS) % D) == 0 && (D % 2u) == 0 &&
+        ((uintptr_t)clocks % 16u) == 0) {
+        // column-resident kernel: ~1024 blocks over all epochs, >= 64 rows each
+        const uint64_t RG = (2u * GST_THREADS) / D;
+        uint64_t bands = (1024 + E - 1) / E;
+        uint64_t rows = (P + bands - 1) / bands;
+        const uint64_t min_rows = 32 * RG;
+        if (rows < min_rows) rows = min_rows;
+        rows = (rows + RG - 1) / RG * RG;  // whole block steps
+        bands = (P + rows - 1) / rows;
+        const uint64_t blocks = E * bands;
+        if (blocks > 0x7fffffffull) return fail(AGN_ENOTSUP, "gst: grid too large");
+        if (defined)
+            hipLaunchKernelGGL(k_gst_cols<true>, dim3((unsigned)blocks), dim3(GST_THREADS), 0, s,
+                               clocks, defined, out, D, P, rows, bands);
+        else
+            hipLaunchKernelGGL(k_gst_cols<false>, dim3((unsigned)blocks), dim3(GST_THREADS), 0, s,
+                               clocks, defined, out, D, P, rows, bands);
+        AGN_HIP(hipGetLastError());
+        return AGN_OK;
+    }
+    // general D: ~16 KB of clocks per block; at least 1 row
     uint64_t rows = (16384 / 8) / D;
     if (rows < 1) rows = 1;
     const uint64_t bands = (P + rows - 1) / rows;
