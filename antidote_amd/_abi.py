@@ -90,6 +90,8 @@ PROTOTYPES = {
     "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
     "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),
     "agn_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
+    "agn_gst_scalar": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P]),
+    "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),
     "agn_comm_unique_id": (C.c_int, [P]),
     "agn_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
     "agn_comm_destroy": (C.c_int, [P]),
@@ -107,6 +109,8 @@ ORACLE_PROTOTYPES = {
     "oracle_gst_min": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, C.c_int]),
     "oracle_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
     "oracle_select_base": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, P, P, P]),
+    "oracle_gst_scalar": (C.c_int, [C.c_uint32, C.c_uint64, P, P]),
+    "oracle_dep_check": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P]),
     "oracle_vc_le": (C.c_int, [C.c_uint32, P, P, P, P]),
     "oracle_vc_all_dots_greater": (C.c_int, [C.c_uint32, P, P, P, P]),
 }

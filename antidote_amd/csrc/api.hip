@@ -339,6 +339,28 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
     return launch_gst_finalize(n_dcs, n_epochs, vec, (hipStream_t)stream);
 }
 
+int agn_gst_scalar(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec,
+                   uint64_t *out_gst, void *stream) {
+    if (n_dcs == 0) return fail(AGN_EINVAL, "gst_scalar: n_dcs=0");
+    if (n_epochs && !vec) return fail(AGN_EINVAL, "gst_scalar: null vec");
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    return launch_gst_scalar(n_dcs, n_epochs, vec, out_gst, (hipStream_t)stream);
+}
+
+int agn_dep_check(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_txn, const uint64_t *deps,
+                  const uint64_t *deps_mask, const uint32_t *origin, const uint32_t *part,
+                  uint64_t n_parts, const uint64_t *part_clock, const uint64_t *part_mask,
+                  uint8_t *out_ok, void *stream) {
+    if (n_dcs == 0 || n_dcs > 4096) return fail(AGN_EINVAL, "dep_check: n_dcs=%u", n_dcs);
+    if (n_txn && (!deps || !origin || !part || !part_clock || !out_ok || n_parts == 0))
+        return fail(AGN_EINVAL, "dep_check: null argument");
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    return launch_dep_check(n_dcs, n_txn, deps, deps_mask, origin, part, n_parts, part_clock,
+                            part_mask, out_ok, (hipStream_t)stream);
+}
+
 int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *nw, int *changed) {
     if (!last || !nw) return fail(AGN_EINVAL, "null clock");
     int c = 0;

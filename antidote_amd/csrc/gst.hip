@@ -158,6 +158,58 @@ __global__ void k_gst_finalize(uint64_t *vec, uint32_t D, uint64_t E) {
     }
 }
 
+// Gentlerain scalar GST: one wave per epoch row, lanes over DCs.
+__global__ __launch_bounds__(256) void k_gst_scalar(uint64_t *vec, uint64_t *out_gst,
+                                                    uint32_t D, uint64_t E) {
+    const uint64_t e = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (e >= E) return;
+    const int lane = lane_id();
+    uint64_t *row = vec + e * (uint64_t)(D + 1);
+    uint64_t m = ~0ull;
+    for (uint32_t d = lane; d < D; d += AGN_WAVE) m = row[d] < m ? row[d] : m;
+#pragma unroll
+    for (int x = 1; x < AGN_WAVE; x <<= 1) {
+        const uint64_t o = shfl_xor_u64(m, x);
+        m = o < m ? o : m;
+    }
+    if (m != ~0ull)
+        for (uint32_t d = lane; d < D; d += AGN_WAVE)
+            if (row[d] != ~0ull) row[d] = m;  // dict:map(fun(_K, _V) -> GST end)
+    if (lane == 0 && out_gst) out_gst[e] = m;
+}
+
+// try_store/2's vectorclock:ge(Cur, Deps) with the origin entry zeroed on
+// both sides: one wave per transaction, lanes over DCs, one ballot.
+__global__ __launch_bounds__(256) void k_dep_check(uint32_t D, uint64_t n,
+                                                   const uint64_t *__restrict__ deps,
+                                                   const uint64_t *__restrict__ dm,
+                                                   const uint32_t *__restrict__ origin,
+                                                   const uint32_t *__restrict__ part,
+                                                   uint64_t n_parts,
+                                                   const uint64_t *__restrict__ pc,
+                                                   const uint64_t *__restrict__ pm,
+                                                   uint8_t *__restrict__ ok) {
+    const uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (t >= n) return;
+    const int lane = lane_id();
+    const uint32_t W = n_words(D);
+    const uint64_t p = part[t];
+    const uint32_t o = origin[t];
+    bool bad = p >= n_parts;
+    if (!bad) {
+        for (uint32_t d = lane; d < D; d += AGN_WAVE) {
+            if (d == o) continue;
+            const bool pa = !dm || ((dm[t * W + (d >> 6)] >> (d & 63)) & 1ull);
+            if (!pa) continue;
+            const bool pb = !pm || ((pm[p * W + (d >> 6)] >> (d & 63)) & 1ull);
+            const uint64_t b = pb ? pc[p * D + d] : 0ull;
+            if (deps[t * D + d] > b) bad = true;
+        }
+    }
+    const uint64_t any = ballot(bad);
+    if (lane == 0) ok[t] = any ? 0 : 1;
+}
+
 __global__ void k_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,
                               const uint64_t *clocks, const uint64_t *clock_mask,
                               const uint64_t *R, const uint64_t *R_mask, int32_t *out_idx,
@@ -234,6 +286,25 @@ int launch_gst_finalize(uint32_t D, uint64_t E, uint64_t *vec, hipStream_t s) {
     if (E == 0 || D == 0) return AGN_OK;
     hipLaunchKernelGGL(k_gst_finalize, dim3(grid_for(E * D, 256, 1024)), dim3(256), 0, s, vec,
                        D, E);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+int launch_gst_scalar(uint32_t D, uint64_t E, uint64_t *vec, uint64_t *out_gst, hipStream_t s) {
+    if (E == 0) return AGN_OK;
+    hipLaunchKernelGGL(k_gst_scalar, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, s, vec, out_gst,
+                       D, E);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+int launch_dep_check(uint32_t D, uint64_t n, const uint64_t *deps, const uint64_t *dm,
+                     const uint32_t *origin, const uint32_t *part, uint64_t n_parts,
+                     const uint64_t *pc, const uint64_t *pm, uint8_t *ok, hipStream_t s) {
+    if (n == 0) return AGN_OK;
+    if ((n + 3) / 4 > 0x7fffffffull) return fail(AGN_EINVAL, "dep_check: batch too large");
+    hipLaunchKernelGGL(k_dep_check, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D, n, deps,
+                       dm, origin, part, n_parts, pc, pm, ok);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }

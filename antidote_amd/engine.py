@@ -183,6 +183,16 @@ class Engine:
         check(self.lib.agn_gst_finalize(self.ctx, n_dcs, n_epochs, vec_ptr, stream),
               "agn_gst_finalize")
 
+    def gst_scalar(self, n_dcs, n_epochs, vec_ptr, out_ptr, stream=None):
+        check(self.lib.agn_gst_scalar(self.ctx, n_dcs, n_epochs, vec_ptr, out_ptr, stream),
+              "agn_gst_scalar")
+
+    def dep_check(self, n_dcs, n_txn, deps_ptr, dmask_ptr, origin_ptr, part_ptr, n_parts,
+                  pc_ptr, pmask_ptr, out_ptr, stream=None):
+        check(self.lib.agn_dep_check(self.ctx, n_dcs, n_txn, deps_ptr, dmask_ptr, origin_ptr,
+                                     part_ptr, n_parts, pc_ptr, pmask_ptr, out_ptr, stream),
+              "agn_dep_check")
+
     def select_base(self, n_dcs, n_req, off_ptr, clocks_ptr, cmask_ptr, R_ptr, Rmask_ptr,
                     idx_ptr, first_ptr, stream=None):
         check(self.lib.agn_select_base(self.ctx, n_dcs, n_req, off_ptr, clocks_ptr, cmask_ptr,

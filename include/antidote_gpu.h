@@ -204,6 +204,32 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
 int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *new_,
                       int *changed);
 
+/* ---- gentlerain scalar GST ----------------------------------------------
+ * dc_utilities:get_scalar_stable_time/0 and the gr branch of
+ * get_stable_snapshot/0 (src/dc_utilities.erl:247-320): GST = the min over
+ * the DCs present in the merged stable dict; every present DC is replaced by
+ * GST (in place on [n_epochs][D+1] rows as produced by agn_gst_min /
+ * agn_gst_finalize; word D is left as is).  out_gst[n_epochs] receives GST,
+ * or UINT64_MAX when the dict is empty (the caller then uses
+ * now - ?OLD_SS_MICROSEC, :303-309).  Device pointers. */
+int agn_gst_scalar(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec,
+                   uint64_t *out_gst, void *stream);
+
+/* ---- causal-dependency check ---------------------------------------------
+ * inter_dc_dep_vnode:try_store/2 (src/inter_dc_dep_vnode.erl:128-155): a
+ * remote transaction is applicable iff vectorclock:ge(CurrentClock, Deps)
+ * with the originating DC's entry set to 0 on both sides.  Batched over
+ * n_txn transactions: deps[n_txn][D] (+ deps_mask, NULL = dense) is the
+ * transaction's snapshot, origin[n_txn] its DC index, part[n_txn] the index
+ * of its partition's clock in part_clock[n_parts][D] (+ part_mask).  Each
+ * transaction is checked against the given clocks (the caller applies the
+ * in-order queue semantics: the first blocked transaction stops its queue).
+ * out_ok[n_txn] = 1 if applicable.  Device pointers. */
+int agn_dep_check(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_txn, const uint64_t *deps,
+                  const uint64_t *deps_mask, const uint32_t *origin, const uint32_t *part,
+                  uint64_t n_parts, const uint64_t *part_clock, const uint64_t *part_mask,
+                  uint8_t *out_ok, void *stream);
+
 /* ---- multi-GPU: the one collective -------------------------------------
  * The meta_data_sender exchange (src/meta_data_sender.erl:230-255: local min,
  * cast to every node, min again) is one RCCL allreduce(ncclUint64, ncclMin)

@@ -358,6 +358,44 @@ int oracle_update_stable(uint32_t D, uint64_t *last, const uint64_t *nw, int *ch
     return AGN_OK;
 }
 
+/* Gentlerain (src/dc_utilities.erl:287-320): GST = lists:min of the values of
+ * the stable dict; get_stable_snapshot's gr branch maps every entry to GST. */
+int oracle_gst_scalar(uint32_t D, uint64_t E, uint64_t *vec, uint64_t *out_gst) {
+    for (uint64_t e = 0; e < E; ++e) {
+        uint64_t *row = vec + e * (D + 1);
+        uint64_t gst = UINT64_MAX;
+        for (uint32_t d = 0; d < D; ++d)
+            if (row[d] != UINT64_MAX && row[d] < gst) gst = row[d];
+        if (gst != UINT64_MAX)
+            for (uint32_t d = 0; d < D; ++d)
+                if (row[d] != UINT64_MAX) row[d] = gst; /* dict:map(fun(_K,_V) -> GST end) */
+        if (out_gst) out_gst[e] = gst;
+    }
+    return AGN_OK;
+}
+
+/* try_store/2 (src/inter_dc_dep_vnode.erl:128-155): Deps = set_clock_of_dc(DCID, 0,
+ * snapshot), Cur = set_clock_of_dc(DCID, 0, partition clock), ok = ge(Cur, Deps)
+ * = le(Deps, Cur): every DC of Deps (except the origin, now 0) <= Cur (missing = 0). */
+int oracle_dep_check(uint32_t D, uint64_t n, const uint64_t *deps, const uint64_t *dm,
+                     const uint32_t *origin, const uint32_t *part, uint64_t n_parts,
+                     const uint64_t *pc, const uint64_t *pm, uint8_t *ok) {
+    const uint32_t W = W_OF(D);
+    for (uint64_t t = 0; t < n; ++t) {
+        const uint64_t p = part[t];
+        if (p >= n_parts) return AGN_EINVAL;
+        const uint64_t *a = deps + t * D, *am = dm ? dm + t * W : NULL;
+        const uint64_t *b = pc + p * D, *bm = pm ? pm + p * W : NULL;
+        int r = 1;
+        for (uint32_t d = 0; d < D && r; ++d) {
+            if (d == origin[t]) continue; /* both sides 0 */
+            if (present(am, d) && a[d] > get_clock(b, bm, d)) r = 0;
+        }
+        ok[t] = (uint8_t)r;
+    }
+    return AGN_OK;
+}
+
 /* get_smaller/2: first (newest) entry whose clock is le the read clock;
  * IsFirst is true until the walk moves past the head (:78-87). */
 int oracle_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,

@@ -40,6 +40,16 @@ int oracle_select_base(uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off
                        const uint64_t *R, const uint64_t *R_mask,
                        int32_t *out_idx, uint8_t *out_is_first);
 
+/* dc_utilities gentlerain GST (get_scalar_stable_time/0), same encoding as
+ * agn_gst_scalar. */
+int oracle_gst_scalar(uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec, uint64_t *out_gst);
+
+/* inter_dc_dep_vnode:try_store/2 dependency check, same encoding as agn_dep_check. */
+int oracle_dep_check(uint32_t n_dcs, uint64_t n_txn, const uint64_t *deps,
+                     const uint64_t *deps_mask, const uint32_t *origin, const uint32_t *part,
+                     uint64_t n_parts, const uint64_t *part_clock, const uint64_t *part_mask,
+                     uint8_t *out_ok);
+
 /* vectorclock 0.1.0 predicates on single clocks (missing entry = 0). */
 int oracle_vc_le(uint32_t n_dcs, const uint64_t *a, const uint64_t *am,
                  const uint64_t *b, const uint64_t *bm);

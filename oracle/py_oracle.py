@@ -534,3 +534,20 @@ def scalar_stable_time(ss: dict):
         return ss
     g = min(ss.values())
     return {dc: g for dc in ss}
+
+
+# ---------------------------------------------------------------- inter-DC dependency check
+def vc_set_clock_of_dc(dc, t, vc: dict) -> dict:
+    out = dict(vc)
+    out[dc] = t
+    return out
+
+
+def dependencies_satisfied(origin_dc, txn_snapshot: dict, partition_clock: dict) -> bool:
+    """inter_dc_dep_vnode:try_store/2 (src/inter_dc_dep_vnode.erl:128-155):
+    Dependencies = set_clock_of_dc(DCID, 0, Snapshot), CurrentClock =
+    set_clock_of_dc(DCID, 0, PartitionClock), applicable iff
+    vectorclock:ge(CurrentClock, Dependencies)."""
+    deps = vc_set_clock_of_dc(origin_dc, 0, txn_snapshot)
+    cur = vc_set_clock_of_dc(origin_dc, 0, partition_clock)
+    return vc_ge(cur, deps)

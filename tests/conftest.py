@@ -26,3 +26,12 @@ def oracle_lib():
     if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     return _abi.bind(ctypes.CDLL(so), _abi.ORACLE_PROTOTYPES)
+
+
+@pytest.fixture(scope="session")
+def eng():
+    """One engine context on cuda:0 for every GPU test of the session."""
+    from antidote_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()

@@ -15,13 +15,6 @@ from synth import compare, random_case
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def eng():
-    e = Engine(0)
-    yield e
-    e.close()
-
-
 def gpu_fn(eng):
     def fn(ls, rs, os_):
         return eng.lib.agn_materialize_host(eng.ctx, C.byref(ls), C.byref(rs), C.byref(os_))
