@@ -18,6 +18,7 @@ EFFECT_INVALID = -(1 << 63)
 TAG_INVALID = 0xFFFFFFFF
 
 F_NEWSS, F_CT_IGNORE, F_ERR_UNEXPECTED, F_ERR_CORRUPTED, F_ERR_CAPACITY = 0x1, 0x2, 0x4, 0x8, 0x10
+GC_ALL_PRUNED = 0x1
 UNIQUE_ID_BYTES = 128
 U64_MAX = (1 << 64) - 1
 
@@ -90,6 +91,7 @@ PROTOTYPES = {
     "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
     "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),
     "agn_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
+    "agn_prune_ops": (C.c_int, [P, C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P, P, P]),
     "agn_gst_scalar": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P]),
     "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),
     "agn_comm_unique_id": (C.c_int, [P]),
@@ -109,6 +111,7 @@ ORACLE_PROTOTYPES = {
     "oracle_gst_min": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, C.c_int]),
     "oracle_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
     "oracle_select_base": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, P, P, P]),
+    "oracle_prune_ops": (C.c_int, [C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P]),
     "oracle_gst_scalar": (C.c_int, [C.c_uint32, C.c_uint64, P, P]),
     "oracle_dep_check": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P]),
     "oracle_vc_le": (C.c_int, [C.c_uint32, P, P, P, P]),

@@ -339,6 +339,33 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
     return launch_gst_finalize(n_dcs, n_epochs, vec, (hipStream_t)stream);
 }
 
+int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
+                  const uint64_t *threshold, const uint64_t *threshold_mask, agn_log *out,
+                  uint32_t *out_flags, uint64_t *out_totals, void *stream) {
+    if (!log || !out) return fail(AGN_EINVAL, "prune_ops: null descriptor");
+    if (log->n_dcs == 0 || log->n_dcs > 256)
+        return fail(AGN_EINVAL, "prune_ops: n_dcs=%u not in [1,256]", log->n_dcs);
+    if (log->n_keys == 0) return AGN_OK;
+    if (!log->key_off || !threshold || !out->key_off)
+        return fail(AGN_EINVAL, "prune_ops: key_off / threshold required");
+    if (log->n_entries && (!log->oc || !log->op_id || !out->oc || !out->op_id))
+        return fail(AGN_EINVAL, "prune_ops: oc / op_id required");
+    if ((log->oc_mask && !out->oc_mask) || (log->txid && !out->txid) ||
+        (log->eff && !out->eff) || (log->tag && !out->tag) || (log->add_tok && !out->add_tok) ||
+        (log->rem_off && (!out->rem_off || (!out->rem_tok && log->rem_tok))))
+        return fail(AGN_EINVAL, "prune_ops: out lacks an array the log has");
+    if (log->n_entries > 0x7fffffffull || log->n_keys > 0x7fffffffull)
+        return fail(AGN_ENOTSUP, "prune_ops: log too large for one pass");
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    out->crdt_type = log->crdt_type;
+    out->n_dcs = log->n_dcs;
+    out->n_keys = log->n_keys;
+    out->key_type = log->key_type;
+    return launch_prune_ops(*log, prune, threshold, threshold_mask, *out, out_flags, out_totals,
+                            (hipStream_t)stream);
+}
+
 int agn_gst_scalar(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec,
                    uint64_t *out_gst, void *stream) {
     if (n_dcs == 0) return fail(AGN_EINVAL, "gst_scalar: n_dcs=0");

@@ -93,6 +93,9 @@ int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
 int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
                    const uint8_t *defined, uint64_t *out, hipStream_t s);
 int launch_gst_finalize(uint32_t D, uint64_t E, uint64_t *vec, hipStream_t s);
+int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+                     const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
+                     uint64_t *totals, hipStream_t st);
 int launch_gst_scalar(uint32_t D, uint64_t E, uint64_t *vec, uint64_t *out_gst, hipStream_t s);
 int launch_dep_check(uint32_t D, uint64_t n, const uint64_t *deps, const uint64_t *dm,
                      const uint32_t *origin, const uint32_t *part, uint64_t n_parts,

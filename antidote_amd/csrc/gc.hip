@@ -1,0 +1,237 @@
+// gc.hip — garbage collection of the device op log on gfx950:
+// materializer_vnode:snapshot_insert_gc -> prune_ops/check_filter
+// (src/materializer_vnode.erl:513-604).  For every key selected for GC the
+// ops already covered by the pruned snapshot are dropped:
+//   keep(op) = belongs_to_snapshot_op(Threshold, op)
+//            = not vectorclock:le(OpSSCommit, Threshold)   (src/materializer.erl:101-106)
+// in log order (check_filter keeps the survivors' order, :592-604).
+//
+// Out-of-place stream compaction in three HBM-bound passes:
+//   1. k_prune_mark   one wave per key: the VC filter over the key's
+//      OpSSCommit rows (filter.hpp shape: LPO lanes x DPL DCs per op) writes
+//      one keep byte per entry, the key's kept-entry and kept-token counts;
+//   2. two inclusive scans (hipcub) turn the counts into the new key_off and
+//      the per-key base of the new removal-token CSR;
+//   3. k_prune_scatter one wave per key, 64 entries per step: ballot prefix
+//      -> destination slot; the kept OpSSCommit rows are copied
+//      cooperatively (kept-rank -> source entry through LDS, so reads and
+//      writes are lane-contiguous), the per-entry fields lane = entry, and the
+//      removal tokens after a wave scan of the kept list lengths.
+// HBM bytes per entry: pass 1 reads 8*D (+4 rem_off for tag logs) and writes
+// 1; pass 3 reads 1 + the entry's fields and writes the kept ones.
+#include <hipcub/hipcub.hpp>
+
+#include "filter.hpp"
+
+namespace agn {
+namespace {
+
+template <int DPL, int LPO, bool SPARSE>
+__global__ __launch_bounds__(256) void k_prune_mark(agn_log log, const uint8_t *__restrict__ prune,
+                                                    const uint64_t *__restrict__ thr,
+                                                    const uint64_t *__restrict__ thr_mask,
+                                                    uint8_t *__restrict__ keep,
+                                                    uint64_t *__restrict__ cnt,
+                                                    uint64_t *__restrict__ rcnt) {
+    using S = Shape<DPL, LPO>;
+    const uint64_t k = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (k >= log.n_keys) return;
+    const int lane = lane_id();
+    const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
+    const uint32_t D = log.n_dcs, W = n_words(D);
+    const uint64_t off = uniform_u64(log.key_off[k]);
+    const uint64_t n = uniform_u64(log.key_off[k + 1]) - off;
+    const bool gc = prune == nullptr || prune[k] != 0;
+    // the threshold slice this lane compares (missing entry = 0)
+    uint64_t t[DPL];
+    const uint32_t tbits = chunk_bits<DPL, SPARSE>(thr_mask, k, W, d0, D);
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) t[j] = ((tbits >> j) & 1u) ? thr[k * D + (uint32_t)(d0 + j)] : 0ull;
+    uint64_t kept = 0, rk = 0;
+    for (uint64_t b = 0; b < n; b += S::OPI) {
+        const uint64_t pos = b + (uint64_t)slot;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);
+        bool le = true;
+        if (gc) {
+            const uint32_t obits = valid ? chunk_bits<DPL, SPARSE>(log.oc_mask, e, W, d0, D) : 0u;
+#pragma unroll
+            for (int j = 0; j < DPL; ++j)
+                if ((obits >> j) & 1u) le = le && (log.oc[e * D + (uint32_t)(d0 + j)] <= t[j]);
+            if (LPO > 1) {
+                const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
+                le = (ballot(!le) & grp) == 0ull;
+            }
+        }
+        const bool kp = valid && (!gc || !le);  // belongs_to_snapshot_op
+        if (valid && sub == 0) keep[e] = kp ? 1 : 0;
+        kept += (uint64_t)__builtin_popcountll(ballot(kp && sub == 0));
+        if (log.rem_off != nullptr && kp && sub == 0) rk += log.rem_off[e + 1] - log.rem_off[e];
+    }
+    rk = (uint64_t)wave_sum_i64((int64_t)rk);
+    if (lane == 0) {
+        cnt[k] = kept;
+        rcnt[k] = rk;
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int x = 1; x < AGN_WAVE; x <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)v, x, AGN_WAVE);
+        if (lane >= x) v += o;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_prune_scatter(agn_log log, agn_log out,
+                                                       const uint8_t *__restrict__ prune,
+                                                       const uint8_t *__restrict__ keep,
+                                                       const uint64_t *__restrict__ rbase,
+                                                       uint32_t *__restrict__ flags) {
+    __shared__ uint64_t src[4][AGN_WAVE];
+    const int w = threadIdx.x >> 6;
+    const uint64_t k = (uint64_t)blockIdx.x * 4u + (uint64_t)w;
+    if (k >= log.n_keys) return;
+    const int lane = lane_id();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t D = log.n_dcs, W = n_words(D);
+    const uint64_t off = uniform_u64(log.key_off[k]);
+    const uint64_t n = uniform_u64(log.key_off[k + 1]) - off;
+    const uint64_t noff = uniform_u64(out.key_off[k]);
+    uint64_t written = 0, rwritten = 0;
+    const uint64_t rb = rbase ? uniform_u64(rbase[k]) : 0ull;
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        const uint64_t pos = b + (uint64_t)lane;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);
+        const bool kp = valid && keep[e] != 0;
+        const uint64_t m = ballot(kp);
+        const uint32_t nk = (uint32_t)__builtin_popcountll(m);
+        const uint64_t dst = noff + written + (uint64_t)__builtin_popcountll(m & lt);
+        if (kp) {
+            src[w][__builtin_popcountll(m & lt)] = e;
+            ((uint32_t *)out.op_id)[dst] = log.op_id[e];
+            if (log.txid) ((uint64_t *)out.txid)[dst] = log.txid[e];
+            if (log.eff) ((int64_t *)out.eff)[dst] = log.eff[e];
+            if (log.tag) ((uint32_t *)out.tag)[dst] = log.tag[e];
+            if (log.add_tok) ((uint64_t *)out.add_tok)[dst] = log.add_tok[e];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // kept OpSSCommit rows (and masks): rank-major, lane-contiguous copy
+        uint64_t *ooc = (uint64_t *)out.oc + (noff + written) * D;
+        for (uint64_t x = (uint64_t)lane; x < (uint64_t)nk * D; x += AGN_WAVE) {
+            const uint64_t r = x / D, d = x % D;
+            ooc[x] = log.oc[src[w][r] * D + d];
+        }
+        if (log.oc_mask) {
+            uint64_t *om = (uint64_t *)out.oc_mask + (noff + written) * W;
+            for (uint64_t x = (uint64_t)lane; x < (uint64_t)nk * W; x += AGN_WAVE)
+                om[x] = log.oc_mask[src[w][x / W] * W + x % W];
+        }
+        // removal tokens: kept lists, concatenated in order
+        if (log.rem_off) {
+            const uint32_t r0 = kp ? log.rem_off[e] : 0u;
+            const uint32_t len = kp ? log.rem_off[e + 1] - r0 : 0u;
+            const uint32_t incl = wave_incl_scan_u32(len);
+            const uint64_t start = rb + rwritten + (uint64_t)(incl - len);
+            if (kp) {
+                ((uint32_t *)out.rem_off)[dst + 1] = (uint32_t)(start + len);
+                for (uint32_t j = 0; j < len; ++j)
+                    ((uint64_t *)out.rem_tok)[start + j] = log.rem_tok[r0 + j];
+            }
+            rwritten += (uint64_t)__builtin_amdgcn_readlane(incl, 63);
+        }
+        written += nk;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0 && flags) {
+        const bool gc = prune == nullptr || prune[k] != 0;
+        // every op covered: the reference stores element(?FIRST_OP+Len) (:580-583)
+        flags[k] = (gc && written == 0) ? AGN_GC_ALL_PRUNED : 0u;
+    }
+}
+
+template <int DPL, int LPO, bool SPARSE>
+int mark_shape(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+               const uint64_t *thr_mask, uint8_t *keep, uint64_t *cnt, uint64_t *rcnt,
+               hipStream_t st) {
+    const unsigned blocks = grid_for(log.n_keys, 4, 0x7fffffffu);
+    hipLaunchKernelGGL((k_prune_mark<DPL, LPO, SPARSE>), dim3(blocks), dim3(256), 0, st, log,
+                       prune, thr, thr_mask, keep, cnt, rcnt);
+    return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_mark launch");
+}
+
+template <bool SPARSE>
+int mark(const agn_log &log, const uint8_t *prune, const uint64_t *thr, const uint64_t *thr_mask,
+         uint8_t *keep, uint64_t *cnt, uint64_t *rcnt, hipStream_t st) {
+#define AGN_L(DPL, LPO) mark_shape<DPL, LPO, SPARSE>(log, prune, thr, thr_mask, keep, cnt, rcnt, st)
+    AGN_DISPATCH_SHAPES(log.n_dcs, AGN_L)
+#undef AGN_L
+}
+
+}  // namespace
+
+int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+                     const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
+                     uint64_t *totals, hipStream_t st) {
+    const uint64_t K = log.n_keys, E = log.n_entries;
+    const bool tags = log.rem_off != nullptr;
+    size_t scan_bytes = 0, scan_bytes2 = 0;
+    AGN_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (uint64_t *)nullptr,
+                                             (uint64_t *)nullptr, (int)K, st));
+    if (tags)
+        AGN_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes2, (uint64_t *)nullptr,
+                                                 (uint64_t *)nullptr, (int)K, st));
+    if (scan_bytes2 > scan_bytes) scan_bytes = scan_bytes2;
+    // layout: [scan temp (256-aligned, rocPRIM assumes an aligned base)]
+    //         [keep E bytes][cnt K+1][rcnt K+1][rbase K+1]
+    const size_t tmp_bytes = (scan_bytes + 255) / 256 * 256;
+    const size_t keep_bytes = (E + 255) / 256 * 256;
+    const size_t bytes = tmp_bytes + keep_bytes + 3 * (K + 1) * sizeof(uint64_t) + 256;
+    uint8_t *scratch = nullptr;
+    AGN_HIP(hipMallocAsync((void **)&scratch, bytes, st));
+    void *tmp = scratch;
+    uint8_t *keep = scratch + tmp_bytes;
+    uint64_t *cnt = (uint64_t *)(keep + keep_bytes);
+    uint64_t *rcnt = cnt + (K + 1);
+    uint64_t *rbase = rcnt + (K + 1);
+    int rc = AGN_OK;
+    const bool sparse = log.oc_mask || thr_mask;
+    if (K) rc = sparse ? mark<true>(log, prune, thr, thr_mask, keep, cnt, rcnt, st)
+                       : mark<false>(log, prune, thr, thr_mask, keep, cnt, rcnt, st);
+    hipError_t e = hipSuccess;
+    // new key_off = [0, inclusive scan of cnt]; token bases likewise
+    if (rc == AGN_OK) e = hipMemsetAsync((void *)out.key_off, 0, sizeof(uint64_t), st);
+    if (rc == AGN_OK && e == hipSuccess && K)
+        e = hipcub::DeviceScan::InclusiveSum(tmp, scan_bytes, cnt, (uint64_t *)out.key_off + 1,
+                                             (int)K, st);
+    if (rc == AGN_OK && e == hipSuccess && tags) {
+        e = hipMemsetAsync(rbase, 0, sizeof(uint64_t), st);
+        if (e == hipSuccess) e = hipMemsetAsync((void *)out.rem_off, 0, sizeof(uint32_t), st);
+        if (e == hipSuccess && K)
+            e = hipcub::DeviceScan::InclusiveSum(tmp, scan_bytes, rcnt, rbase + 1, (int)K, st);
+    }
+    if (rc == AGN_OK && e == hipSuccess && K) {
+        hipLaunchKernelGGL(k_prune_scatter, dim3(grid_for(K, 4, 0x7fffffffu)), dim3(256), 0, st,
+                           log, out, prune, keep, tags ? rbase : nullptr, flags);
+        e = hipGetLastError();
+    }
+    if (rc == AGN_OK && e == hipSuccess && totals) {
+        e = hipMemcpyAsync(totals, (const uint64_t *)out.key_off + K, sizeof(uint64_t),
+                           hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess)
+            e = tags ? hipMemcpyAsync(totals + 1, rbase + K, sizeof(uint64_t),
+                                      hipMemcpyDeviceToDevice, st)
+                     : hipMemsetAsync(totals + 1, 0, sizeof(uint64_t), st);
+    }
+    if (rc == AGN_OK && e != hipSuccess) rc = fail(AGN_EHIP, "prune_ops: %s", hipGetErrorString(e));
+    const hipError_t ef = hipFreeAsync(scratch, st);
+    if (rc == AGN_OK && ef != hipSuccess) rc = fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
+    return rc;
+}
+
+}  // namespace agn

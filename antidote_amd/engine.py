@@ -112,6 +112,31 @@ class Engine:
             setattr(s, name, b.ptr)
         return d
 
+    def alloc_log_like(self, log: EncodedLog) -> DeviceArrays:
+        """Device arrays with the sizes (and presence) of `log`'s (agn_prune_ops output)."""
+        s = _abi.AgnLog()
+        s.crdt_type, s.n_dcs = log.crdt_type, log.n_dcs
+        s.n_keys, s.n_entries = log.n_keys, log.n_entries
+        d = DeviceArrays(s)
+        for name in ("key_off", "oc", "oc_mask", "op_id", "txid", "eff", "tag", "add_tok",
+                     "rem_off", "rem_tok"):
+            a = getattr(log, name)
+            if a is None or (isinstance(a, np.ndarray) and a.size == 0 and name != "rem_tok"):
+                setattr(s, name, None)
+                continue
+            b = self.empty(a.nbytes)
+            d.bufs[name] = b
+            d.shapes[name] = (a.dtype, a.shape)
+            setattr(s, name, b.ptr)
+        return d
+
+    def prune_ops(self, dlog: DeviceArrays, prune_ptr, thr_ptr, thr_mask_ptr, dout: DeviceArrays,
+                  flags_ptr=None, totals_ptr=None, stream=None):
+        """agn_prune_ops: materializer_vnode GC of the device op log (out of place)."""
+        check(self.lib.agn_prune_ops(self.ctx, C.byref(dlog.struct), prune_ptr, thr_ptr,
+                                     thr_mask_ptr, C.byref(dout.struct), flags_ptr, totals_ptr,
+                                     stream), "agn_prune_ops")
+
     def upload_read(self, req: EncodedRead, sparse: bool = True) -> DeviceArrays:
         s = read_struct(req, sparse=sparse)
         d = DeviceArrays(s)

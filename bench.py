@@ -58,6 +58,8 @@ def parse():
                     help="CPU-baseline sample size in keys (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="extra multi-thread CPU run")
     ap.add_argument("--gst", action="store_true", help="also time a GST epoch + RCCL min-allreduce")
+    ap.add_argument("--gc", action="store_true",
+                    help="also time the op-log GC (agn_prune_ops) over the whole log")
     return ap.parse_args()
 
 
@@ -184,6 +186,8 @@ def main():
 
     probe = probe_read_gbs(eng, dl, n_keys * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
 
+    gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch) if a.gc else None
+
     gst = None
     if a.gst:
         gst = gst_bench(eng, torch, dist, world, rank, sp)
@@ -230,12 +234,59 @@ def main():
         }
         if gst:
             line["gst"] = gst
+        if gc:
+            line["gc"] = gc
         print(json.dumps(line), flush=True)
 
     eng.free_gen(dl, dr)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
+    """materializer_vnode GC (prune_ops) over every key of the device log, with
+    each key's read snapshot R as the pruning threshold (a snapshot covering a
+    random prefix of its ops).  Out-of-place: a second log of the same size."""
+    from antidote_amd import _abi
+    from antidote_amd.engine import DeviceArrays
+    D, N = cfg["n_dcs"], cfg["ops_per_key"]
+    E = n_keys * N
+    s = _abi.AgnLog()
+    s.crdt_type, s.n_dcs, s.n_keys, s.n_entries = cfg["crdt_type"], D, n_keys, E
+    out = DeviceArrays(s)
+    spec = {"key_off": 8 * (n_keys + 1), "oc": 8 * E * D, "op_id": 4 * E}
+    if cfg["crdt_type"] == 1:
+        spec["eff"] = 8 * E
+    else:
+        n_rem = int(eng.download(type("B", (), {"ptr": dl.rem_off})(), np.uint32, (E + 1,))[-1])
+        spec.update({"tag": 4 * E, "add_tok": 8 * E, "rem_off": 4 * (E + 1),
+                     "rem_tok": 8 * max(n_rem, 1)})
+    for name, nb in spec.items():
+        b = eng.empty(nb)
+        out.bufs[name] = b
+        setattr(s, name, b.ptr)
+    tot = eng.empty(16)
+    din = DeviceArrays(dl)
+    eng.prune_ops(din, None, dr.R, None, out, None, tot.ptr, sp)
+    torch.cuda.synchronize()
+    b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b.record()
+    for _ in range(3):
+        eng.prune_ops(din, None, dr.R, None, out, None, tot.ptr, sp)
+    e.record()
+    torch.cuda.synchronize()
+    ms = b.elapsed_time(e) / 3
+    kept, kept_rem = (int(x) for x in eng.download(tot, np.uint64, (2,)))
+    per_entry = 8 * D + 4 + (8 if cfg["crdt_type"] == 1 else 16)
+    # pass 1: rows + keep byte written; pass 3: keep byte + kept entries read and written
+    byts = E * (8 * D + 1) + E + 2 * kept * per_entry + 16 * kept_rem + 8 * 4 * n_keys
+    for bb in out.bufs.values():
+        bb.free()
+    tot.free()
+    return {"ms": ms, "entries": E, "kept": kept, "algorithmic_bytes": byts,
+            "achieved_GBps": byts / (ms * 1e-3) / 1e9,
+            "frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def probe_read_gbs(eng, dl, nbytes, sp, torch):

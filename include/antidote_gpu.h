@@ -204,6 +204,30 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
 int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *new_,
                       int *changed);
 
+/* ---- op-log garbage collection ------------------------------------------
+ * materializer_vnode:snapshot_insert_gc -> prune_ops/check_filter
+ * (src/materializer_vnode.erl:513-604): for every key k with prune[k] != 0
+ * (prune == NULL: every key) drop the entries already covered by the pruned
+ * snapshot, keeping exactly those with
+ *   belongs_to_snapshot_op(Threshold_k, op) = not vectorclock:le(OpSSCommit, Threshold_k)
+ * (src/materializer.erl:101-106) in log order.  threshold[n_keys][D] (+ mask,
+ * NULL = dense; missing entries read 0) is vectorclock:min over the kept
+ * snapshots' commit times (:523-527), computed by the caller.  Keys with
+ * prune[k] == 0 are copied unchanged.
+ * Out-of-place: `out` (host descriptor of device arrays) must provide
+ * key_off[n_keys+1], oc, op_id (+ oc_mask, txid, eff, tag, add_tok,
+ * rem_off[n_entries+1], rem_tok when `log` has them) with at least the input
+ * sizes; n_keys / n_dcs / crdt_type / key_type are taken from `log`.
+ * out_flags[n_keys] (device, may be NULL): AGN_GC_ALL_PRUNED when no op of
+ * a collected key survives (every op covered, or none to begin with) — the
+ * reference then stores element(?FIRST_OP+Len) of the ETS tuple, an empty
+ * slot, as a length-1 op list (:580-583); here the key keeps zero entries.  out_totals (device, may be NULL) receives
+ * {kept entries, kept removal tokens}.  Asynchronous on `stream`. */
+#define AGN_GC_ALL_PRUNED 0x1u
+int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
+                  const uint64_t *threshold, const uint64_t *threshold_mask, agn_log *out,
+                  uint32_t *out_flags, uint64_t *out_totals, void *stream);
+
 /* ---- gentlerain scalar GST ----------------------------------------------
  * dc_utilities:get_scalar_stable_time/0 and the gr branch of
  * get_stable_snapshot/0 (src/dc_utilities.erl:247-320): GST = the min over

@@ -358,6 +358,54 @@ int oracle_update_stable(uint32_t D, uint64_t *last, const uint64_t *nw, int *ch
     return AGN_OK;
 }
 
+/* prune_ops/2 + check_filter/7 (src/materializer_vnode.erl:566-604): walk the
+ * key's ops oldest first and keep those for which
+ * belongs_to_snapshot_op(Threshold, CommitTime, SnapshotTime) holds, i.e.
+ * not le(OpSSCommit, Threshold).  A key whose every op is covered keeps no
+ * entry and is flagged (the reference stores the empty slot after the last
+ * op, :580-583). */
+int oracle_prune_ops(const agn_log *log, const uint8_t *prune, const uint64_t *thr,
+                     const uint64_t *thr_mask, agn_log *out, uint32_t *out_flags) {
+    const uint32_t D = log->n_dcs, W = W_OF(D);
+    uint64_t *ko = (uint64_t *)out->key_off;
+    uint64_t *oc = (uint64_t *)out->oc, *om = (uint64_t *)out->oc_mask;
+    uint32_t *id = (uint32_t *)out->op_id, *tag = (uint32_t *)out->tag;
+    uint64_t *tx = (uint64_t *)out->txid, *add = (uint64_t *)out->add_tok;
+    int64_t *eff = (int64_t *)out->eff;
+    uint32_t *ro = (uint32_t *)out->rem_off;
+    uint64_t *rt = (uint64_t *)out->rem_tok;
+    uint64_t w = 0, rw = 0;
+    ko[0] = 0;
+    if (ro) ro[0] = 0;
+    for (uint64_t k = 0; k < log->n_keys; ++k) {
+        const int gc = prune == NULL || prune[k] != 0;
+        const uint64_t *t = thr + k * D, *tm = thr_mask ? thr_mask + k * W : NULL;
+        uint64_t kept = 0;
+        for (uint64_t e = log->key_off[k]; e < log->key_off[k + 1]; ++e) {
+            const uint64_t *o = log->oc + e * D, *m = log->oc_mask ? log->oc_mask + e * W : NULL;
+            if (gc && oracle_vc_le(D, o, m, t, tm)) continue; /* already in the snapshot */
+            for (uint32_t d = 0; d < D; ++d) oc[w * D + d] = o[d];
+            if (om) for (uint32_t x = 0; x < W; ++x) om[w * W + x] = m[x];
+            id[w] = log->op_id[e];
+            if (tx) tx[w] = log->txid[e];
+            if (eff) eff[w] = log->eff[e];
+            if (tag) tag[w] = log->tag[e];
+            if (add) add[w] = log->add_tok[e];
+            if (ro) {
+                for (uint32_t r = log->rem_off[e]; r < log->rem_off[e + 1]; ++r) rt[rw++] = log->rem_tok[r];
+                ro[w + 1] = (uint32_t)rw;
+            }
+            ++w;
+            ++kept;
+        }
+        ko[k + 1] = w;
+        if (out_flags)
+            out_flags[k] = (gc && kept == 0) ? AGN_GC_ALL_PRUNED : 0u;
+    }
+    out->n_entries = w;
+    return AGN_OK;
+}
+
 /* Gentlerain (src/dc_utilities.erl:287-320): GST = lists:min of the values of
  * the stable dict; get_stable_snapshot's gr branch maps every entry to GST. */
 int oracle_gst_scalar(uint32_t D, uint64_t E, uint64_t *vec, uint64_t *out_gst) {

@@ -40,6 +40,11 @@ int oracle_select_base(uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off
                        const uint64_t *R, const uint64_t *R_mask,
                        int32_t *out_idx, uint8_t *out_is_first);
 
+/* materializer_vnode prune_ops/check_filter over the SoA log (host arrays),
+ * same contract as agn_prune_ops (out arrays sized like the input). */
+int oracle_prune_ops(const agn_log *log, const uint8_t *prune, const uint64_t *threshold,
+                     const uint64_t *threshold_mask, agn_log *out, uint32_t *out_flags);
+
 /* dc_utilities gentlerain GST (get_scalar_stable_time/0), same encoding as
  * agn_gst_scalar. */
 int oracle_gst_scalar(uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec, uint64_t *out_gst);
