@@ -59,6 +59,17 @@ class AgnResult(C.Structure):
     ]
 
 
+class AgnSsCache(C.Structure):
+    _fields_ = [
+        ("n_dcs", C.c_uint32), ("slots", C.c_uint32), ("n_keys", C.c_uint64),
+        ("n", P), ("clock", P), ("clock_mask", P), ("last_op", P), ("value", P),
+    ]
+
+
+SNAPSHOT_THRESHOLD, SNAPSHOT_MIN, MIN_OP_STORE_SS = 10, 3, 5
+SS_HIT, SS_NEW, SS_LOG = 0, 1, 2
+
+
 class AgnGenCfg(C.Structure):
     _fields_ = [
         ("crdt_type", C.c_uint32), ("n_dcs", C.c_uint32), ("n_keys", C.c_uint64),
@@ -91,6 +102,10 @@ PROTOTYPES = {
     "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
     "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),
     "agn_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
+    "agn_ss_lookup": (C.c_int, [P, C.POINTER(AgnSsCache), C.c_uint64, P, P, P, P, P, P, P, P,
+                                P, P]),
+    "agn_ss_store": (C.c_int, [P, C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P, P,
+                               P, C.POINTER(AgnResult), P, P, P, P, P]),
     "agn_prune_ops": (C.c_int, [P, C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P, P, P]),
     "agn_gst_scalar": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P]),
     "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),
@@ -111,6 +126,10 @@ ORACLE_PROTOTYPES = {
     "oracle_gst_min": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, C.c_int]),
     "oracle_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
     "oracle_select_base": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, P, P, P]),
+    "oracle_ss_lookup": (C.c_int, [C.POINTER(AgnSsCache), C.c_uint64, P, P, P, P, P, P, P, P,
+                                   P]),
+    "oracle_ss_store": (C.c_int, [C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P,
+                                  P, P, C.POINTER(AgnResult), P, P, P, P]),
     "oracle_prune_ops": (C.c_int, [C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P]),
     "oracle_gst_scalar": (C.c_int, [C.c_uint32, C.c_uint64, P, P]),
     "oracle_dep_check": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P]),

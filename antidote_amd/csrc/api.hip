@@ -339,6 +339,53 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
     return launch_gst_finalize(n_dcs, n_epochs, vec, (hipStream_t)stream);
 }
 
+static int check_cache(const agn_ss_cache *c) {
+    if (!c) return fail(AGN_EINVAL, "ss cache: null");
+    if (c->n_dcs == 0 || c->n_dcs > 256) return fail(AGN_EINVAL, "ss cache: n_dcs=%u", c->n_dcs);
+    if (c->slots < AGN_SNAPSHOT_THRESHOLD - 1)
+        return fail(AGN_EINVAL, "ss cache: slots=%u < %d", c->slots, AGN_SNAPSHOT_THRESHOLD - 1);
+    if (c->n_keys && (!c->n || !c->clock || !c->last_op || !c->value))
+        return fail(AGN_EINVAL, "ss cache: null array");
+    return AGN_OK;
+}
+
+int agn_ss_lookup(agn_ctx *ctx, agn_ss_cache *cache, uint64_t n_req, const uint64_t *keys,
+                  const uint64_t *R, const uint64_t *R_mask, uint64_t *sct, uint64_t *sct_mask,
+                  uint8_t *sct_ignore, int64_t *base_value, uint8_t *is_first, uint8_t *status,
+                  void *stream) {
+    int rc = check_cache(cache);
+    if (rc) return rc;
+    if (n_req && (!R || !sct || !sct_ignore || !base_value || !is_first || !status))
+        return fail(AGN_EINVAL, "ss_lookup: null argument");
+    if (!keys && n_req != cache->n_keys)
+        return fail(AGN_EINVAL, "ss_lookup: keys == NULL needs n_req == n_keys");
+    rc = use_device(ctx);
+    if (rc) return rc;
+    return launch_ss_lookup(*cache, n_req, keys, R, R_mask, sct, sct_mask, sct_ignore, base_value,
+                            is_first, status, (hipStream_t)stream);
+}
+
+int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
+                 const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
+                 const uint8_t *should_gc, const agn_result *res, const int64_t *handle,
+                 uint8_t *prune, uint64_t *threshold, uint64_t *threshold_mask, void *stream) {
+    int rc = check_cache(cache);
+    if (rc) return rc;
+    if (!log || !res || !log->key_off || !prune || !threshold)
+        return fail(AGN_EINVAL, "ss_store: null argument");
+    if (log->n_keys != cache->n_keys || log->n_dcs != cache->n_dcs)
+        return fail(AGN_EINVAL, "ss_store: log and cache disagree on keys / DCs");
+    if (n_req && (!is_first || !status || !res->hole || !res->lastct || !res->count ||
+                  !res->flags || (!handle && !res->value)))
+        return fail(AGN_EINVAL, "ss_store: null argument");
+    if (!keys && n_req != cache->n_keys)
+        return fail(AGN_EINVAL, "ss_store: keys == NULL needs n_req == n_keys");
+    rc = use_device(ctx);
+    if (rc) return rc;
+    return launch_ss_store(*cache, log->key_off, n_req, keys, is_first, status, should_gc, *res,
+                           handle, prune, threshold, threshold_mask, (hipStream_t)stream);
+}
+
 int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
                   const uint64_t *threshold, const uint64_t *threshold_mask, agn_log *out,
                   uint32_t *out_flags, uint64_t *out_totals, void *stream) {

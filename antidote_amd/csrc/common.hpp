@@ -93,6 +93,14 @@ int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
 int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
                    const uint8_t *defined, uint64_t *out, hipStream_t s);
 int launch_gst_finalize(uint32_t D, uint64_t E, uint64_t *vec, hipStream_t s);
+int launch_ss_lookup(const agn_ss_cache &c, uint64_t n_req, const uint64_t *keys,
+                     const uint64_t *R, const uint64_t *Rm, uint64_t *sct, uint64_t *sctm,
+                     uint8_t *sct_ign, int64_t *base, uint8_t *first, uint8_t *status,
+                     hipStream_t st);
+int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, uint64_t n_req,
+                    const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
+                    const uint8_t *should_gc, const agn_result &res, const int64_t *handle,
+                    uint8_t *prune, uint64_t *thr, uint64_t *thrm, hipStream_t st);
 int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
                      const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
                      uint64_t *totals, hipStream_t st);

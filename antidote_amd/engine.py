@@ -130,6 +130,20 @@ class Engine:
             setattr(s, name, b.ptr)
         return d
 
+    def ss_lookup(self, cache, n_req, keys_ptr, R_ptr, Rm_ptr, sct_ptr, sctm_ptr, ign_ptr,
+                  base_ptr, first_ptr, status_ptr, stream=None):
+        check(self.lib.agn_ss_lookup(self.ctx, C.byref(cache), n_req, keys_ptr, R_ptr, Rm_ptr,
+                                     sct_ptr, sctm_ptr, ign_ptr, base_ptr, first_ptr, status_ptr,
+                                     stream), "agn_ss_lookup")
+
+    def ss_store(self, cache, dlog, n_req, keys_ptr, first_ptr, status_ptr, gc_ptr, dres,
+                 handle_ptr, prune_ptr, thr_ptr, thrm_ptr, stream=None):
+        ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
+        rs = dres.struct if isinstance(dres, DeviceArrays) else dres
+        check(self.lib.agn_ss_store(self.ctx, C.byref(cache), C.byref(ls), n_req, keys_ptr,
+                                    first_ptr, status_ptr, gc_ptr, C.byref(rs), handle_ptr,
+                                    prune_ptr, thr_ptr, thrm_ptr, stream), "agn_ss_store")
+
     def prune_ops(self, dlog: DeviceArrays, prune_ptr, thr_ptr, thr_mask_ptr, dout: DeviceArrays,
                   flags_ptr=None, totals_ptr=None, stream=None):
         """agn_prune_ops: materializer_vnode GC of the device op log (out of place)."""

@@ -204,6 +204,73 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
 int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *new_,
                       int *changed);
 
+/* ---- device snapshot cache -------------------------------------------------
+ * The per-partition ETS snapshot cache of materializer_vnode
+ * (src/materializer_vnode.erl:341-413, 466-563) as a device table: per key a
+ * vector_orddict (src/vector_orddict.erl:36-146) of at most `slots` entries,
+ * newest first, each {commit clock, #materialized_snapshot{last_op_id, value}}
+ * (include/antidote.hrl:169-176).  `value` is the counter_pn value, or for
+ * set_aw / register_mv a caller handle to the state (e.g. an index into the
+ * caller's state store).  Clocks are dense rows (+ optional presence masks;
+ * an empty clock, vectorclock:new(), is all-absent / all-zero). */
+#define AGN_SNAPSHOT_THRESHOLD 10 /* src/materializer_vnode.erl:37 */
+#define AGN_SNAPSHOT_MIN 3        /* :39 */
+#define AGN_MIN_OP_STORE_SS 5     /* :47 */
+typedef struct agn_ss_cache {
+    uint32_t n_dcs;
+    uint32_t slots;        /* >= AGN_SNAPSHOT_THRESHOLD - 1 */
+    uint64_t n_keys;
+    uint32_t *n;           /* [n_keys] entries in use; 0 = key absent from the cache */
+    uint64_t *clock;       /* [n_keys][slots][D] */
+    uint64_t *clock_mask;  /* [n_keys][slots][W] or NULL (dense) */
+    int64_t *last_op;      /* [n_keys][slots] last_op_id */
+    int64_t *value;        /* [n_keys][slots] value / state handle */
+} agn_ss_cache;
+
+/* lookup status */
+#define AGN_SS_HIT 0 /* a cached snapshot <= R: base = it */
+#define AGN_SS_NEW 1 /* key absent: base {ignore, Type:new()}, empty snapshot stored */
+#define AGN_SS_LOG 2 /* no cached snapshot <= R: get_from_snapshot_log (:416-419) */
+
+/* get_from_snapshot_cache/5 (:384-413) for a batch of reads (device
+ * pointers; writes the agn_read fields of the materialize that follows):
+ *  - key absent (n[k] == 0): sct_ignore = 1, base_value = 0, is_first = 1,
+ *    status AGN_SS_NEW, and the empty snapshot {last_op_id 0, value 0} is
+ *    stored at vectorclock:new() (store_snapshot, :398-402);
+ *  - else vector_orddict:get_smaller(R, SD) (src/vector_orddict.erl:74-87):
+ *    the newest entry whose clock <= R: sct (+ sct_mask) = its clock,
+ *    sct_ignore = 0, base_value = its value, is_first = (it is the head),
+ *    status AGN_SS_HIT;
+ *  - no entry <= R: status AGN_SS_LOG, is_first = 0 (the caller falls back
+ *    to the log; agn_ss_store ignores the request).
+ * sct_mask / R_mask may be NULL for dense caches.  Requests of one batch must
+ * name distinct keys. */
+int agn_ss_lookup(agn_ctx *ctx, agn_ss_cache *cache, uint64_t n_req, const uint64_t *keys,
+                  const uint64_t *R, const uint64_t *R_mask, uint64_t *sct, uint64_t *sct_mask,
+                  uint8_t *sct_ignore, int64_t *base_value, uint8_t *is_first, uint8_t *status,
+                  void *stream);
+
+/* The cache half of materialize_snapshot/7 + internal_store_ss/5 +
+ * snapshot_insert_gc/4 (:466-563), after agn_materialize of the same batch
+ * (`res`, device): for a request that materialized (no error, status !=
+ * AGN_SS_LOG, the key has >= 1 op, LastOpCt != ignore):
+ *   refresh = IsNewSS and is_first and Count >= MIN_OP_STORE_SS
+ *   if refresh or should_gc:  ShouldInsert = SD empty or
+ *        NewLastOp - first.last_op_id >= MIN_OP_STORE_SS
+ *     if ShouldInsert or should_gc:  SD1 = insert_bigger(LastOpCt, {NewLastOp,
+ *        value}, SD) (prepend iff not le(LastOpCt, first clock));
+ *        if size(SD1) >= SNAPSHOT_THRESHOLD or should_gc: SD := first
+ *        SNAPSHOT_MIN entries of SD1, prune[k] = 1 and threshold[k] =
+ *        vectorclock:min of their clocks (missing entry = 0) — the input of
+ *        agn_prune_ops; else SD := SD1.
+ * value = handle[i] when handle != NULL, else res->value[i].  should_gc may
+ * be NULL (no GC reads).  prune[n_keys] is cleared first; threshold_mask may
+ * be NULL for dense caches.  Requests of one batch must name distinct keys. */
+int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
+                 const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
+                 const uint8_t *should_gc, const agn_result *res, const int64_t *handle,
+                 uint8_t *prune, uint64_t *threshold, uint64_t *threshold_mask, void *stream);
+
 /* ---- op-log garbage collection ------------------------------------------
  * materializer_vnode:snapshot_insert_gc -> prune_ops/check_filter
  * (src/materializer_vnode.erl:513-604): for every key k with prune[k] != 0

@@ -358,6 +358,139 @@ int oracle_update_stable(uint32_t D, uint64_t *last, const uint64_t *nw, int *ch
     return AGN_OK;
 }
 
+/* ---- snapshot cache: a literal walk of the Erlang, one request at a time ---- */
+static void row_copy(uint64_t *dst, const uint64_t *src, uint32_t n) {
+    for (uint32_t x = 0; x < n; ++x) dst[x] = src[x];
+}
+static void full_mask(uint64_t *m, uint32_t D) {
+    for (uint32_t x = 0; x < W_OF(D); ++x)
+        m[x] = (x + 1 < W_OF(D) || D % 64 == 0) ? ~0ull : ((1ull << (D % 64)) - 1ull);
+}
+
+/* get_from_snapshot_cache/5 (src/materializer_vnode.erl:384-413) with
+ * vector_orddict:get_smaller/2 (src/vector_orddict.erl:74-87). */
+int oracle_ss_lookup(agn_ss_cache *c, uint64_t n_req, const uint64_t *keys, const uint64_t *R,
+                     const uint64_t *Rm, uint64_t *sct, uint64_t *sctm, uint8_t *sct_ign,
+                     int64_t *base, uint8_t *first, uint8_t *status) {
+    const uint32_t D = c->n_dcs, W = W_OF(D), S = c->slots;
+    for (uint64_t i = 0; i < n_req; ++i) {
+        const uint64_t k = keys ? keys[i] : i;
+        if (c->n[k] == 0) { /* [] -> store the empty snapshot at vectorclock:new() */
+            for (uint32_t d = 0; d < D; ++d) c->clock[k * S * D + d] = 0, sct[i * D + d] = 0;
+            for (uint32_t x = 0; x < W; ++x) {
+                if (c->clock_mask) c->clock_mask[k * S * W + x] = 0;
+                if (sctm) sctm[i * W + x] = 0;
+            }
+            c->last_op[k * S] = 0;
+            c->value[k * S] = 0;
+            c->n[k] = 1;
+            sct_ign[i] = 1, base[i] = 0, first[i] = 1, status[i] = AGN_SS_NEW;
+            continue;
+        }
+        int found = -1;
+        for (uint32_t j = 0; j < c->n[k] && found < 0; ++j) {
+            const uint64_t row = k * S + j;
+            if (oracle_vc_le(D, c->clock + row * D, c->clock_mask ? c->clock_mask + row * W : NULL,
+                             R + i * D, Rm ? Rm + i * W : NULL))
+                found = (int)j;
+        }
+        if (found >= 0) {
+            const uint64_t row = k * S + (uint64_t)found;
+            row_copy(sct + i * D, c->clock + row * D, D);
+            if (sctm) {
+                if (c->clock_mask) row_copy(sctm + i * W, c->clock_mask + row * W, W);
+                else full_mask(sctm + i * W, D);
+            }
+        }
+        sct_ign[i] = found >= 0 ? 0 : 1;
+        base[i] = found >= 0 ? c->value[k * S + (uint64_t)found] : 0;
+        first[i] = found == 0;
+        status[i] = found >= 0 ? AGN_SS_HIT : AGN_SS_LOG;
+    }
+    return AGN_OK;
+}
+
+/* materialize_snapshot/7 (:466-509) -> internal_store_ss/5 (:341-364) ->
+ * vector_orddict:insert_bigger/3 (src/vector_orddict.erl:126-140) ->
+ * snapshot_insert_gc/4 (:513-563) up to the prune_ops call, whose threshold
+ * (vectorclock:min of the kept clocks, missing = 0) is returned. */
+int oracle_ss_store(agn_ss_cache *c, const agn_log *log, uint64_t n_req, const uint64_t *keys,
+                    const uint8_t *is_first, const uint8_t *status, const uint8_t *should_gc,
+                    const agn_result *res, const int64_t *handle, uint8_t *prune, uint64_t *thr,
+                    uint64_t *thrm) {
+    const uint32_t D = c->n_dcs, W = W_OF(D), S = c->slots;
+    uint64_t *lst = (uint64_t *)malloc((size_t)(S + 1) * (D + W) * sizeof(uint64_t));
+    int64_t *lop = (int64_t *)malloc((S + 1) * sizeof(int64_t));
+    int64_t *lval = (int64_t *)malloc((S + 1) * sizeof(int64_t));
+    for (uint64_t k = 0; k < c->n_keys; ++k) prune[k] = 0;
+    for (uint64_t i = 0; i < n_req; ++i) {
+        const uint64_t k = keys ? keys[i] : i;
+        if (status[i] == AGN_SS_LOG) continue;
+        if (log->key_off[k + 1] == log->key_off[k]) continue; /* number_of_ops = 0 */
+        const uint32_t fl = res->flags[i];
+        if (fl & (AGN_F_ERR_UNEXPECTED | AGN_F_ERR_CORRUPTED | AGN_F_ERR_CAPACITY)) continue;
+        if (fl & AGN_F_CT_IGNORE) continue; /* CommitTime == ignore */
+        const int gc = should_gc && should_gc[i];
+        const int refresh = (fl & AGN_F_NEWSS) && is_first[i] && res->count[i] >= AGN_MIN_OP_STORE_SS;
+        if (!(refresh || gc)) continue;
+        const int64_t new_op = res->hole[i], val = handle ? handle[i] : res->value[i];
+        const uint32_t n = c->n[k];
+        const int should_insert = n == 0 || new_op - c->last_op[k * S] >= AGN_MIN_OP_STORE_SS;
+        if (!(should_insert || gc)) continue;
+        /* SD as a list: rows of D clock words + W mask words */
+        uint32_t m = 0;
+        const uint64_t *ct = res->lastct + i * D;
+        const uint64_t *ctm = res->lastct_mask ? res->lastct_mask + i * W : NULL;
+        int prepend = n == 0 || !oracle_vc_le(D, ct, ctm, c->clock + k * S * D,
+                                              c->clock_mask ? c->clock_mask + k * S * W : NULL);
+        if (prepend) {
+            row_copy(lst, ct, D);
+            if (ctm) row_copy(lst + D, ctm, W); else full_mask(lst + D, D);
+            lop[0] = new_op, lval[0] = val, m = 1;
+        }
+        for (uint32_t j = 0; j < n; ++j, ++m) {
+            const uint64_t row = k * S + j;
+            row_copy(lst + (size_t)m * (D + W), c->clock + row * D, D);
+            if (c->clock_mask) row_copy(lst + (size_t)m * (D + W) + D, c->clock_mask + row * W, W);
+            else full_mask(lst + (size_t)m * (D + W) + D, D);
+            lop[m] = c->last_op[row], lval[m] = c->value[row];
+        }
+        if (m >= AGN_SNAPSHOT_THRESHOLD || gc) { /* sublist(SD1, 1, SNAPSHOT_MIN) */
+            if (m > AGN_SNAPSHOT_MIN) m = AGN_SNAPSHOT_MIN;
+            /* CommitTime = fold of vectorclock:min([CT1, Acc]) from the last entry */
+            for (uint32_t d = 0; d < D; ++d) {
+                uint64_t mn = UINT64_MAX;
+                int any = 0;
+                for (uint32_t j = 0; j < m; ++j) {
+                    const uint64_t *r = lst + (size_t)j * (D + W);
+                    const int p = (int)((r[D + (d >> 6)] >> (d & 63)) & 1u);
+                    const uint64_t v = p ? r[d] : 0;
+                    any |= p;
+                    if (v < mn) mn = v;
+                }
+                thr[k * D + d] = any ? mn : 0;
+                if (thrm) {
+                    if (d % 64 == 0) thrm[k * W + (d >> 6)] = 0;
+                    if (any) thrm[k * W + (d >> 6)] |= 1ull << (d & 63);
+                }
+            }
+            prune[k] = 1;
+        }
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint64_t row = k * S + j;
+            row_copy(c->clock + row * D, lst + (size_t)j * (D + W), D);
+            if (c->clock_mask) row_copy(c->clock_mask + row * W, lst + (size_t)j * (D + W) + D, W);
+            c->last_op[row] = lop[j];
+            c->value[row] = lval[j];
+        }
+        c->n[k] = m;
+    }
+    free(lst);
+    free(lop);
+    free(lval);
+    return AGN_OK;
+}
+
 /* prune_ops/2 + check_filter/7 (src/materializer_vnode.erl:566-604): walk the
  * key's ops oldest first and keep those for which
  * belongs_to_snapshot_op(Threshold, CommitTime, SnapshotTime) holds, i.e.

@@ -40,6 +40,16 @@ int oracle_select_base(uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off
                        const uint64_t *R, const uint64_t *R_mask,
                        int32_t *out_idx, uint8_t *out_is_first);
 
+/* materializer_vnode snapshot cache (host arrays), same contracts as
+ * agn_ss_lookup / agn_ss_store. */
+int oracle_ss_lookup(agn_ss_cache *cache, uint64_t n_req, const uint64_t *keys, const uint64_t *R,
+                     const uint64_t *R_mask, uint64_t *sct, uint64_t *sct_mask, uint8_t *sct_ignore,
+                     int64_t *base_value, uint8_t *is_first, uint8_t *status);
+int oracle_ss_store(agn_ss_cache *cache, const agn_log *log, uint64_t n_req, const uint64_t *keys,
+                    const uint8_t *is_first, const uint8_t *status, const uint8_t *should_gc,
+                    const agn_result *res, const int64_t *handle, uint8_t *prune,
+                    uint64_t *threshold, uint64_t *threshold_mask);
+
 /* materializer_vnode prune_ops/check_filter over the SoA log (host arrays),
  * same contract as agn_prune_ops (out arrays sized like the input). */
 int oracle_prune_ops(const agn_log *log, const uint8_t *prune, const uint64_t *threshold,
