@@ -66,6 +66,15 @@ class AgnSsCache(C.Structure):
     ]
 
 
+class AgnLogRecords(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64), ("kind", P), ("txid", P), ("key", P), ("commit_dc", P),
+        ("commit_time", P), ("ss", P), ("ss_mask", P), ("eff", P), ("tag", P), ("add_tok", P),
+        ("rem_off", P), ("rem_tok", P),
+    ]
+
+
+REC_OTHER, REC_UPDATE, REC_COMMIT = 0, 1, 2
 SNAPSHOT_THRESHOLD, SNAPSHOT_MIN, MIN_OP_STORE_SS = 10, 3, 5
 SS_HIT, SS_NEW, SS_LOG = 0, 1, 2
 
@@ -102,6 +111,8 @@ PROTOTYPES = {
     "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
     "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),
     "agn_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
+    "agn_log_ingest": (C.c_int, [P, C.POINTER(AgnLogRecords), C.c_uint32, C.c_uint32,
+                                 C.c_uint64, P, P, C.c_uint32, C.POINTER(AgnLog), P, P]),
     "agn_ss_lookup": (C.c_int, [P, C.POINTER(AgnSsCache), C.c_uint64, P, P, P, P, P, P, P, P,
                                 P, P]),
     "agn_ss_store": (C.c_int, [P, C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P, P,
@@ -126,6 +137,8 @@ ORACLE_PROTOTYPES = {
     "oracle_gst_min": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, C.c_int]),
     "oracle_update_stable": (C.c_int, [C.c_uint32, P, P, C.POINTER(C.c_int)]),
     "oracle_select_base": (C.c_int, [C.c_uint32, C.c_uint64, P, P, P, P, P, P, P]),
+    "oracle_log_ingest": (C.c_int, [C.POINTER(AgnLogRecords), C.c_uint32, C.c_uint32,
+                                    C.c_uint64, P, P, C.c_uint32, C.POINTER(AgnLog)]),
     "oracle_ss_lookup": (C.c_int, [C.POINTER(AgnSsCache), C.c_uint64, P, P, P, P, P, P, P, P,
                                    P]),
     "oracle_ss_store": (C.c_int, [C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P,

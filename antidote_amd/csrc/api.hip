@@ -339,6 +339,48 @@ int agn_gst_finalize(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *
     return launch_gst_finalize(n_dcs, n_epochs, vec, (hipStream_t)stream);
 }
 
+int agn_log_ingest(agn_ctx *ctx, const agn_log_records *recs, uint32_t crdt_type,
+                   uint32_t n_dcs, uint64_t n_keys, const uint64_t *max_time,
+                   const uint64_t *max_time_mask, uint32_t op_id_base, agn_log *out,
+                   uint64_t *out_totals, void *stream) {
+    if (!recs || !out) return fail(AGN_EINVAL, "log_ingest: null descriptor");
+    if (n_dcs == 0 || n_dcs > 256) return fail(AGN_EINVAL, "log_ingest: n_dcs=%u", n_dcs);
+    if (crdt_type != AGN_COUNTER_PN && !is_tag_type(crdt_type))
+        return fail(AGN_EINVAL, "log_ingest: crdt_type %u", crdt_type);
+    if (n_keys >= (1ull << 24)) return fail(AGN_ENOTSUP, "log_ingest: n_keys >= 2^24");
+    if (recs->n >= 0x7fffffffull) return fail(AGN_ENOTSUP, "log_ingest: n >= 2^31 records");
+    if (recs->n && (!recs->kind || !recs->txid || !recs->key || !recs->commit_dc ||
+                    !recs->commit_time || !recs->ss))
+        return fail(AGN_EINVAL, "log_ingest: null record array");
+    if (crdt_type == AGN_COUNTER_PN ? !recs->eff
+                                    : (!recs->tag || !recs->add_tok || !recs->rem_off))
+        return fail(AGN_EINVAL, "log_ingest: effect arrays missing for type %u", crdt_type);
+    if (!out->key_off || !out->oc || !out->op_id || (recs->ss_mask && !out->oc_mask) ||
+        (crdt_type == AGN_COUNTER_PN ? !out->eff
+                                     : (!out->tag || !out->add_tok || !out->rem_off)))
+        return fail(AGN_EINVAL, "log_ingest: out arrays missing");
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    agn_log_records r = *recs;
+    if (crdt_type == AGN_COUNTER_PN) r.tag = nullptr, r.add_tok = nullptr, r.rem_off = nullptr,
+                                     r.rem_tok = nullptr;
+    else r.eff = nullptr;
+    agn_log o = *out;
+    if (crdt_type == AGN_COUNTER_PN) o.tag = nullptr, o.add_tok = nullptr, o.rem_off = nullptr,
+                                     o.rem_tok = nullptr;
+    else o.eff = nullptr;
+    out->crdt_type = crdt_type;
+    out->n_dcs = n_dcs;
+    out->n_keys = n_keys;
+    if (recs->n == 0) {
+        AGN_HIP(hipMemsetAsync((void *)out->key_off, 0, (n_keys + 1) * 8, (hipStream_t)stream));
+        if (out_totals) AGN_HIP(hipMemsetAsync(out_totals, 0, 16, (hipStream_t)stream));
+        return AGN_OK;
+    }
+    return launch_log_ingest(r, n_dcs, n_keys, max_time, max_time_mask, op_id_base, o, out_totals,
+                             (hipStream_t)stream);
+}
+
 static int check_cache(const agn_ss_cache *c) {
     if (!c) return fail(AGN_EINVAL, "ss cache: null");
     if (c->n_dcs == 0 || c->n_dcs > 256) return fail(AGN_EINVAL, "ss cache: n_dcs=%u", c->n_dcs);

@@ -93,6 +93,9 @@ int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
 int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
                    const uint8_t *defined, uint64_t *out, hipStream_t s);
 int launch_gst_finalize(uint32_t D, uint64_t E, uint64_t *vec, hipStream_t s);
+int launch_log_ingest(const agn_log_records &r, uint32_t D, uint64_t n_keys,
+                      const uint64_t *max_t, const uint64_t *max_m, uint32_t base,
+                      const agn_log &out, uint64_t *totals, hipStream_t st);
 int launch_ss_lookup(const agn_ss_cache &c, uint64_t n_req, const uint64_t *keys,
                      const uint64_t *R, const uint64_t *Rm, uint64_t *sct, uint64_t *sctm,
                      uint8_t *sct_ign, int64_t *base, uint8_t *first, uint8_t *status,

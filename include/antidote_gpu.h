@@ -271,6 +271,50 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
                  const uint8_t *should_gc, const agn_result *res, const int64_t *handle,
                  uint8_t *prune, uint64_t *threshold, uint64_t *threshold_mask, void *stream);
 
+/* ---- log-read fallback and recovery ingest ------------------------------
+ * A partition's logging_vnode disk log, decoded into records in log order
+ * (#log_record{} -> #log_operation{tx_id, op_type, log_payload},
+ * include/antidote.hrl:120-145).  Update records carry the key and the
+ * effect (same encodings as agn_log); commit records the commit
+ * {DcId, Time} and the transaction's snapshot_time. */
+#define AGN_REC_OTHER 0   /* prepare / abort / noop: ignored */
+#define AGN_REC_UPDATE 1
+#define AGN_REC_COMMIT 2
+typedef struct agn_log_records {
+    uint64_t n;
+    const uint8_t *kind;         /* [n] AGN_REC_* */
+    const uint64_t *txid;        /* [n] */
+    const uint64_t *key;         /* [n] update: key index (< n_keys) */
+    const uint32_t *commit_dc;   /* [n] commit: DC index of commit_time */
+    const uint64_t *commit_time; /* [n] commit */
+    const uint64_t *ss;          /* [n][D] commit: snapshot_time rows */
+    const uint64_t *ss_mask;     /* [n][W] or NULL (dense) */
+    const int64_t *eff;          /* update effects, as in agn_log */
+    const uint32_t *tag;
+    const uint64_t *add_tok;
+    const uint32_t *rem_off;     /* [n+1] */
+    const uint64_t *rem_tok;
+} agn_log_records;
+
+/* logging_vnode get_ops_from_log / filter_terms_for_key / handle_commit
+ * (src/logging_vnode.erl:522-549, 660-779) for every key at once: an update
+ * is committed by the first later commit record of its transaction; it is
+ * emitted iff check_max_time(CommitSnapshotTime, MaxSnapshotTime) holds
+ * (max_time[n_keys][D] + mask per key, NULL = undefined, i.e. recovery
+ * get_all); per key the emitted ops keep commit order, then update order
+ * (dict:append), and become the device op log `out` (caller-allocated
+ * arrays of >= the update count): OpSSCommit = snapshot_time with the commit
+ * DC replaced by the commit time (src/clocksi_materializer.erl:224),
+ * op_id = op_id_base + rank (0 for the get_up_to_time response of
+ * reverse_and_add_op_id, :586-591; 1 for the op_insert_gc ids of
+ * load_from_log, src/materializer_vnode.erl:288-319), txid = the
+ * transaction id.  out_totals (device, may be NULL) = {ops, removal tokens}.
+ * Requires n_keys < 2^24 and n < 2^40. */
+int agn_log_ingest(agn_ctx *ctx, const agn_log_records *recs, uint32_t crdt_type,
+                   uint32_t n_dcs, uint64_t n_keys, const uint64_t *max_time,
+                   const uint64_t *max_time_mask, uint32_t op_id_base, agn_log *out,
+                   uint64_t *out_totals, void *stream);
+
 /* ---- op-log garbage collection ------------------------------------------
  * materializer_vnode:snapshot_insert_gc -> prune_ops/check_filter
  * (src/materializer_vnode.erl:513-604): for every key k with prune[k] != 0

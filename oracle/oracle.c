@@ -358,6 +358,93 @@ int oracle_update_stable(uint32_t D, uint64_t *last, const uint64_t *nw, int *ch
     return AGN_OK;
 }
 
+/* ---- logging_vnode filter_terms_for_key (src/logging_vnode.erl:722-779) ----
+ * Walk the records in log order.  Ops (dict TxId -> buffered updates):
+ * handle_update appends the update to its transaction's list; handle_commit
+ * takes the list (if any), and for every buffered update, if
+ * check_max_time(SnapshotTime, Max) holds, dict:append(Key, #clocksi_payload{})
+ * to CommittedOpsDict; then erases the transaction.  Each key's list ends up
+ * in append order; op ids are base + position (reverse_and_add_op_id). */
+typedef struct { uint64_t txid; int64_t head, tail; int used; } txslot;
+
+int oracle_log_ingest(const agn_log_records *r, uint32_t crdt, uint32_t D, uint64_t K,
+                      const uint64_t *max_t, const uint64_t *max_m, uint32_t base, agn_log *out) {
+    const uint32_t W = W_OF(D);
+    const uint64_t n = r->n;
+    uint64_t T = 16;
+    while (T < 2 * n + 2) T <<= 1;
+    txslot *tab = (txslot *)calloc(T, sizeof(txslot));
+    int64_t *next = (int64_t *)malloc((n + 1) * sizeof(int64_t));
+    /* committed ops per key as linked lists of (update, commit) in append order */
+    int64_t *khead = (int64_t *)malloc((K + 1) * sizeof(int64_t));
+    int64_t *ktail = (int64_t *)malloc((K + 1) * sizeof(int64_t));
+    int64_t *knext = (int64_t *)malloc((n + 1) * sizeof(int64_t));
+    uint64_t *kcommit = (uint64_t *)malloc((n + 1) * sizeof(uint64_t));
+    for (uint64_t k = 0; k < K; ++k) khead[k] = ktail[k] = -1;
+    for (uint64_t x = 0; x < n; ++x) {
+        const uint64_t t = r->txid[x];
+        uint64_t s = (t * 0x9E3779B97F4A7C15ull >> 17) & (T - 1);
+        while (tab[s].used && tab[s].txid != t) s = (s + 1) & (T - 1);
+        if (r->kind[x] == AGN_REC_UPDATE) { /* dict:append(TxId, OpPayload, Ops) */
+            if (!tab[s].used) { tab[s].used = 1; tab[s].txid = t; tab[s].head = tab[s].tail = -1; }
+            next[x] = -1;
+            if (tab[s].tail < 0) tab[s].head = (int64_t)x; else next[tab[s].tail] = (int64_t)x;
+            tab[s].tail = (int64_t)x;
+        } else if (r->kind[x] == AGN_REC_COMMIT) {
+            if (!tab[s].used || tab[s].head < 0) continue; /* dict:find -> error */
+            for (int64_t u = tab[s].head; u >= 0; u = next[u]) {
+                const uint64_t k = r->key[u];
+                int ok = 1;
+                if (max_t) /* check_max_time: vectorclock:le(SnapshotTime, Max) */
+                    ok = oracle_vc_le(D, r->ss + x * D, r->ss_mask ? r->ss_mask + x * W : NULL,
+                                      max_t + k * D, max_m ? max_m + k * W : NULL);
+                if (!ok) continue;
+                knext[u] = -1;
+                kcommit[u] = x;
+                if (ktail[k] < 0) khead[k] = u; else knext[ktail[k]] = u;
+                ktail[k] = u;
+            }
+            tab[s].head = tab[s].tail = -1; /* dict:erase(TxId, Ops) */
+        }
+    }
+    uint64_t *ko = (uint64_t *)out->key_off, *oc = (uint64_t *)out->oc, *om = (uint64_t *)out->oc_mask;
+    uint32_t *id = (uint32_t *)out->op_id;
+    uint64_t w = 0, rw = 0;
+    ko[0] = 0;
+    if (out->rem_off && crdt != AGN_COUNTER_PN) ((uint32_t *)out->rem_off)[0] = 0;
+    for (uint64_t k = 0; k < K; ++k) {
+        uint32_t rank = 0;
+        for (int64_t u = khead[k]; u >= 0; u = knext[u], ++w, ++rank) {
+            const uint64_t c = kcommit[u];
+            for (uint32_t d = 0; d < D; ++d)
+                oc[w * D + d] = d == r->commit_dc[c] ? r->commit_time[c] : r->ss[c * D + d];
+            if (om) {
+                for (uint32_t x2 = 0; x2 < W; ++x2) om[w * W + x2] = r->ss_mask ? r->ss_mask[c * W + x2] : ~0ull;
+                om[w * W + (r->commit_dc[c] >> 6)] |= 1ull << (r->commit_dc[c] & 63);
+                if (D % 64) om[w * W + W - 1] &= (1ull << (D % 64)) - 1ull;
+            }
+            id[w] = base + rank;
+            if (out->txid) ((uint64_t *)out->txid)[w] = r->txid[u];
+            if (crdt == AGN_COUNTER_PN) {
+                ((int64_t *)out->eff)[w] = r->eff[u];
+            } else {
+                ((uint32_t *)out->tag)[w] = r->tag[u];
+                ((uint64_t *)out->add_tok)[w] = r->add_tok[u];
+                for (uint32_t q = r->rem_off[u]; q < r->rem_off[u + 1]; ++q)
+                    ((uint64_t *)out->rem_tok)[rw++] = r->rem_tok[q];
+                ((uint32_t *)out->rem_off)[w + 1] = (uint32_t)rw;
+            }
+        }
+        ko[k + 1] = w;
+    }
+    out->crdt_type = crdt;
+    out->n_dcs = D;
+    out->n_keys = K;
+    out->n_entries = w;
+    free(tab); free(next); free(khead); free(ktail); free(knext); free(kcommit);
+    return AGN_OK;
+}
+
 /* ---- snapshot cache: a literal walk of the Erlang, one request at a time ---- */
 static void row_copy(uint64_t *dst, const uint64_t *src, uint32_t n) {
     for (uint32_t x = 0; x < n; ++x) dst[x] = src[x];

@@ -40,6 +40,13 @@ int oracle_select_base(uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off
                        const uint64_t *R, const uint64_t *R_mask,
                        int32_t *out_idx, uint8_t *out_is_first);
 
+/* logging_vnode filter_terms_for_key / handle_commit over decoded records
+ * (host arrays), same contract as agn_log_ingest (out arrays sized >= the
+ * update count; out->n_entries is set). */
+int oracle_log_ingest(const agn_log_records *recs, uint32_t crdt_type, uint32_t n_dcs,
+                      uint64_t n_keys, const uint64_t *max_time, const uint64_t *max_time_mask,
+                      uint32_t op_id_base, agn_log *out);
+
 /* materializer_vnode snapshot cache (host arrays), same contracts as
  * agn_ss_lookup / agn_ss_store. */
 int oracle_ss_lookup(agn_ss_cache *cache, uint64_t n_req, const uint64_t *keys, const uint64_t *R,

@@ -1,0 +1,5 @@
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_ingest.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ingest.log 2>&1 || { echo "pytest rc=$?"; tail -40 gpurun_out/pytest_ingest.log; exit 1; }
+tail -1 gpurun_out/pytest_ingest.log
