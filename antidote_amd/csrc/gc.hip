@@ -26,7 +26,7 @@
 namespace agn {
 namespace {
 
-template <int DPL, int LPO, bool SPARSE>
+template <int DPL, int LPO, bool SPARSE, bool FULL>
 __global__ __launch_bounds__(256) void k_prune_mark(agn_log log, const uint8_t *__restrict__ prune,
                                                     const uint64_t *__restrict__ thr,
                                                     const uint64_t *__restrict__ thr_mask,
@@ -54,10 +54,13 @@ __global__ __launch_bounds__(256) void k_prune_mark(agn_log log, const uint8_t *
         const uint64_t e = off + (valid ? pos : 0ull);
         bool le = true;
         if (gc) {
-            const uint32_t obits = valid ? chunk_bits<DPL, SPARSE>(log.oc_mask, e, W, d0, D) : 0u;
+            uint64_t o[DPL];
+            uint32_t obits;
+            load_rows<DPL, SPARSE, FULL>(log, e, d0, D, W, o, obits);
+            if (!valid) obits = 0u;
 #pragma unroll
             for (int j = 0; j < DPL; ++j)
-                if ((obits >> j) & 1u) le = le && (log.oc[e * D + (uint32_t)(d0 + j)] <= t[j]);
+                if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
             if (LPO > 1) {
                 const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
                 le = (ballot(!le) & grp) == 0ull;
@@ -121,10 +124,17 @@ __global__ __launch_bounds__(256) void k_prune_scatter(agn_log log, agn_log out,
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // kept OpSSCommit rows (and masks): rank-major, lane-contiguous copy
+        // (16-byte units when D is even)
         uint64_t *ooc = (uint64_t *)out.oc + (noff + written) * D;
-        for (uint64_t x = (uint64_t)lane; x < (uint64_t)nk * D; x += AGN_WAVE) {
-            const uint64_t r = x / D, d = x % D;
-            ooc[x] = log.oc[src[w][r] * D + d];
+        if ((D & 1u) == 0u) {
+            const uint32_t H = D / 2;
+            u64x2 *o2 = reinterpret_cast<u64x2 *>(ooc);
+            const u64x2 *i2 = reinterpret_cast<const u64x2 *>(log.oc);
+            for (uint64_t x = (uint64_t)lane; x < (uint64_t)nk * H; x += AGN_WAVE)
+                o2[x] = i2[src[w][x / H] * H + x % H];
+        } else {
+            for (uint64_t x = (uint64_t)lane; x < (uint64_t)nk * D; x += AGN_WAVE)
+                ooc[x] = log.oc[src[w][x / D] * D + x % D];
         }
         if (log.oc_mask) {
             uint64_t *om = (uint64_t *)out.oc_mask + (noff + written) * W;
@@ -160,8 +170,14 @@ int mark_shape(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
                const uint64_t *thr_mask, uint8_t *keep, uint64_t *cnt, uint64_t *rcnt,
                hipStream_t st) {
     const unsigned blocks = grid_for(log.n_keys, 4, 0x7fffffffu);
-    hipLaunchKernelGGL((k_prune_mark<DPL, LPO, SPARSE>), dim3(blocks), dim3(256), 0, st, log,
-                       prune, thr, thr_mask, keep, cnt, rcnt);
+    // FULL: dense rows that split exactly into 16-byte loads
+    const bool full = !log.oc_mask && (DPL % 2 == 0) && log.n_dcs == (uint32_t)(DPL * LPO);
+    if (full)
+        hipLaunchKernelGGL((k_prune_mark<DPL, LPO, SPARSE, (DPL % 2 == 0)>), dim3(blocks),
+                           dim3(256), 0, st, log, prune, thr, thr_mask, keep, cnt, rcnt);
+    else
+        hipLaunchKernelGGL((k_prune_mark<DPL, LPO, SPARSE, false>), dim3(blocks), dim3(256), 0,
+                           st, log, prune, thr, thr_mask, keep, cnt, rcnt);
     return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_mark launch");
 }
 

@@ -45,7 +45,6 @@ namespace {
 constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t NIL = 0xffffffffu;
 
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
 template <int CAP>
 struct CandLds {
@@ -158,27 +157,6 @@ __device__ __forceinline__ void bitonic(CandLds<CAP> &L, uint32_t n) {
             }
             wave_sync();
         }
-    }
-}
-
-// One sub-iteration's OpSSCommit slice: DPL DCs of one op per lane.
-template <int DPL, bool SPARSE, bool FULL>
-__device__ __forceinline__ void load_rows(const agn_log &log, uint64_t e, int d0, uint32_t D,
-                                          uint32_t W, uint64_t (&v)[DPL], uint32_t &bits) {
-    if constexpr (FULL) {
-        const u64x2 *q = reinterpret_cast<const u64x2 *>(log.oc + e * D + (uint32_t)d0);
-#pragma unroll
-        for (int j = 0; j < DPL / 2; ++j) {
-            const u64x2 x = q[j];
-            v[2 * j] = x.x;
-            v[2 * j + 1] = x.y;
-        }
-        bits = (1u << DPL) - 1u;
-    } else {
-        bits = chunk_bits<DPL, SPARSE>(log.oc_mask, e, W, d0, D);
-#pragma unroll
-        for (int j = 0; j < DPL; ++j)
-            v[j] = ((bits >> j) & 1u) ? log.oc[e * D + (uint32_t)(d0 + j)] : 0ull;
     }
 }
 
