@@ -58,6 +58,9 @@ def parse():
                     help="CPU-baseline sample size in keys (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="extra multi-thread CPU run")
     ap.add_argument("--gst", action="store_true", help="also time a GST epoch + RCCL min-allreduce")
+    ap.add_argument("--warm", action="store_true",
+                    help="also time the warm read path through the device snapshot cache "
+                         "(agn_ss_lookup -> agn_materialize -> agn_ss_store)")
     ap.add_argument("--gc", action="store_true",
                     help="also time the op-log GC (agn_prune_ops) over the whole log")
     return ap.parse_args()
@@ -187,6 +190,7 @@ def main():
     probe = probe_read_gbs(eng, dl, n_keys * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
 
     gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch) if a.gc else None
+    warm = warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.steps) if a.warm else None
 
     gst = None
     if a.gst:
@@ -236,12 +240,79 @@ def main():
             line["gst"] = gst
         if gc:
             line["gc"] = gc
+        if warm:
+            line["warm"] = warm
         print(json.dumps(line), flush=True)
 
     eng.free_gen(dl, dr)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
+    """materializer_vnode:read/6 served from the device snapshot cache: one
+    priming pass stores each key's snapshot (IsNewSS, >= 5 ops), then every
+    timed step is get_from_snapshot_cache (agn_ss_lookup) -> materialize/4
+    from the cached base (SCT, base value: the warm filter, two compares per
+    op) -> the cache policy (agn_ss_store)."""
+    from antidote_amd import _abi
+    D = cfg["n_dcs"]
+    if cfg["crdt_type"] != 1:
+        return None  # set/register states need a caller state store for the handles
+    S = _abi.SNAPSHOT_THRESHOLD
+    bufs = {"n": eng.empty(4 * n_keys), "clock": eng.empty(8 * n_keys * S * D),
+            "last_op": eng.empty(8 * n_keys * S), "value": eng.empty(8 * n_keys * S),
+            "sct": eng.empty(8 * n_keys * D), "ign": eng.empty(n_keys), "base": eng.empty(8 * n_keys),
+            "first": eng.empty(n_keys), "status": eng.empty(n_keys), "prune": eng.empty(n_keys),
+            "thr": eng.empty(8 * n_keys * D)}
+    eng.lib.agn_memset_d(eng.ctx, bufs["n"].ptr, 0, 4 * n_keys, sp)
+    c = _abi.AgnSsCache()
+    c.n_dcs, c.slots, c.n_keys = D, S, n_keys
+    c.n, c.clock, c.last_op, c.value = (bufs[x].ptr for x in ("n", "clock", "last_op", "value"))
+    req = _abi.AgnRead()
+    C.memmove(C.addressof(req), C.addressof(dr), C.sizeof(_abi.AgnRead))
+    req.sct, req.sct_ignore, req.base_value = bufs["sct"].ptr, bufs["ign"].ptr, bufs["base"].ptr
+    res = eng.alloc_result(n_keys, D, sparse=False)
+
+    def step():
+        eng.ss_lookup(c, n_keys, None, dr.R, None, bufs["sct"].ptr, None, bufs["ign"].ptr,
+                      bufs["base"].ptr, bufs["first"].ptr, bufs["status"].ptr, sp)
+        eng.materialize(dl, req, res, sp)
+        eng.ss_store(c, dl, n_keys, None, bufs["first"].ptr, bufs["status"].ptr, None, res, None,
+                     bufs["prune"].ptr, bufs["thr"].ptr, None, sp)
+    step()  # priming: absent keys -> empty snapshot -> cold read -> store
+    step()
+    torch.cuda.synchronize()
+    hits = eng.download(bufs["status"], np.uint8, (n_keys,))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t_lookup = t_mat = t_store = 0.0
+    for _ in range(steps):
+        ev[0].record()
+        eng.ss_lookup(c, n_keys, None, dr.R, None, bufs["sct"].ptr, None, bufs["ign"].ptr,
+                      bufs["base"].ptr, bufs["first"].ptr, bufs["status"].ptr, sp)
+        ev[1].record()
+        eng.materialize(dl, req, res, sp)
+        ev[2].record()
+        eng.ss_store(c, dl, n_keys, None, bufs["first"].ptr, bufs["status"].ptr, None, res, None,
+                     bufs["prune"].ptr, bufs["thr"].ptr, None, sp)
+        ev[3].record()
+        torch.cuda.synchronize()
+        t_lookup += ev[0].elapsed_time(ev[1])
+        t_mat += ev[1].elapsed_time(ev[2])
+        t_store += ev[2].elapsed_time(ev[3])
+    ms = (t_lookup + t_mat + t_store) / steps
+    flags = eng.download(res.bufs["flags"], np.uint32, (n_keys,))
+    cnt = eng.download(res.bufs["count"], np.uint32, (n_keys,))
+    for b in list(bufs.values()) + list(res.bufs.values()):
+        b.free()
+    ops = n_keys * cfg["ops_per_key"]
+    return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
+            "store_ms": t_store / steps, "ops_per_s": ops / (ms * 1e-3),
+            "vc_compares_per_s": 2 * ops / (ms * 1e-3),
+            "cache_hit_frac": float((hits == _abi.SS_HIT).mean()),
+            "mean_applied_ops": float(cnt.mean()),
+            "error_keys": int((flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED)).astype(bool).sum())}
 
 
 def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
