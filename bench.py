@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--warm", action="store_true",
                     help="also time the warm read path through the device snapshot cache "
                          "(agn_ss_lookup -> agn_materialize -> agn_ss_store)")
+    ap.add_argument("--ingest", action="store_true",
+                    help="also time the log-read / recovery ingest (agn_log_ingest) of a "
+                         "synthetic partition log")
     ap.add_argument("--gc", action="store_true",
                     help="also time the op-log GC (agn_prune_ops) over the whole log")
     return ap.parse_args()
@@ -191,6 +194,7 @@ def main():
 
     gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch) if a.gc else None
     warm = warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.steps) if a.warm else None
+    ingest = ingest_bench(eng, cfg, sp, torch) if a.ingest else None
 
     gst = None
     if a.gst:
@@ -242,12 +246,78 @@ def main():
             line["gc"] = gc
         if warm:
             line["warm"] = warm
+        if ingest:
+            line["ingest"] = ingest
         print(json.dumps(line), flush=True)
 
     eng.free_gen(dl, dr)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def ingest_bench(eng, cfg, sp, torch, n_txn=10_000_000, n_keys=1_000_000):
+    """logging_vnode recovery ingest (load_from_log -> get_all ->
+    filter_terms_for_key) of a synthetic partition log: n_txn transactions of
+    2 counter updates + 1 commit each, 4-way interleaved, D = cfg's DCs."""
+    from antidote_amd import _abi
+    D = cfg["n_dcs"]
+    rng = np.random.default_rng(11)
+    n = 3 * n_txn
+    # transaction t's records: updates at 3t, 3t+1, commit at 3t+2, then the
+    # stream of 4 consecutive transactions is interleaved (u u u u u u u u c c c c)
+    t = np.arange(n_txn, dtype=np.uint64)
+    kind = np.empty(n, np.uint8)
+    txid = np.empty(n, np.uint64)
+    blk = n_txn // 4 * 4
+    idx = np.arange(blk).reshape(-1, 4)
+    base = (idx // 4 * 4)[:, :1] * 3
+    for j in range(4):  # updates first, then the four commits
+        u0 = (base[:, 0] + 2 * j)
+        kind[u0], kind[u0 + 1] = 1, 1
+        txid[u0], txid[u0 + 1] = t[idx[:, j]], t[idx[:, j]]
+        c = base[:, 0] + 8 + j
+        kind[c], txid[c] = 2, t[idx[:, j]]
+    rest = np.arange(blk, n_txn)
+    kind[3 * rest], kind[3 * rest + 1], kind[3 * rest + 2] = 1, 1, 2
+    txid[3 * rest] = txid[3 * rest + 1] = txid[3 * rest + 2] = t[rest]
+    key = rng.integers(0, n_keys, n).astype(np.uint64)
+    cdc = rng.integers(0, D, n).astype(np.uint32)
+    ss = (1_700_000_000_000_000 + rng.integers(0, 10 ** 6, (n, D))).astype(np.uint64)
+    ct = ss.max(axis=1) + np.uint64(1)
+    eff = rng.integers(-1000, 1000, n).astype(np.int64)
+    dev = {k: eng.upload(v) for k, v in dict(kind=kind, txid=txid, key=key, commit_dc=cdc,
+                                                commit_time=ct, ss=ss, eff=eff).items()}
+    r = _abi.AgnLogRecords()
+    r.n = n
+    for k, b in dev.items():
+        setattr(r, k, b.ptr)
+    n_upd = 2 * n_txn
+    out = {"key_off": eng.empty(8 * (n_keys + 1)), "oc": eng.empty(8 * n_upd * D),
+           "op_id": eng.empty(4 * n_upd), "txid": eng.empty(8 * n_upd), "eff": eng.empty(8 * n_upd)}
+    o = _abi.AgnLog()
+    for k, b in out.items():
+        setattr(o, k, b.ptr)
+    tot = eng.empty(16)
+
+    def run():
+        rc = eng.lib.agn_log_ingest(eng.ctx, C.byref(r), 1, D, n_keys, None, None, 1, C.byref(o),
+                                    tot.ptr, sp)
+        assert rc == 0, eng.lib.agn_last_error()
+    run()
+    torch.cuda.synchronize()
+    b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b.record()
+    for _ in range(3):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    ms = b.elapsed_time(e) / 3
+    emitted = int(eng.download(tot, np.uint64, (2,))[0])
+    for bb in list(dev.values()) + list(out.values()) + [tot]:
+        bb.free()
+    return {"records": n, "ops_out": emitted, "ms": ms, "records_per_s": n / (ms * 1e-3),
+            "ops_per_s": emitted / (ms * 1e-3), "n_keys": n_keys, "n_dcs": D}
 
 
 def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
