@@ -82,35 +82,48 @@ def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0):
     return ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key
 
 
-def cpu_baseline(cfg, n_keys, threads):
+def cpu_baseline(cfg, n_keys, threads, target_s=10.0):
     """The C oracle (oracle/liboracle.so, a restatement of the Erlang path) on a
-    bounded host-generated sample of the same workload."""
+    bounded host-generated sample of the same workload.  Each chunk of the
+    sample is materialized `reps` times so that the timed CPU work is about
+    target_s seconds per thread count (reps from the first chunk's rate)."""
     from antidote_amd import _abi
     from antidote_amd.encode import alloc_result, result_struct
     from antidote_amd.engine import free_gen_host, gen_host
     lib = _abi.bind(C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so")), _abi.ORACLE_PROTOTYPES)
     chunk = min(n_keys, 500_000 if cfg["n_dcs"] <= 16 else 100_000)
-    out = {}
-    for nt in ([1] + ([threads] if threads > 1 else [])):
-        done, secs = 0, 0.0
-        while done < n_keys:
-            k = min(chunk, n_keys - done)
-            g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=cfg["n_dcs"], n_keys=k,
-                               ops_per_key=cfg["ops_per_key"], n_elems=cfg["n_elems"],
-                               seed=cfg["seed"], key_base=done, key_stride=1, warm=0)
-            hl, hr = gen_host(g)
-            cap = (np.arange(k + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
-                   if cfg["crdt_type"] != 1 else None)
-            res = alloc_result(k, cfg["n_dcs"], sparse=False, cap_off=cap)
-            os_ = result_struct(res)
-            t0 = time.perf_counter()
-            rc = lib.oracle_materialize(C.byref(hl), C.byref(hr), C.byref(os_), nt)
-            secs += time.perf_counter() - t0
-            free_gen_host(hl, hr)
-            assert rc == 0
-            done += k
-        out[nt] = n_keys * cfg["ops_per_key"] / secs
-    return out
+    n_chunks = (n_keys + chunk - 1) // chunk
+    tcounts = [1] + ([threads] if threads > 1 else [])
+    secs = {nt: 0.0 for nt in tcounts}
+    work = {nt: 0 for nt in tcounts}
+    reps = {nt: 0 for nt in tcounts}
+    done = 0
+    while done < n_keys:
+        k = min(chunk, n_keys - done)
+        g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=cfg["n_dcs"], n_keys=k,
+                           ops_per_key=cfg["ops_per_key"], n_elems=cfg["n_elems"],
+                           seed=cfg["seed"], key_base=done, key_stride=1, warm=0)
+        hl, hr = gen_host(g)
+        cap = (np.arange(k + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
+               if cfg["crdt_type"] != 1 else None)
+        res = alloc_result(k, cfg["n_dcs"], sparse=False, cap_off=cap)
+        os_ = result_struct(res)
+        for nt in tcounts:
+            r = 0
+            while True:
+                t0 = time.perf_counter()
+                rc = lib.oracle_materialize(C.byref(hl), C.byref(hr), C.byref(os_), nt)
+                secs[nt] += time.perf_counter() - t0
+                assert rc == 0
+                work[nt] += k * cfg["ops_per_key"]
+                r += 1
+                if not reps[nt]:  # first chunk: size the repetitions
+                    reps[nt] = max(1, int(np.ceil(target_s / (secs[nt] * n_chunks))))
+                if r >= reps[nt]:
+                    break
+        free_gen_host(hl, hr)
+        done += k
+    return {nt: work[nt] / secs[nt] for nt in tcounts}, {nt: secs[nt] for nt in tcounts}, reps
 
 
 def main():
@@ -202,14 +215,16 @@ def main():
 
     if rank == 0:
         cpu = None
-        n_cpu = a.cpu_keys if a.cpu_keys >= 0 else (2_000_000 if cfg["n_dcs"] <= 16 else 200_000)
+        # ~64M ops of host-generated sample, timed for ~10 s per thread count
+        n_cpu = a.cpu_keys if a.cpu_keys >= 0 else 64_000_000 // cfg["ops_per_key"]
         if world == 1 and n_cpu > 0:
             thr = a.cpu_threads or min(16, os.cpu_count() or 1)
-            rates = cpu_baseline(cfg, min(n_cpu, n_keys), thr)
+            rates, secs, reps = cpu_baseline(cfg, min(n_cpu, n_keys), thr)
             cpu = {"value": rates[1], "unit": "ops/s", "cores": 1, "kind": "port",
                    "sample": f"{min(n_cpu, n_keys)} keys x {cfg['ops_per_key']} ops of the same "
                              f"workload (host-generated, same SplitMix64 streams), "
-                             f"oracle/oracle.c -O3, 1 thread",
+                             f"oracle/oracle.c -O3, 1 thread, {reps[1]} pass(es) = "
+                             f"{secs[1]:.1f} s of CPU time",
                    "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
         traffic = None
