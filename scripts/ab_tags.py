@@ -23,7 +23,7 @@ for c in (3, 4):
     res = eng.alloc_result(K, cfg["n_dcs"], sparse=False, cap_off=cap)
     E = K * cfg["ops_per_key"]
     n_rem = int(eng.download(type("B", (), {"ptr": dl.rem_off})(), np.uint32, (E + 1,))[-1])
-    GR = ["2048", "8192", "32768", "0"]
+    GR = ["0"]
     times = {x: [] for x in GR}
     outs = {}
     for rnd in range(6):
