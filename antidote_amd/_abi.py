@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK = 0
 EINVAL, EHIP, ENOMEM, ECAPACITY, ENOTSUP, ERCCL, ENODEV = -1, -2, -3, -4, -5, -6, -7
@@ -36,7 +36,7 @@ class AgnLog(C.Structure):
     _fields_ = [
         ("crdt_type", C.c_uint32), ("n_dcs", C.c_uint32),
         ("n_keys", C.c_uint64), ("n_entries", C.c_uint64),
-        ("key_off", P), ("key_type", P), ("oc", P), ("oc_mask", P),
+        ("key_off", P), ("key_len", P), ("key_type", P), ("oc", P), ("oc_mask", P),
         ("op_id", P), ("txid", P), ("eff", P),
         ("tag", P), ("add_tok", P), ("rem_off", P), ("rem_tok", P),
     ]

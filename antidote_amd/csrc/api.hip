@@ -197,7 +197,8 @@ int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_of
         const uint64_t k = req->keys ? req->keys[i] : i;
         uint64_t c = 0;
         if (log->add_tok)
-            for (uint64_t e = log->key_off[k]; e < log->key_off[k + 1]; ++e) c += log->add_tok[e] != 0;
+            for (uint64_t e = log->key_off[k]; e < log->key_off[k] + key_n(log->key_off, log->key_len, k); ++e)
+                c += log->add_tok[e] != 0;
         if (req->base_off) c += req->base_off[i + 1] - req->base_off[i];
         cap_off[i + 1] = cap_off[i] + c;
     }
@@ -256,6 +257,7 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     Staging st;
     agn_log dl = *log;
     dl.key_off = st.up(log->key_off, K + 1);
+    dl.key_len = st.up(log->key_len, K);
     dl.key_type = st.up(log->key_type, K);
     dl.oc = st.up(log->oc, E * D);
     dl.oc_mask = st.up(log->oc_mask, E * W);
@@ -265,7 +267,9 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     dl.tag = st.up(log->tag, E);
     dl.add_tok = st.up(log->add_tok, E);
     dl.rem_off = st.up(log->rem_off, log->rem_off ? E + 1 : 0);
-    const uint64_t n_rem = log->rem_off ? log->rem_off[E] : 0;
+    uint64_t n_rem = log->rem_off ? log->rem_off[E] : 0;
+    if (log->rem_off && log->key_len)  // segmented log: the token arena's high-water mark
+        for (uint64_t e = 0; e <= E; ++e) n_rem = std::max<uint64_t>(n_rem, log->rem_off[e]);
     dl.rem_tok = st.up(log->rem_tok, n_rem);
     agn_read dr = *req;
     dr.keys = st.up(req->keys, Q);
@@ -424,7 +428,7 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
         return fail(AGN_EINVAL, "ss_store: keys == NULL needs n_req == n_keys");
     rc = use_device(ctx);
     if (rc) return rc;
-    return launch_ss_store(*cache, log->key_off, n_req, keys, is_first, status, should_gc, *res,
+    return launch_ss_store(*cache, log->key_off, log->key_len, n_req, keys, is_first, status, should_gc, *res,
                            handle, prune, threshold, threshold_mask, (hipStream_t)stream);
 }
 

@@ -122,6 +122,7 @@ __global__ __launch_bounds__(256) void k_ss_lookup(agn_ss_cache c, uint64_t n_re
 
 template <int G>
 __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t *__restrict__ key_off,
+                                                  const uint64_t *__restrict__ key_len,
                                                   uint64_t n_req, const uint64_t *__restrict__ keys,
                                                   const uint8_t *__restrict__ is_first,
                                                   const uint8_t *__restrict__ status,
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t
     const uint32_t D = c.n_dcs, W = n_words(D), S = c.slots;
     const uint64_t k = keys ? keys[i] : i;
     if (status[i] == AGN_SS_LOG) return;
-    if (key_off[k + 1] == key_off[k]) return;  // number_of_ops = 0 (:468-471)
+    if (key_n(key_off, key_len, k) == 0) return;  // number_of_ops = 0 (:468-471)
     const uint32_t fl = res.flags[i];
     if (fl & (AGN_F_ERR_UNEXPECTED | AGN_F_ERR_CORRUPTED | AGN_F_ERR_CAPACITY)) return;
     if (fl & AGN_F_CT_IGNORE) return;  // CommitTime == ignore (:483-484)
@@ -223,12 +224,12 @@ int lookup_g(const agn_ss_cache &c, uint64_t n_req, const uint64_t *keys, const 
 }
 
 template <int G>
-int store_g(const agn_ss_cache &c, const uint64_t *key_off, uint64_t n_req, const uint64_t *keys,
+int store_g(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len, uint64_t n_req, const uint64_t *keys,
             const uint8_t *is_first, const uint8_t *status, const uint8_t *should_gc,
             const agn_result &res, const int64_t *handle, uint8_t *prune, uint64_t *thr,
             uint64_t *thrm, hipStream_t st) {
     hipLaunchKernelGGL((k_ss_store<G>), dim3(grid_for(n_req, 256 / G, 0x7fffffffu)), dim3(256), 0,
-                       st, c, key_off, n_req, keys, is_first, status, should_gc, res, handle,
+                       st, c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, handle,
                        prune, thr, thrm);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
@@ -257,14 +258,16 @@ int launch_ss_lookup(const agn_ss_cache &c, uint64_t n_req, const uint64_t *keys
 #undef AGN_C
 }
 
-int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, uint64_t n_req,
+int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len,
+                    uint64_t n_req,
                     const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
                     const uint8_t *should_gc, const agn_result &res, const int64_t *handle,
                     uint8_t *prune, uint64_t *thr, uint64_t *thrm, hipStream_t st) {
     AGN_HIP(hipMemsetAsync(prune, 0, c.n_keys, st));
     if (n_req == 0) return AGN_OK;
 #define AGN_C(G) \
-    store_g<G>(c, key_off, n_req, keys, is_first, status, should_gc, res, handle, prune, thr, thrm, st)
+    store_g<G>(c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, handle, prune, \
+               thr, thrm, st)
     AGN_GROUP_DISPATCH(c.n_dcs, AGN_C)
 #undef AGN_C
 }

@@ -44,6 +44,12 @@ __device__ inline int64_t wave_sum_i64(int64_t v) {
 
 __device__ inline uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
+// Entries of key k: [key_off[k], key_off[k] + key_len[k]) or CSR.
+__host__ __device__ inline uint64_t key_n(const uint64_t *key_off, const uint64_t *key_len,
+                                          uint64_t k) {
+    return key_len ? key_len[k] : key_off[k + 1] - key_off[k];
+}
+
 // Scalar (wave-uniform) value: lets hipcc keep it in an SGPR.
 __device__ inline uint64_t uniform_u64(uint64_t v) {
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
@@ -100,7 +106,8 @@ int launch_ss_lookup(const agn_ss_cache &c, uint64_t n_req, const uint64_t *keys
                      const uint64_t *R, const uint64_t *Rm, uint64_t *sct, uint64_t *sctm,
                      uint8_t *sct_ign, int64_t *base, uint8_t *first, uint8_t *status,
                      hipStream_t st);
-int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, uint64_t n_req,
+int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len,
+                    uint64_t n_req,
                     const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
                     const uint8_t *should_gc, const agn_result &res, const int64_t *handle,
                     uint8_t *prune, uint64_t *thr, uint64_t *thrm, hipStream_t st);

@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_prune_mark(agn_log log, const uint8_t *
     const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
     const uint32_t D = log.n_dcs, W = n_words(D);
     const uint64_t off = uniform_u64(log.key_off[k]);
-    const uint64_t n = uniform_u64(log.key_off[k + 1]) - off;
+    const uint64_t n = uniform_u64(key_n(log.key_off, log.key_len, k));
     const bool gc = prune == nullptr || prune[k] != 0;
     // the threshold slice this lane compares (missing entry = 0)
     uint64_t t[DPL];
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_prune_scatter(agn_log log, agn_log out,
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t D = log.n_dcs, W = n_words(D);
     const uint64_t off = uniform_u64(log.key_off[k]);
-    const uint64_t n = uniform_u64(log.key_off[k + 1]) - off;
+    const uint64_t n = uniform_u64(key_n(log.key_off, log.key_len, k));
     const uint64_t noff = uniform_u64(out.key_off[k]);
     uint64_t written = 0, rwritten = 0;
     const uint64_t rb = rbase ? uniform_u64(rbase[k]) : 0ull;

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void k_counter(agn_log log, agn_read req, agn_
     for (uint64_t i = (uint64_t)blockIdx.x * 4u + (uint64_t)w; i < req.n_req; i += nw) {
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
         const uint64_t off = uniform_u64(log.key_off[key]);
-        const uint64_t n = uniform_u64(log.key_off[key + 1]) - off;
+        const uint64_t n = uniform_u64(key_n(log.key_off, log.key_len, key));
         const int lane = lane_id();
 
         if (n != 0 && log.key_type != nullptr && log.key_type[key] != (uint8_t)req.req_type) {

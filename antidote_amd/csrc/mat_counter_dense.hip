@@ -168,7 +168,8 @@ __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
 template <int D, bool ANY_WARM, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
-    const uint8_t *__restrict__ key_type, const uint64_t *__restrict__ oc,
+    const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
+    const uint64_t *__restrict__ oc,
     const uint32_t *__restrict__ op_id, const int64_t *__restrict__ eff,
     const uint64_t *__restrict__ log_txid, const uint64_t *__restrict__ R,
     const uint64_t *__restrict__ sct, const uint8_t *__restrict__ sct_ignore,
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     if (i >= a.n_req) return;
     const uint64_t key = keys ? uniform_u64(keys[i]) : i;
     const uint64_t off = uniform_u64(key_off[key]);
-    const uint64_t n = uniform_u64(key_off[key + 1]) - off;
+    const uint64_t n = uniform_u64(key_len ? key_len[key] : key_off[key + 1] - off);
     if (n != 0 && key_type != nullptr && byte_of(key_type, key) != (a.req_type & 0xffu)) {
         if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
             o_flags[i] = AGN_F_ERR_CORRUPTED;
@@ -256,13 +257,13 @@ int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, h
                                         (unsigned long long)req.n_req);
     if (req.sct)
         hipLaunchKernelGGL((k_counter_key<D, true, WPB>), dim3((unsigned)nb), dim3(64 * WPB), 0,
-                           st, a, req.keys, log.key_off, log.key_type, log.oc, log.op_id,
+                           st, a, req.keys, log.key_off, log.key_len, log.key_type, log.oc, log.op_id,
                            log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
                            req.base_value, out.value, out.hole, out.lastct, out.count,
                            out.flags, out.err_pos);
     else
         hipLaunchKernelGGL((k_counter_key<D, false, WPB>), dim3((unsigned)nb), dim3(64 * WPB), 0,
-                           st, a, req.keys, log.key_off, log.key_type, log.oc, log.op_id,
+                           st, a, req.keys, log.key_off, log.key_len, log.key_type, log.oc, log.op_id,
                            log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
                            req.base_value, out.value, out.hole, out.lastct, out.count,
                            out.flags, out.err_pos);

@@ -201,7 +201,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         const uint64_t i = SLOW ? (uint64_t)__builtin_amdgcn_readfirstlane(wl[it]) : it;
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
         const uint64_t off = uniform_u64(log.key_off[key]);
-        const uint64_t n = uniform_u64(log.key_off[key + 1]) - off;
+        const uint64_t n = uniform_u64(key_n(log.key_off, log.key_len, key));
 
         if (n != 0 && log.key_type != nullptr && log.key_type[key] != (uint8_t)req.req_type) {
             if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)

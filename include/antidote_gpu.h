@@ -21,7 +21,10 @@
  * Data model (the SoA "device op log", mirroring the per-key ETS ops tuple of
  * src/materializer_vnode.erl:621-647 and include/antidote.hrl:81-90):
  *   - a log holds n_keys keys; key k owns entries [key_off[k], key_off[k+1])
- *     stored OLDEST -> NEWEST (tuple slot ?FIRST_OP is the oldest op);
+ *     stored OLDEST -> NEWEST (tuple slot ?FIRST_OP is the oldest op) — or,
+ *     when key_len is given, [key_off[k], key_off[k] + key_len[k]): segments
+ *     with slack capacity, like the ETS tuple's Length / ListLen (the
+ *     engine-owned agn_oplog below);
  *   - vector clocks are dense rows of n_dcs u64 words (DC index = column) with
  *     an optional presence bitmask of W = ceil(n_dcs/64) words per clock; a
  *     NULL mask means "every DC present" (the dense fast path);
@@ -41,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AGN_ABI_VERSION 1
+#define AGN_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define AGN_OK 0
@@ -78,7 +81,8 @@ typedef struct agn_log {
     uint32_t n_dcs;           /* D: vector-clock width */
     uint64_t n_keys;
     uint64_t n_entries;
-    const uint64_t *key_off;  /* [n_keys+1] */
+    const uint64_t *key_off;  /* [n_keys+1] CSR, or segment starts when key_len != NULL */
+    const uint64_t *key_len;  /* [n_keys] entries in use per segment, or NULL (CSR) */
     const uint8_t *key_type;  /* [n_keys] type of the key's ops or AGN_TYPE_MIXED; NULL: all crdt_type */
     const uint64_t *oc;       /* [n_entries * D] OpSSCommit */
     const uint64_t *oc_mask;  /* [n_entries * W] presence, NULL = dense */
@@ -90,7 +94,8 @@ typedef struct agn_log {
      * AGN_REGISTER_MV: entry = {Value, Token, Overridden} or {reset, Overridden} */
     const uint32_t *tag;      /* [n_entries] elem id (set) / value id (register) */
     const uint64_t *add_tok;  /* [n_entries] token added (0 = none: remove / reset) */
-    const uint32_t *rem_off;  /* [n_entries+1] CSR into rem_tok */
+    const uint32_t *rem_off;  /* [n_entries+1] CSR into rem_tok (with key_len: contiguous
+                                 within a key, rem_off[key_off[k]+key_len[k]] = end) */
     const uint64_t *rem_tok;  /* removed (set) / overridden (register) tokens */
 } agn_log;
 

@@ -30,6 +30,8 @@
 #include <string.h>
 
 #define W_OF(d) (((d) + 63u) / 64u)
+/* entries of key k: [key_off[k], key_off[k] + KEY_N) (segments with key_len, else CSR) */
+#define KEY_N(log, k) ((log)->key_len ? (log)->key_len[k] : (log)->key_off[(k) + 1] - (log)->key_off[k])
 
 static inline int present(const uint64_t *mask, uint32_t d) {
     return mask == NULL || ((mask[d >> 6] >> (d & 63)) & 1u);
@@ -143,7 +145,7 @@ static void materialize_one(const agn_log *log, const agn_read *req, agn_result 
                             uint64_t i, uint32_t *incl_buf) {
     const uint32_t D = log->n_dcs, W = W_OF(D);
     const uint64_t key = req->keys ? req->keys[i] : i;
-    const uint64_t off = log->key_off[key], n = log->key_off[key + 1] - off;
+    const uint64_t off = log->key_off[key], n = KEY_N(log, key);
     const uint64_t *R = req->R + i * D;
     const uint64_t *Rm = req->R_mask ? req->R_mask + i * W : NULL;
     int sct_ign = (req->sct == NULL) || (req->sct_ignore && req->sct_ignore[i]);
@@ -298,7 +300,7 @@ int oracle_materialize(const agn_log *log, const agn_read *req, agn_result *out,
     if (!req->keys && req->n_req != log->n_keys) return AGN_EINVAL;
     uint64_t max_n = 0;
     for (uint64_t k = 0; k < log->n_keys; ++k) {
-        uint64_t n = log->key_off[k + 1] - log->key_off[k];
+        uint64_t n = KEY_N(log, k);
         if (n > max_n) max_n = n;
     }
     if (n_threads < 1) n_threads = 1;
@@ -513,7 +515,7 @@ int oracle_ss_store(agn_ss_cache *c, const agn_log *log, uint64_t n_req, const u
     for (uint64_t i = 0; i < n_req; ++i) {
         const uint64_t k = keys ? keys[i] : i;
         if (status[i] == AGN_SS_LOG) continue;
-        if (log->key_off[k + 1] == log->key_off[k]) continue; /* number_of_ops = 0 */
+        if (KEY_N(log, k) == 0) continue; /* number_of_ops = 0 */
         const uint32_t fl = res->flags[i];
         if (fl & (AGN_F_ERR_UNEXPECTED | AGN_F_ERR_CORRUPTED | AGN_F_ERR_CAPACITY)) continue;
         if (fl & AGN_F_CT_IGNORE) continue; /* CommitTime == ignore */
@@ -601,7 +603,7 @@ int oracle_prune_ops(const agn_log *log, const uint8_t *prune, const uint64_t *t
         const int gc = prune == NULL || prune[k] != 0;
         const uint64_t *t = thr + k * D, *tm = thr_mask ? thr_mask + k * W : NULL;
         uint64_t kept = 0;
-        for (uint64_t e = log->key_off[k]; e < log->key_off[k + 1]; ++e) {
+        for (uint64_t e = log->key_off[k]; e < log->key_off[k] + KEY_N(log, k); ++e) {
             const uint64_t *o = log->oc + e * D, *m = log->oc_mask ? log->oc_mask + e * W : NULL;
             if (gc && oracle_vc_le(D, o, m, t, tm)) continue; /* already in the snapshot */
             for (uint32_t d = 0; d < D; ++d) oc[w * D + d] = o[d];
