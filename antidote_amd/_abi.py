@@ -18,6 +18,8 @@ EFFECT_INVALID = -(1 << 63)
 TAG_INVALID = 0xFFFFFFFF
 
 F_NEWSS, F_CT_IGNORE, F_ERR_UNEXPECTED, F_ERR_CORRUPTED, F_ERR_CAPACITY = 0x1, 0x2, 0x4, 0x8, 0x10
+OPS_THRESHOLD = 50  # src/materializer_vnode.erl:41
+RESIZE_THRESHOLD = 5  # :44
 GC_ALL_PRUNED = 0x1
 UNIQUE_ID_BYTES = 128
 U64_MAX = (1 << 64) - 1
@@ -119,6 +121,14 @@ PROTOTYPES = {
                                P, C.POINTER(AgnResult), P, P, P, P, P]),
     "agn_prune_ops": (C.c_int, [P, C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P, P, P]),
     "agn_gst_scalar": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P]),
+    "agn_oplog_create": (C.c_int, [P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,
+                                   C.POINTER(P)]),
+    "agn_oplog_destroy": (C.c_int, [P]),
+    "agn_oplog_append": (C.c_int, [P, C.c_uint64, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "agn_oplog_flush": (C.c_int, [P, C.POINTER(AgnLog), P]),
+    "agn_oplog_prune": (C.c_int, [P, P, P, P, P, P]),
+    "agn_oplog_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_uint64)]),
     "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),
     "agn_comm_unique_id": (C.c_int, [P]),
     "agn_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),

@@ -42,7 +42,7 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
-static int use_device(agn_ctx *ctx) {
+int use_device(agn_ctx *ctx) {
     if (!ctx) return fail(AGN_EINVAL, "null context");
     AGN_HIP(hipSetDevice(ctx->device));
     return AGN_OK;

@@ -13,6 +13,8 @@ namespace agn {
 // Thread-local last-error message (agn_last_error).
 void set_error(const char *fmt, ...);
 int fail(int code, const char *fmt, ...);
+// hipSetDevice(ctx's device); AGN_EINVAL for a null context.
+int use_device(agn_ctx *ctx);
 
 #define AGN_HIP(call)                                                              \
     do {                                                                           \

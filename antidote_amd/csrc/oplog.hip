@@ -1,0 +1,721 @@
+// oplog.hip — the engine-owned per-partition op log (include/antidote_gpu.h,
+// "engine-owned op log").  It keeps the materializer_vnode ETS ops cache
+// (src/materializer_vnode.erl:284-286, 321-338, 621-647) resident in HBM so
+// reads never re-upload a key's ops.
+//
+// Layout in HBM.  Entry arrays (oc rows, masks, op_id, txid, effect fields,
+// rem_off) form one arena; key k owns the segment [start[k], start[k] +
+// cap[k] + 1) of it — cap slots for its ops, oldest first (the ETS tuple's
+// element FIRST_OP.. of ListLen slots), plus one rem_off slot for the end of
+// its last token list.  A second arena holds removal tokens, key k owning
+// [tstart[k], tstart[k] + tcap[k]).  The flushed view is an agn_log with
+// key_off = segment starts and key_len = lengths, which every kernel reads.
+//
+// Writes.  agn_oplog_append is host-only: it assigns op ids (the per-key
+// counter of ets:update_counter, :630) and stages the entries with their
+// final slot (key, position).  A key whose segment fills gets a new one of
+// twice the size at the arena's end (a "move", copied on the device at the
+// next flush, before the staged entries land).  agn_oplog_flush packs
+// everything into one pinned buffer, does one H2D copy and three kernels:
+// move segments, scatter entries, update key_off/key_len.  The arenas grow by
+// doubling with stream-ordered alloc/copy/free.
+//
+// GC.  agn_oplog_prune runs the prune_ops stream compaction (gc.hip) into a
+// CSR, reads back the per-key lengths, applies the ETS resize policy
+// (snapshot_insert_gc, :540-558) and re-segments into a fresh arena.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+namespace agn {
+namespace {
+
+struct Arena {  // entry arrays of one log (null when the type lacks them)
+    uint64_t *oc = nullptr, *mask = nullptr, *txid = nullptr, *add = nullptr;
+    uint32_t *op_id = nullptr, *tag = nullptr, *rem_off = nullptr;
+    int64_t *eff = nullptr;
+    uint64_t *tok = nullptr;  // token arena
+};
+
+struct Move {  // one segment copy: entries [src, src+len) -> dst, tokens likewise
+    uint64_t src, dst, tsrc, tdst;
+    uint32_t len, tlen;
+};
+
+// Copies one key's segment (entries, their rows and fields, the token list)
+// and rebases rem_off onto the destination token segment.  One wave.
+__device__ void copy_segment(const Arena &a, const Arena &b, uint32_t D, uint32_t W,
+                             uint64_t src, uint64_t dst, uint32_t len, uint64_t tsrc,
+                             uint64_t tdst, uint32_t tlen, int lane) {
+    const bool same = (src == dst) && (a.oc == b.oc);
+    if (!same) {
+        const uint64_t nw = (uint64_t)len * D;
+        for (uint64_t j = lane; j < nw; j += AGN_WAVE) b.oc[dst * D + j] = a.oc[src * D + j];
+        if (a.mask) {
+            const uint64_t nm = (uint64_t)len * W;
+            for (uint64_t j = lane; j < nm; j += AGN_WAVE) b.mask[dst * W + j] = a.mask[src * W + j];
+        }
+        for (uint32_t j = lane; j < len; j += AGN_WAVE) {
+            b.op_id[dst + j] = a.op_id[src + j];
+            b.txid[dst + j] = a.txid[src + j];
+            if (a.eff) b.eff[dst + j] = a.eff[src + j];
+            if (a.tag) {
+                b.tag[dst + j] = a.tag[src + j];
+                b.add[dst + j] = a.add[src + j];
+            }
+        }
+    }
+    if (a.rem_off) {
+        if (len == 0 && lane == 0) b.rem_off[dst] = (uint32_t)tdst;
+        for (uint32_t j = lane; j < len + (len ? 1u : 0u); j += AGN_WAVE)
+            b.rem_off[dst + j] = (uint32_t)(a.rem_off[src + j] - tsrc + tdst);
+        if (!(tsrc == tdst && a.tok == b.tok))
+            for (uint32_t j = lane; j < tlen; j += AGN_WAVE) b.tok[tdst + j] = a.tok[tsrc + j];
+    }
+}
+
+// Pending segment moves of a flush.  Source and destination ranges never
+// overlap: a destination is always fresh arena space.  Rebase-only moves
+// (token segment moved, entry segment not) have src == dst.
+__global__ void __launch_bounds__(256) k_move(Arena a, uint32_t D, uint32_t W,
+                                              const Move *__restrict__ mv, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const Move m = mv[i];
+    copy_segment(a, a, D, W, m.src, m.dst, m.len, m.tsrc, m.tdst, m.tlen, lane_id());
+}
+
+// Staged entries: fields and token lists, one thread per entry.
+__global__ void __launch_bounds__(256) k_scatter(
+    Arena a, uint32_t W, uint64_t n, const uint64_t *__restrict__ dst,
+    const uint64_t *__restrict__ tdst, const uint32_t *__restrict__ tlen,
+    const uint64_t *__restrict__ toff, const uint32_t *__restrict__ op_id,
+    const uint64_t *__restrict__ txid, const int64_t *__restrict__ eff,
+    const uint32_t *__restrict__ tag, const uint64_t *__restrict__ add,
+    const uint64_t *__restrict__ mask, const uint64_t *__restrict__ tok) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t e = dst[i];
+    a.op_id[e] = op_id[i];
+    a.txid[e] = txid[i];
+    if (a.eff) a.eff[e] = eff[i];
+    if (a.tag) {
+        a.tag[e] = tag[i];
+        a.add[e] = add[i];
+    }
+    if (a.mask)
+        for (uint32_t w = 0; w < W; ++w) a.mask[e * W + w] = mask[i * W + w];
+    if (a.rem_off) {
+        // The next entry of the key writes the same value into e + 1.
+        const uint64_t t = tdst[i];
+        const uint32_t l = tlen[i];
+        a.rem_off[e] = (uint32_t)t;
+        a.rem_off[e + 1] = (uint32_t)(t + l);
+        const uint64_t s = toff[i];
+        for (uint32_t j = 0; j < l; ++j) a.tok[t + j] = tok[s + j];
+    }
+}
+
+// Staged oc rows: one thread per clock word, coalesced on the staging side.
+__global__ void __launch_bounds__(256) k_scatter_rows(uint64_t *__restrict__ oc, uint32_t D,
+                                                      uint64_t n, const uint64_t *__restrict__ dst,
+                                                      const uint64_t *__restrict__ rows) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n * D) return;
+    const uint64_t i = j / D;
+    oc[dst[i] * D + (j - i * D)] = rows[j];
+}
+
+__global__ void __launch_bounds__(256) k_keys(uint64_t *__restrict__ key_off,
+                                              uint64_t *__restrict__ key_len, uint64_t n,
+                                              const uint64_t *__restrict__ kv) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = kv[3 * i];
+    key_off[k] = kv[3 * i + 1];
+    key_len[k] = kv[3 * i + 2];
+}
+
+// Per-key entry and token counts of a CSR log (prune output).
+__global__ void __launch_bounds__(256) k_csr_lens(uint64_t K, const uint64_t *__restrict__ key_off,
+                                                  const uint32_t *__restrict__ rem_off,
+                                                  uint32_t *__restrict__ len,
+                                                  uint32_t *__restrict__ tlen) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    const uint64_t s = key_off[k], e = key_off[k + 1];
+    len[k] = (uint32_t)(e - s);
+    if (tlen) tlen[k] = rem_off ? rem_off[e] - rem_off[s] : 0u;
+}
+
+// CSR (prune output) -> fresh segmented arena; one wave per key.
+__global__ void __launch_bounds__(256) k_reseg(Arena csr, Arena b, uint32_t D, uint32_t W,
+                                               uint64_t K, const uint64_t *__restrict__ csr_off,
+                                               const uint64_t *__restrict__ start,
+                                               const uint64_t *__restrict__ tstart,
+                                               uint64_t *__restrict__ key_off,
+                                               uint64_t *__restrict__ key_len) {
+    const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= K) return;
+    const uint64_t dst = start[k];  // ~0: the key never had a segment
+    if (lane_id() == 0) key_off[k] = dst == ~0ull ? 0ull : dst;
+    if (dst == ~0ull) {
+        if (lane_id() == 0) key_len[k] = 0;
+        return;
+    }
+    const uint64_t s = csr_off[k];
+    const uint32_t len = (uint32_t)(csr_off[k + 1] - s);
+    uint64_t ts = 0;
+    uint32_t tl = 0;
+    if (csr.rem_off) {
+        ts = csr.rem_off[s];
+        tl = csr.rem_off[s + len] - (uint32_t)ts;
+    }
+    if (lane_id() == 0) key_len[k] = len;
+    copy_segment(csr, b, D, W, s, dst, len, ts, tstart ? tstart[k] : 0, tl, lane_id());
+}
+
+template <class T>
+hipError_t grow_array(T *&p, uint64_t old_n, uint64_t new_n, hipStream_t st) {
+    if (!p && old_n) return hipErrorInvalidValue;
+    T *q = nullptr;
+    hipError_t e = hipMallocAsync((void **)&q, std::max<uint64_t>(new_n, 1) * sizeof(T), st);
+    if (e != hipSuccess) return e;
+    if (p && old_n) {
+        e = hipMemcpyAsync(q, p, old_n * sizeof(T), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    if (p) e = hipFreeAsync(p, st);
+    p = q;
+    return e;
+}
+
+template <class T>
+void free_async(T *&p, hipStream_t st) {
+    if (p) (void)hipFreeAsync(p, st);
+    p = nullptr;
+}
+
+inline uint64_t align8(uint64_t b) { return (b + 255) & ~255ull; }
+
+}  // namespace
+}  // namespace agn
+
+using namespace agn;
+
+struct agn_oplog {
+    agn_ctx *ctx = nullptr;
+    uint32_t crdt = 0, D = 0, W = 0, init_slots = AGN_OPS_THRESHOLD;
+    bool sparse = false, tags = false;
+    uint64_t K = 0;
+
+    // host metadata per key
+    std::vector<uint64_t> start, tstart;
+    std::vector<uint32_t> cap, len, counter, tcap, tlen;
+    std::vector<uint32_t> dlen, dtlen;  // lengths the device already holds
+    std::vector<uint8_t> dirty;
+    std::vector<uint64_t> dirty_keys;
+    std::vector<int64_t> move_of;  // index into moves, -1 = none pending
+    std::vector<Move> moves;
+    uint64_t used = 0, tused = 0;  // arena high-water marks (slots)
+    uint64_t n_entries = 0, n_tokens = 0;
+
+    // device
+    Arena a;
+    uint64_t dcap = 0, tdcap = 0;  // allocated slots
+    uint64_t *key_off = nullptr, *key_len = nullptr;
+    hipEvent_t up_done = nullptr;
+    bool up_pending = false;
+    void *pinned = nullptr;
+    size_t pinned_bytes = 0;
+
+    // staging (host)
+    std::vector<uint64_t> s_dst, s_tdst, s_toff, s_txid, s_add, s_oc, s_mask, s_tok;
+    std::vector<uint32_t> s_tlen, s_opid, s_tag;
+    std::vector<int64_t> s_eff;
+    // staged entries are stored by key + position and resolved at flush
+    std::vector<uint64_t> s_key;
+    std::vector<uint32_t> s_pos, s_tpos;
+};
+
+namespace {
+
+void oplog_new_segment(agn_oplog *L, uint64_t k, uint32_t need, uint32_t tneed) {
+    // Entry segment.
+    if (need > L->cap[k]) {
+        uint32_t c = L->cap[k] ? L->cap[k] : L->init_slots;
+        while (c < need) c *= 2;
+        const uint64_t old = L->start[k];
+        L->start[k] = L->used;
+        L->used += (uint64_t)c + 1;
+        L->cap[k] = c;
+        if (L->dlen[k] || L->dtlen[k] || L->move_of[k] >= 0) {
+            if (L->move_of[k] < 0) {
+                L->move_of[k] = (int64_t)L->moves.size();
+                L->moves.push_back(Move{old, 0, L->tstart[k], 0, L->dlen[k], L->dtlen[k]});
+            }
+        }
+    }
+    if (L->tags && tneed > L->tcap[k]) {
+        uint32_t c = L->tcap[k] ? L->tcap[k] : 16u;
+        while (c < tneed) c *= 2;
+        const uint64_t old = L->tstart[k];
+        L->tstart[k] = L->tused;
+        L->tused += c;
+        L->tcap[k] = c;
+        if (L->dlen[k] || L->dtlen[k] || L->move_of[k] >= 0) {
+            if (L->move_of[k] < 0) {
+                L->move_of[k] = (int64_t)L->moves.size();
+                L->moves.push_back(Move{L->start[k], 0, old, 0, L->dlen[k], L->dtlen[k]});
+            }
+        }
+    }
+}
+
+int ensure_pinned(agn_oplog *L, size_t bytes) {
+    if (L->up_pending) {
+        AGN_HIP(hipEventSynchronize(L->up_done));
+        L->up_pending = false;
+    }
+    if (bytes <= L->pinned_bytes) return AGN_OK;
+    if (L->pinned) AGN_HIP(hipHostFree(L->pinned));
+    L->pinned = nullptr;
+    size_t b = std::max<size_t>(bytes, 2 * L->pinned_bytes);
+    AGN_HIP(hipHostMalloc(&L->pinned, b, hipHostMallocDefault));
+    L->pinned_bytes = b;
+    return AGN_OK;
+}
+
+int ensure_arena(agn_oplog *L, hipStream_t st) {
+    if (L->used > L->dcap || !L->a.op_id) {
+        uint64_t c = std::max<uint64_t>(L->used, 2 * L->dcap);
+        Arena &a = L->a;
+        AGN_HIP(grow_array(a.oc, L->dcap * L->D, c * L->D, st));
+        if (L->sparse) AGN_HIP(grow_array(a.mask, L->dcap * L->W, c * L->W, st));
+        AGN_HIP(grow_array(a.op_id, L->dcap, c, st));
+        AGN_HIP(grow_array(a.txid, L->dcap, c, st));
+        if (L->tags) {
+            AGN_HIP(grow_array(a.tag, L->dcap, c, st));
+            AGN_HIP(grow_array(a.add, L->dcap, c, st));
+            AGN_HIP(grow_array(a.rem_off, L->dcap, c, st));
+        } else {
+            AGN_HIP(grow_array(a.eff, L->dcap, c, st));
+        }
+        L->dcap = c;
+    }
+    if (L->tags && (L->tused > L->tdcap || !L->a.tok)) {
+        if (L->tused >= 0xffffffffull)
+            return fail(AGN_ENOTSUP, "oplog: token arena beyond 2^32 slots");
+        uint64_t c = std::min<uint64_t>(std::max<uint64_t>(L->tused, 2 * L->tdcap), 0xffffffffull);
+        AGN_HIP(grow_array(L->a.tok, L->tdcap, c, st));
+        L->tdcap = c;
+    }
+    return AGN_OK;
+}
+
+void fill_view(const agn_oplog *L, agn_log *v) {
+    std::memset(v, 0, sizeof *v);
+    v->crdt_type = L->crdt;
+    v->n_dcs = L->D;
+    v->n_keys = L->K;
+    v->n_entries = L->used;
+    v->key_off = L->key_off;
+    v->key_len = L->key_len;
+    v->oc = L->a.oc;
+    v->oc_mask = L->a.mask;
+    v->op_id = L->a.op_id;
+    v->txid = L->a.txid;
+    v->eff = L->a.eff;
+    v->tag = L->a.tag;
+    v->add_tok = L->a.add;
+    v->rem_off = L->a.rem_off;
+    v->rem_tok = L->a.tok;
+}
+
+int do_flush(agn_oplog *L, hipStream_t st) {
+    const uint64_t n = L->s_key.size(), nm = L->moves.size(), nk = L->dirty_keys.size();
+    int rc = ensure_arena(L, st);
+    if (rc) return rc;
+    if (n == 0 && nm == 0 && nk == 0) return AGN_OK;
+    const uint32_t D = L->D, W = L->W;
+    // Resolve staged (key, position) to arena slots now that segments are final.
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t k = L->s_key[i];
+        L->s_dst[i] = L->start[k] + L->s_pos[i];
+        L->s_tdst[i] = L->tstart[k] + L->s_tpos[i];
+    }
+    for (uint64_t k : L->dirty_keys)
+        if (L->move_of[k] >= 0) {
+            Move &m = L->moves[L->move_of[k]];
+            m.dst = L->start[k];
+            m.tdst = L->tstart[k];
+        }
+    // Pack: moves | dst | tdst | toff | txid | add | tlen | opid | tag | eff | oc | mask | tok | keys
+    size_t off = 0;
+    auto slot = [&](size_t bytes) { size_t o = off; off = align8(off + bytes); return o; };
+    const size_t o_mv = slot(nm * sizeof(Move)), o_dst = slot(n * 8), o_tdst = slot(n * 8),
+                 o_toff = slot(n * 8), o_txid = slot(n * 8), o_add = slot(L->tags ? n * 8 : 0),
+                 o_tlen = slot(n * 4), o_opid = slot(n * 4), o_tag = slot(L->tags ? n * 4 : 0),
+                 o_eff = slot(L->tags ? 0 : n * 8), o_oc = slot(n * D * 8),
+                 o_mask = slot(L->sparse ? n * W * 8 : 0), o_tok = slot(L->s_tok.size() * 8),
+                 o_keys = slot(nk * 24);
+    rc = ensure_pinned(L, off);
+    if (rc) return rc;
+    char *h = (char *)L->pinned;
+    auto put = [&](size_t o, const void *src, size_t bytes) { if (bytes) std::memcpy(h + o, src, bytes); };
+    put(o_mv, L->moves.data(), nm * sizeof(Move));
+    put(o_dst, L->s_dst.data(), n * 8);
+    put(o_tdst, L->s_tdst.data(), n * 8);
+    put(o_toff, L->s_toff.data(), n * 8);
+    put(o_txid, L->s_txid.data(), n * 8);
+    if (L->tags) {
+        put(o_add, L->s_add.data(), n * 8);
+        put(o_tag, L->s_tag.data(), n * 4);
+    } else {
+        put(o_eff, L->s_eff.data(), n * 8);
+    }
+    put(o_tlen, L->s_tlen.data(), n * 4);
+    put(o_opid, L->s_opid.data(), n * 4);
+    put(o_oc, L->s_oc.data(), n * D * 8);
+    if (L->sparse) put(o_mask, L->s_mask.data(), n * W * 8);
+    put(o_tok, L->s_tok.data(), L->s_tok.size() * 8);
+    {
+        uint64_t *kv = (uint64_t *)(h + o_keys);
+        for (uint64_t j = 0; j < nk; ++j) {
+            const uint64_t k = L->dirty_keys[j];
+            kv[3 * j] = k;
+            kv[3 * j + 1] = L->start[k];
+            kv[3 * j + 2] = L->len[k];
+        }
+    }
+    char *d = nullptr;
+    AGN_HIP(hipMallocAsync((void **)&d, off, st));
+    AGN_HIP(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, st));
+    AGN_HIP(hipEventRecord(L->up_done, st));
+    L->up_pending = true;
+    if (nm)
+        k_move<<<(unsigned)((nm + 3) / 4), 256, 0, st>>>(L->a, D, W, (const Move *)(d + o_mv), nm);
+    if (n) {
+        k_scatter<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+            L->a, W, n, (const uint64_t *)(d + o_dst), (const uint64_t *)(d + o_tdst),
+            (const uint32_t *)(d + o_tlen), (const uint64_t *)(d + o_toff),
+            (const uint32_t *)(d + o_opid), (const uint64_t *)(d + o_txid),
+            (const int64_t *)(d + o_eff), (const uint32_t *)(d + o_tag),
+            (const uint64_t *)(d + o_add), (const uint64_t *)(d + o_mask),
+            (const uint64_t *)(d + o_tok));
+        k_scatter_rows<<<(unsigned)((n * D + 255) / 256), 256, 0, st>>>(
+            L->a.oc, D, n, (const uint64_t *)(d + o_dst), (const uint64_t *)(d + o_oc));
+    }
+    if (nk)
+        k_keys<<<(unsigned)((nk + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, nk,
+                                                              (const uint64_t *)(d + o_keys));
+    AGN_HIP(hipGetLastError());
+    AGN_HIP(hipFreeAsync(d, st));
+    for (uint64_t k : L->dirty_keys) {
+        L->dlen[k] = L->len[k];
+        L->dtlen[k] = L->tlen[k];
+        L->dirty[k] = 0;
+        L->move_of[k] = -1;
+    }
+    L->dirty_keys.clear();
+    L->moves.clear();
+    for (auto *v : {&L->s_dst, &L->s_tdst, &L->s_toff, &L->s_txid, &L->s_add, &L->s_oc, &L->s_mask,
+                    &L->s_tok, &L->s_key})
+        v->clear();
+    for (auto *v : {&L->s_tlen, &L->s_opid, &L->s_tag, &L->s_pos, &L->s_tpos}) v->clear();
+    L->s_eff.clear();
+    return AGN_OK;
+}
+
+// snapshot_insert_gc's NewListLen (src/materializer_vnode.erl:540-558).
+uint32_t resize_list_len(uint32_t new_len, uint32_t list_len) {
+    if ((int64_t)new_len > (int64_t)list_len - AGN_RESIZE_THRESHOLD) return list_len * 2;
+    const uint32_t half = list_len / 2;
+    if (half <= AGN_OPS_THRESHOLD) return list_len;
+    return ((int64_t)half - AGN_RESIZE_THRESHOLD > (int64_t)new_len) ? half : list_len;
+}
+
+}  // namespace
+
+extern "C" {
+
+int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t n_keys,
+                     int sparse, uint32_t init_slots, agn_oplog **out) {
+    if (!out) return fail(AGN_EINVAL, "oplog_create: null out");
+    *out = nullptr;
+    if (n_dcs == 0 || n_dcs > 256) return fail(AGN_EINVAL, "oplog_create: n_dcs=%u", n_dcs);
+    if (crdt_type != AGN_COUNTER_PN && crdt_type != AGN_SET_AW && crdt_type != AGN_REGISTER_MV)
+        return fail(AGN_EINVAL, "oplog_create: crdt_type %u", crdt_type);
+    if (init_slots > (1u << 30)) return fail(AGN_EINVAL, "oplog_create: init_slots %u", init_slots);
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    agn_oplog *L = new (std::nothrow) agn_oplog;
+    if (!L) return fail(AGN_ENOMEM, "oplog_create");
+    L->ctx = ctx;
+    L->crdt = crdt_type;
+    L->D = n_dcs;
+    L->W = n_words(n_dcs);
+    L->sparse = sparse != 0;
+    L->tags = crdt_type != AGN_COUNTER_PN;
+    L->init_slots = init_slots ? init_slots : AGN_OPS_THRESHOLD;
+    L->K = n_keys;
+    try {
+        L->start.assign(n_keys, 0);
+        L->tstart.assign(n_keys, 0);
+        for (auto *v : {&L->cap, &L->len, &L->counter, &L->tcap, &L->tlen, &L->dlen, &L->dtlen})
+            v->assign(n_keys, 0);
+        L->dirty.assign(n_keys, 0);
+        L->move_of.assign(n_keys, -1);
+    } catch (...) {
+        delete L;
+        return fail(AGN_ENOMEM, "oplog_create: host metadata for %llu keys",
+                    (unsigned long long)n_keys);
+    }
+    hipError_t e = hipMalloc((void **)&L->key_off, std::max<uint64_t>(n_keys, 1) * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->key_len, std::max<uint64_t>(n_keys, 1) * 8);
+    if (e == hipSuccess) e = hipMemset(L->key_off, 0, std::max<uint64_t>(n_keys, 1) * 8);
+    if (e == hipSuccess) e = hipMemset(L->key_len, 0, std::max<uint64_t>(n_keys, 1) * 8);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L->up_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        agn_oplog_destroy(L);
+        return fail(AGN_ENOMEM, "oplog_create: device key arrays");
+    }
+    *out = L;
+    return AGN_OK;
+}
+
+int agn_oplog_destroy(agn_oplog *L) {
+    if (!L) return AGN_OK;
+    if (L->ctx) use_device(L->ctx);
+    (void)hipDeviceSynchronize();
+    Arena &a = L->a;
+    for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
+                    (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok,
+                    (void *)L->key_off, (void *)L->key_len})
+        if (p) (void)hipFree(p);
+    if (L->pinned) (void)hipHostFree(L->pinned);
+    if (L->up_done) (void)hipEventDestroy(L->up_done);
+    delete L;
+    return AGN_OK;
+}
+
+int agn_oplog_append(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint8_t *same_op,
+                     const uint64_t *oc, const uint64_t *oc_mask, const uint64_t *txid,
+                     const int64_t *eff, const uint32_t *tag, const uint64_t *add_tok,
+                     const uint32_t *rem_off, const uint64_t *rem_tok, uint32_t *out_op_id,
+                     uint8_t *out_gc_due) {
+    if (!L) return fail(AGN_EINVAL, "oplog_append: null oplog");
+    if (n == 0) return AGN_OK;
+    if (!keys || !oc) return fail(AGN_EINVAL, "oplog_append: keys / oc required");
+    if (L->sparse && !oc_mask) return fail(AGN_EINVAL, "oplog_append: sparse log needs oc_mask");
+    if (L->tags ? (!tag || !add_tok || !rem_off || (rem_off[n] > rem_off[0] && !rem_tok)) : !eff)
+        return fail(AGN_EINVAL, "oplog_append: effect arrays missing for type %u", L->crdt);
+    // Validate the whole batch before touching any state (all or nothing).
+    for (uint64_t i = 0; i < n; ++i) {
+        if (keys[i] >= L->K)
+            return fail(AGN_EINVAL, "oplog_append: key %llu >= n_keys", (unsigned long long)keys[i]);
+        if (same_op && same_op[i] && (i == 0 || keys[i - 1] != keys[i]))
+            return fail(AGN_EINVAL, "oplog_append: same_op[%llu] without a preceding entry of its key",
+                        (unsigned long long)i);
+        if (L->tags && rem_off[i + 1] < rem_off[i])
+            return fail(AGN_EINVAL, "oplog_append: rem_off not monotone at %llu",
+                        (unsigned long long)i);
+    }
+    const uint32_t D = L->D, W = L->W;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t k = keys[i];
+        if (!(same_op && same_op[i])) ++L->counter[k];
+        const uint32_t id = L->counter[k];
+        if (out_op_id) out_op_id[i] = id;
+        if (out_gc_due)
+            out_gc_due[i] = !(same_op && same_op[i]) &&
+                            (L->len[k] >= std::max(L->cap[k], L->init_slots) ||
+                             id % AGN_OPS_THRESHOLD == 0);
+        const uint32_t tl = L->tags ? rem_off[i + 1] - rem_off[i] : 0u;
+        oplog_new_segment(L, k, L->len[k] + 1, L->tlen[k] + tl);
+        L->s_key.push_back(k);
+        L->s_pos.push_back(L->len[k]);
+        L->s_tpos.push_back(L->tlen[k]);
+        L->s_opid.push_back(id);
+        L->s_txid.push_back(txid ? txid[i] : 0ull);
+        L->s_oc.insert(L->s_oc.end(), oc + i * D, oc + (i + 1) * D);
+        if (L->sparse) L->s_mask.insert(L->s_mask.end(), oc_mask + i * W, oc_mask + (i + 1) * W);
+        if (L->tags) {
+            L->s_tag.push_back(tag[i]);
+            L->s_add.push_back(add_tok[i]);
+            L->s_toff.push_back(L->s_tok.size());
+            L->s_tok.insert(L->s_tok.end(), rem_tok + rem_off[i], rem_tok + rem_off[i + 1]);
+        } else {
+            L->s_eff.push_back(eff[i]);
+            L->s_toff.push_back(0);
+        }
+        L->s_tlen.push_back(tl);
+        L->s_dst.push_back(0);
+        L->s_tdst.push_back(0);
+        ++L->len[k];
+        L->tlen[k] += tl;
+        if (!L->dirty[k]) {
+            L->dirty[k] = 1;
+            L->dirty_keys.push_back(k);
+        }
+    }
+    L->n_entries += n;
+    if (L->tags) L->n_tokens += rem_off[n] - rem_off[0];
+    return AGN_OK;
+}
+
+int agn_oplog_flush(agn_oplog *L, agn_log *view, void *stream) {
+    if (!L) return fail(AGN_EINVAL, "oplog_flush: null oplog");
+    int rc = use_device(L->ctx);
+    if (rc) return rc;
+    rc = do_flush(L, (hipStream_t)stream);
+    if (rc) return rc;
+    if (view) fill_view(L, view);
+    return AGN_OK;
+}
+
+int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshold,
+                    const uint64_t *threshold_mask, uint32_t *out_flags, void *stream) {
+    if (!L) return fail(AGN_EINVAL, "oplog_prune: null oplog");
+    if (!threshold) return fail(AGN_EINVAL, "oplog_prune: threshold required");
+    if (L->sparse && !threshold_mask) return fail(AGN_EINVAL, "oplog_prune: sparse log needs threshold_mask");
+    int rc = use_device(L->ctx);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    rc = do_flush(L, st);
+    if (rc) return rc;
+    if (L->K == 0) return AGN_OK;
+    const uint64_t K = L->K, NE = std::max<uint64_t>(L->n_entries, 1), NT = std::max<uint64_t>(L->n_tokens, 1);
+    const uint32_t D = L->D, W = L->W;
+    if (L->n_entries > 0x7fffffffull) return fail(AGN_ENOTSUP, "oplog_prune: log too large for one pass");
+    agn_log view;
+    fill_view(L, &view);
+    // 1. prune_ops into a compact CSR.
+    Arena c;
+    uint64_t *c_off = nullptr;
+    uint32_t *lens = nullptr;
+    hipError_t e = hipMallocAsync((void **)&c_off, (K + 1) * 8, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&c.oc, NE * D * 8, st);
+    if (e == hipSuccess && L->sparse) e = hipMallocAsync((void **)&c.mask, NE * W * 8, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&c.op_id, NE * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&c.txid, NE * 8, st);
+    if (e == hipSuccess && !L->tags) e = hipMallocAsync((void **)&c.eff, NE * 8, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.tag, NE * 4, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.add, NE * 8, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.rem_off, (NE + 1) * 4, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.tok, NT * 8, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&lens, 2 * K * 4, st);
+    auto release = [&]() {
+        for (void *p : {(void *)c_off, (void *)c.oc, (void *)c.mask, (void *)c.op_id, (void *)c.txid,
+                        (void *)c.eff, (void *)c.tag, (void *)c.add, (void *)c.rem_off,
+                        (void *)c.tok, (void *)lens})
+            if (p) (void)hipFreeAsync(p, st);
+    };
+    if (e != hipSuccess) {
+        release();
+        return fail(AGN_ENOMEM, "oplog_prune: CSR scratch");
+    }
+    agn_log out;
+    std::memset(&out, 0, sizeof out);
+    out.key_off = c_off;
+    out.oc = c.oc;
+    out.oc_mask = c.mask;
+    out.op_id = c.op_id;
+    out.txid = c.txid;
+    out.eff = c.eff;
+    out.tag = c.tag;
+    out.add_tok = c.add;
+    out.rem_off = c.rem_off;
+    out.rem_tok = c.tok;
+    rc = launch_prune_ops(view, prune, threshold, threshold_mask, out, out_flags, nullptr, st);
+    if (rc) {
+        release();
+        return rc;
+    }
+    k_csr_lens<<<(unsigned)((K + 255) / 256), 256, 0, st>>>(K, c_off, c.rem_off, lens,
+                                                            lens + K);
+    // 2. read back lengths and which keys were collected.
+    std::vector<uint32_t> nlen(2 * K);
+    std::vector<uint8_t> pr(prune ? K : 0);
+    e = hipMemcpyAsync(nlen.data(), lens, 2 * K * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && prune) e = hipMemcpyAsync(pr.data(), prune, K, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        release();
+        return fail(AGN_EHIP, "oplog_prune: read back: %s", hipGetErrorString(e));
+    }
+    // 3. new segments (resize policy on the collected keys), fresh arena.
+    std::vector<uint64_t> ns(2 * K);
+    uint64_t used = 0, tused = 0, ne = 0, nt = 0;
+    for (uint64_t k = 0; k < K; ++k) {
+        const uint32_t l = nlen[k], tl = nlen[K + k];
+        if ((!prune || pr[k]) && L->cap[k]) L->cap[k] = resize_list_len(l, L->cap[k]);
+        if (L->tags && (!prune || pr[k]) && L->tcap[k])
+            L->tcap[k] = std::max<uint32_t>(16u, std::max(tl, std::min(L->tcap[k], 2 * tl)));
+        if (L->cap[k] && L->cap[k] < l) L->cap[k] = l;  // never below the kept length
+        ns[k] = L->cap[k] ? used : ~0ull;
+        ns[K + k] = L->tcap[k] ? tused : 0;
+        if (L->cap[k]) used += (uint64_t)L->cap[k] + 1;
+        tused += L->tcap[k];
+        L->len[k] = L->dlen[k] = l;
+        L->tlen[k] = L->dtlen[k] = tl;
+        ne += l;
+        nt += tl;
+    }
+    for (uint64_t k = 0; k < K; ++k) L->start[k] = L->cap[k] ? ns[k] : 0;
+    L->tstart.assign(ns.begin() + K, ns.end());
+    Arena b;
+    uint64_t *d_start = nullptr;
+    const uint64_t U = std::max<uint64_t>(used, 1), TU = std::max<uint64_t>(tused, 1);
+    e = hipMallocAsync((void **)&d_start, 2 * K * 8, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&b.oc, U * D * 8, st);
+    if (e == hipSuccess && L->sparse) e = hipMallocAsync((void **)&b.mask, U * W * 8, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&b.op_id, U * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&b.txid, U * 8, st);
+    if (e == hipSuccess && !L->tags) e = hipMallocAsync((void **)&b.eff, U * 8, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.tag, U * 4, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.add, U * 8, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.rem_off, U * 4, st);
+    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.tok, TU * 8, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_start, ns.data(), 2 * K * 8, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) {
+        release();
+        return fail(AGN_ENOMEM, "oplog_prune: new arena");
+    }
+    k_reseg<<<(unsigned)((K + 3) / 4), 256, 0, st>>>(c, b, D, W, K, c_off, d_start,
+                                                    L->tags ? d_start + K : nullptr, L->key_off,
+                                                    L->key_len);
+    e = hipGetLastError();
+    // ns must outlive the async H2D above.
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFreeAsync(d_start, st);
+    release();
+    Arena &a = L->a;
+    for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
+                    (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok})
+        if (p) (void)hipFreeAsync(p, st);
+    L->a = b;
+    L->dcap = U;
+    L->tdcap = L->tags ? TU : 0;
+    L->used = used;
+    L->tused = tused;
+    L->n_entries = ne;
+    L->n_tokens = nt;
+    if (e != hipSuccess) return fail(AGN_EHIP, "oplog_prune: %s", hipGetErrorString(e));
+    return AGN_OK;
+}
+
+int agn_oplog_stats(const agn_oplog *L, uint64_t *entries, uint64_t *slots, uint64_t *tokens) {
+    if (!L) return fail(AGN_EINVAL, "oplog_stats: null oplog");
+    if (entries) *entries = L->n_entries;
+    if (slots) *slots = L->used;
+    if (tokens) *tokens = L->n_tokens;
+    return AGN_OK;
+}
+
+}  // extern "C"

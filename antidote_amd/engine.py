@@ -254,6 +254,71 @@ class Engine:
         check(self.lib.agn_gst_allreduce(self.ctx, vec_ptr, n_words_, stream), "agn_gst_allreduce")
 
 
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class OpLog:
+    """Engine-owned per-partition op log (agn_oplog_*): the materializer_vnode
+    ETS ops cache (src/materializer_vnode.erl:621-647) resident in HBM.
+    `append` mirrors op_insert_gc for a batch of entries (host arrays),
+    `flush` returns the device view (an AgnLog with key_len) for
+    Engine.materialize / ss_store, `prune` is snapshot_insert_gc's
+    prune_ops + ETS resize."""
+
+    def __init__(self, eng: Engine, crdt_type: int, n_dcs: int, n_keys: int,
+                 sparse: bool = False, init_slots: int = 0):
+        self.eng, self.crdt_type, self.n_dcs, self.n_keys = eng, crdt_type, n_dcs, n_keys
+        self.sparse = sparse
+        self.h = C.c_void_p()
+        check(eng.lib.agn_oplog_create(eng.ctx, crdt_type, n_dcs, n_keys, int(sparse),
+                                       init_slots, C.byref(self.h)), "agn_oplog_create")
+
+    def close(self):
+        if self.h:
+            self.eng.lib.agn_oplog_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def append(self, keys, oc, *, oc_mask=None, txid=None, eff=None, tag=None, add_tok=None,
+               rem_off=None, rem_tok=None, same_op=None):
+        """Returns (op_id[n] u32, gc_due[n] u8)."""
+        keys = np.ascontiguousarray(keys, np.uint64)
+        n = len(keys)
+        cv = lambda a, dt: None if a is None else np.ascontiguousarray(a, dt)  # noqa: E731
+        oc, oc_mask, txid = cv(oc, np.uint64), cv(oc_mask, np.uint64), cv(txid, np.uint64)
+        eff, tag, add_tok = cv(eff, np.int64), cv(tag, np.uint32), cv(add_tok, np.uint64)
+        rem_off, rem_tok, same_op = cv(rem_off, np.uint32), cv(rem_tok, np.uint64), \
+            cv(same_op, np.uint8)
+        if rem_tok is not None and rem_tok.size == 0:
+            rem_tok = np.zeros(1, np.uint64)
+        ids, due = np.zeros(n, np.uint32), np.zeros(n, np.uint8)
+        check(self.eng.lib.agn_oplog_append(
+            self.h, n, _ptr(keys), _ptr(same_op), _ptr(oc), _ptr(oc_mask), _ptr(txid), _ptr(eff),
+            _ptr(tag), _ptr(add_tok), _ptr(rem_off), _ptr(rem_tok), _ptr(ids), _ptr(due)),
+            "agn_oplog_append")
+        return ids, due
+
+    def flush(self, stream=None) -> _abi.AgnLog:
+        v = _abi.AgnLog()
+        check(self.eng.lib.agn_oplog_flush(self.h, C.byref(v), stream), "agn_oplog_flush")
+        return v
+
+    def prune(self, prune_ptr, thr_ptr, thr_mask_ptr=None, flags_ptr=None, stream=None):
+        check(self.eng.lib.agn_oplog_prune(self.h, prune_ptr, thr_ptr, thr_mask_ptr, flags_ptr,
+                                           stream), "agn_oplog_prune")
+
+    def stats(self):
+        e, s, t = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(self.eng.lib.agn_oplog_stats(self.h, C.byref(e), C.byref(s), C.byref(t)))
+        return {"entries": e.value, "slots": s.value, "tokens": t.value}
+
+
 def gen_host(cfg: _abi.AgnGenCfg):
     """Host-generated synthetic log (library-owned arrays) as numpy views."""
     lib = load()

@@ -176,6 +176,58 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req,
 int agn_state_capacity(const agn_log *host_log, const agn_read *host_req,
                        uint64_t *cap_off);
 
+/* ---- engine-owned op log: one per partition ------------------------------
+ * The materializer_vnode ETS ops cache (ops_cache-<P>,
+ * src/materializer_vnode.erl:284-286, 321-338) resident in HBM: per key a
+ * segment of `cap` slots (the ETS tuple's ListLen: OPS_THRESHOLD = 50 slots
+ * at first, doubling) holding its ops oldest first, plus the per-key op
+ * counter of ets:update_counter (:630).  update/2 calls are staged on the
+ * host and moved to HBM by agn_oplog_flush in one batched transfer + scatter
+ * kernel (the micro-batch of a partition's writes); reads then run on the
+ * flushed view.  Single writer: append / flush / prune of one oplog must be
+ * serialised by the caller (the vnode process); views are invalidated by the
+ * next append, flush or prune. */
+#define AGN_OPS_THRESHOLD 50 /* src/materializer_vnode.erl:41 */
+#define AGN_RESIZE_THRESHOLD 5 /* :44 */
+typedef struct agn_oplog agn_oplog;
+/* init_slots: a key's first segment (0 = AGN_OPS_THRESHOLD, as :626). */
+int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t n_keys,
+                     int sparse, uint32_t init_slots, agn_oplog **out);
+int agn_oplog_destroy(agn_oplog *log);
+/* materializer_vnode:update/2 -> op_insert_gc/3 for n log entries (host
+ * arrays).  Entry i belongs to key keys[i]; same_op[i] = 1 (same_op may be
+ * NULL) continues the previous entry's op (an effect with several parts,
+ * e.g. set_aw add_all), which must be of the same key; every other entry
+ * starts an op whose id is ++counter[key] (ets:update_counter(OpsCache, Key,
+ * {3, 1}), :630), written to out_op_id[i] (may be NULL).  out_gc_due[i]
+ * (may be NULL) = 1 where op_insert_gc would first run its GC read (:635:
+ * Length >= ListLen or NewId rem OPS_THRESHOLD == 0, counted in entries
+ * before this one is inserted); the engine grows the segment instead of
+ * forcing it, the caller may run the GC read (agn_materialize +
+ * agn_ss_store(should_gc) + agn_oplog_prune) when it sees the flag.  oc[n][D] is the
+ * OpSSCommit row (+ oc_mask[n][W] for a sparse log), txid may be NULL, the
+ * effect arrays are those of the log's type, rem_off[n+1] is a CSR into
+ * rem_tok. */
+int agn_oplog_append(agn_oplog *log, uint64_t n, const uint64_t *keys, const uint8_t *same_op,
+                     const uint64_t *oc, const uint64_t *oc_mask, const uint64_t *txid,
+                     const int64_t *eff, const uint32_t *tag, const uint64_t *add_tok,
+                     const uint32_t *rem_off, const uint64_t *rem_tok, uint32_t *out_op_id,
+                     uint8_t *out_gc_due);
+/* Moves the staged appends to HBM (ordered on `stream`) and fills *view with
+ * the device descriptor (key_off = segment starts, key_len) for
+ * agn_materialize / agn_ss_store / agn_prune_ops. */
+int agn_oplog_flush(agn_oplog *log, agn_log *view, void *stream);
+/* GC of the resident log: snapshot_insert_gc's prune_ops for every key with
+ * prune[k] != 0 (device arrays, e.g. from agn_ss_store), then the ETS resize
+ * policy (:540-560: ListLen doubles when fewer than RESIZE_THRESHOLD slots
+ * stay free, halves when that leaves room and stays above OPS_THRESHOLD).
+ * Flushes first and synchronises `stream` (the new lengths are read back).
+ * out_flags (device, may be NULL) as agn_prune_ops. */
+int agn_oplog_prune(agn_oplog *log, const uint8_t *prune, const uint64_t *threshold,
+                    const uint64_t *threshold_mask, uint32_t *out_flags, void *stream);
+/* Host-side accounting: entries in use, allocated slots, removal tokens. */
+int agn_oplog_stats(const agn_oplog *log, uint64_t *entries, uint64_t *slots, uint64_t *tokens);
+
 /* ---- base-snapshot selection: vector_orddict:get_smaller/2 --------------
  * (src/vector_orddict.erl:74-87, called from
  * src/materializer_vnode.erl:400).  cache_off[n_req+1] CSR over cached

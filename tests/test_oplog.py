@@ -1,0 +1,307 @@
+"""SURVEY.md §8(b) ownership: the engine-owned op log (agn_oplog_*), the
+materializer_vnode ETS ops cache (src/materializer_vnode.erl:621-647) kept in
+HBM.  A random log is appended op by op in random interleavings and batch
+sizes (segments start small so they move and grow), flushed, and then:
+
+* the op ids it assigns are the per-key counter of ets:update_counter (:630);
+* agn_materialize over the flushed view (segments with key_len) is bit-exact
+  with the C oracle over the same ops in CSR form;
+* agn_oplog_prune leaves, per key, exactly the oracle's prune_ops output
+  (snapshot_insert_gc, :513-604), and the log stays appendable after it."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from antidote_amd import _abi
+from antidote_amd.encode import (EncodedLog, alloc_result, log_struct, read_struct,
+                                 result_struct, state_capacity)
+from antidote_amd.engine import OpLog
+from synth import compare, random_case
+from test_prune import oracle_prune, thresholds
+
+pytestmark = pytest.mark.gpu
+
+
+def dl(eng, ptr, dtype, n):
+    out = np.empty(n, dtype)
+    if n:
+        assert eng.lib.agn_memcpy_d2h(eng.ctx, out.ctypes.data, ptr, out.nbytes, None) == 0
+    return out
+
+
+def ops_of(log):
+    """Entries grouped into ops: (key, first entry, n entries), per key oldest first."""
+    ops = []
+    for k in range(log.n_keys):
+        a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+        e = a
+        while e < b:
+            f = e + 1
+            while f < b and log.op_id[f] == log.op_id[e]:
+                f += 1
+            ops.append((k, e, f - e))
+            e = f
+    return ops
+
+
+def interleave(rng, ops):
+    """Random global order of the ops that keeps each key's own order."""
+    by_key: dict = {}
+    for op in ops:
+        by_key.setdefault(op[0], []).append(op)
+    seq = np.array([op[0] for op in ops], np.int64)
+    rng.shuffle(seq)
+    pos = {k: 0 for k in by_key}
+    out = []
+    for k in seq:
+        out.append(by_key[k][pos[k]])
+        pos[k] += 1
+    return out
+
+
+def append_ops(oplog, log, ops, rng, flush_p=0.5, max_batch=40):
+    """Appends `ops` in random batches; returns {entry: assigned op id}."""
+    tags = log.crdt_type != _abi.COUNTER_PN
+    got = {}
+    i = 0
+    while i < len(ops):
+        nb = int(rng.integers(1, max_batch + 1))
+        batch = ops[i:i + nb]
+        i += nb
+        ent = [(k, e0 + j, j > 0) for k, e0, n in batch for j in range(n)]
+        es = np.array([e for _, e, _ in ent], np.int64)
+        kw = dict(oc=log.oc[es], txid=log.txid[es],
+                  same_op=np.array([s for *_, s in ent], np.uint8))
+        if log.oc_mask is not None:
+            kw["oc_mask"] = log.oc_mask[es]
+        if tags:
+            lens = (log.rem_off[es + 1] - log.rem_off[es]).astype(np.int64)
+            ro = np.zeros(len(es) + 1, np.uint32)
+            ro[1:] = np.cumsum(lens)
+            toks = [log.rem_tok[int(log.rem_off[e]):int(log.rem_off[e + 1])] for e in es]
+            kw.update(tag=log.tag[es], add_tok=log.add_tok[es], rem_off=ro,
+                      rem_tok=np.concatenate(toks) if toks else np.zeros(0, np.uint64))
+        else:
+            kw["eff"] = log.eff[es]
+        ids, _ = oplog.append(np.array([k for k, _, _ in ent], np.uint64), **kw)
+        for (_, e, _), op_id in zip(ent, ids):
+            got[e] = int(op_id)
+        if rng.random() < flush_p:
+            oplog.flush()
+    return got
+
+
+def renumbered(log, got):
+    out = EncodedLog(**{f: getattr(log, f) for f in ("crdt_type", "n_dcs", "key_off", "key_type",
+                                                      "oc", "oc_mask", "txid", "eff", "tag",
+                                                      "add_tok", "rem_off", "rem_tok")},
+                     op_id=np.array([got[e] for e in range(log.n_entries)], np.uint32))
+    return out
+
+
+def expect_counter_ids(log, got, start=None):
+    """Per key: ops numbered start[k]+1, +2, ... in order (ets:update_counter)."""
+    for k in range(log.n_keys):
+        a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+        nxt = 0 if start is None else int(start[k])
+        for e in range(a, b):
+            if e == a or log.op_id[e] != log.op_id[e - 1]:
+                nxt += 1
+            assert got[e] == nxt, (k, e)
+
+
+def materialize_view(eng, oracle_lib, view, log, req, sparse):
+    cap = state_capacity(log, req)
+    dreq = eng.upload_read(req, sparse=sparse)
+    dres = eng.alloc_result(req.n_req, log.n_dcs, sparse, cap_off=cap)
+    eng.materialize(view, dreq, dres)
+    eng.sync()
+    res_g = eng.fetch_result(dres)
+    res_o = alloc_result(req.n_req, log.n_dcs, sparse=sparse, cap_off=cap)
+    ls, rs, os_ = log_struct(log), read_struct(req, sparse=sparse), result_struct(res_o)
+    if log.oc_mask is None:
+        ls.oc_mask = None
+    assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
+    for d in (dreq, dres):
+        for b in d.bufs.values():
+            b.free()
+    return compare(log.crdt_type, log.n_dcs, res_g, res_o, sparse, req.n_req)
+
+
+def segments(eng, view, K, D, W, tags, sparse):
+    """Downloads the view: per key a dict of its entry arrays."""
+    off = dl(eng, view.key_off, np.uint64, K)
+    ln = dl(eng, view.key_len, np.uint64, K)
+    n = int(view.n_entries)
+    arrs = {"oc": dl(eng, view.oc, np.uint64, n * D).reshape(n, D),
+            "op_id": dl(eng, view.op_id, np.uint32, n), "txid": dl(eng, view.txid, np.uint64, n)}
+    if sparse:
+        arrs["oc_mask"] = dl(eng, view.oc_mask, np.uint64, n * W).reshape(n, W)
+    if tags:
+        arrs["tag"] = dl(eng, view.tag, np.uint32, n)
+        arrs["add_tok"] = dl(eng, view.add_tok, np.uint64, n)
+        arrs["rem_off"] = dl(eng, view.rem_off, np.uint32, n)
+    else:
+        arrs["eff"] = dl(eng, view.eff, np.int64, n)
+    ntok = max((int(arrs["rem_off"][int(off[k]) + int(ln[k])]) for k in range(K) if ln[k]),
+               default=0) if tags else 0
+    tok = dl(eng, view.rem_tok, np.uint64, ntok) if ntok else np.zeros(0, np.uint64)
+    out = []
+    for k in range(K):
+        a, b = int(off[k]), int(off[k]) + int(ln[k])
+        seg = {name: v[a:b] for name, v in arrs.items() if name != "rem_off"}
+        if tags:
+            ro = arrs["rem_off"]
+            seg["rems"] = [tok[int(ro[e]):int(ro[e + 1])].tolist() for e in range(a, b)]
+        out.append(seg)
+    return out
+
+
+def csr_key(arrs, k, tags):
+    a, b = int(arrs["key_off"][k]), int(arrs["key_off"][k + 1])
+    seg = {name: v[a:b] for name, v in arrs.items()
+           if v is not None and name not in ("key_off", "rem_off", "rem_tok")}
+    if tags:
+        ro, tok = arrs["rem_off"], arrs["rem_tok"]
+        seg["rems"] = [tok[int(ro[e]):int(ro[e + 1])].tolist() for e in range(a, b)]
+    return seg
+
+
+CASES = [(_abi.COUNTER_PN, 8, False, 4), (_abi.COUNTER_PN, 3, True, 0),
+         (_abi.COUNTER_PN, 70, True, 2), (_abi.SET_AW, 5, False, 4), (_abi.SET_AW, 16, True, 1),
+         (_abi.REGISTER_MV, 8, False, 3), (_abi.REGISTER_MV, 64, True, 0)]
+
+
+@pytest.mark.parametrize("crdt,D,sparse,init", CASES)
+def test_oplog_append_materialize(eng, oracle_lib, crdt, D, sparse, init):
+    rng = np.random.default_rng(D * 7 + crdt + 100 * init)
+    log, req, _ = random_case(5 * D + crdt + init, crdt, 80, D, 70, sparse=sparse, warm=0.3,
+                              txid=0.2, multi=0.2 if crdt == _abi.SET_AW else 0.0, empty=0.1)
+    with OpLog(eng, crdt, D, log.n_keys, sparse=sparse, init_slots=init) as ol:
+        got = append_ops(ol, log, interleave(rng, ops_of(log)), rng)
+        expect_counter_ids(log, got)
+        log2 = renumbered(log, got)
+        view = ol.flush()
+        st = ol.stats()
+        assert st["entries"] == log.n_entries and st["slots"] >= log.n_entries
+        assert not materialize_view(eng, oracle_lib, view, log2, req, sparse)
+
+
+@pytest.mark.parametrize("crdt,D,sparse,init", CASES)
+def test_oplog_prune_then_append(eng, oracle_lib, crdt, D, sparse, init):
+    rng = np.random.default_rng(D * 11 + crdt + init)
+    tags = crdt != _abi.COUNTER_PN
+    W = (D + 63) // 64
+    log, req, _ = random_case(9 * D + crdt + init, crdt, 60, D, 90, sparse=sparse,
+                              multi=0.2 if crdt == _abi.SET_AW else 0.0, empty=0.1)
+    with OpLog(eng, crdt, D, log.n_keys, sparse=sparse, init_slots=init) as ol:
+        got = append_ops(ol, log, interleave(rng, ops_of(log)), rng)
+        log2 = renumbered(log, got)
+        prune, thr, tm = thresholds(D + crdt + 5, log2, sparse)
+        want, wflags, n_out = oracle_prune(oracle_lib, log2, prune, thr, tm)
+        bp, bt = eng.upload(prune), eng.upload(thr)
+        btm = eng.upload(tm) if tm is not None else None
+        fl = eng.empty(4 * log.n_keys)
+        ol.prune(bp.ptr, bt.ptr, btm.ptr if btm else None, fl.ptr)
+        assert np.array_equal(eng.download(fl, np.uint32, (log.n_keys,)), wflags)
+        assert ol.stats()["entries"] == n_out
+        view = ol.flush()
+        segs = segments(eng, view, log.n_keys, D, W, tags, sparse)
+        for k in range(log.n_keys):
+            w = csr_key(want, k, tags)
+            for name, v in w.items():
+                g = segs[k][name]
+                if name == "rems":
+                    assert g == v, (k, name)
+                else:
+                    assert np.array_equal(np.asarray(g), np.asarray(v)), (k, name)
+        # Materialize the pruned log, then keep appending to it.
+        pruned = EncodedLog(crdt_type=crdt, n_dcs=D, key_off=want["key_off"],
+                            key_type=np.full(log.n_keys, crdt, np.uint8),
+                            oc=want["oc"][:n_out], oc_mask=None if tm is None else
+                            want["oc_mask"][:n_out], op_id=want["op_id"][:n_out],
+                            txid=want["txid"][:n_out])
+        if tags:
+            nr = int(want["rem_off"][n_out])
+            pruned.tag, pruned.add_tok = want["tag"][:n_out], want["add_tok"][:n_out]
+            pruned.rem_off = want["rem_off"][:n_out + 1]
+            pruned.rem_tok = want["rem_tok"][:max(nr, 1)]
+        else:
+            pruned.eff = want["eff"][:n_out]
+        assert not materialize_view(eng, oracle_lib, view, pruned, req, sparse)
+
+        more, req2, _ = random_case(13 * D + crdt + init, crdt, 60, D, 40, sparse=sparse,
+                                    multi=0.2 if crdt == _abi.SET_AW else 0.0, empty=0.3)
+        got2 = append_ops(ol, more, interleave(rng, ops_of(more)), rng)
+        counters = np.zeros(log.n_keys, np.int64)
+        for k in range(log.n_keys):
+            a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+            counters[k] = max((got[e] for e in range(a, b)), default=0)
+        expect_counter_ids(more, got2, counters)
+        both = concat(pruned, renumbered(more, got2))
+        view = ol.flush()
+        assert not materialize_view(eng, oracle_lib, view, both, req2, sparse)
+        for b in (bp, bt, btm, fl):
+            if b is not None:
+                b.free()
+
+
+def concat(a, b):
+    """Per key: a's entries then b's (both CSR)."""
+    K, tags = a.n_keys, a.crdt_type != _abi.COUNTER_PN
+    idx, src = [], []
+    for k in range(K):
+        for log, s in ((a, 0), (b, 1)):
+            for e in range(int(log.key_off[k]), int(log.key_off[k + 1])):
+                idx.append(e)
+                src.append(s)
+    lens = [int(a.key_off[k + 1] - a.key_off[k] + b.key_off[k + 1] - b.key_off[k])
+            for k in range(K)]
+    key_off = np.zeros(K + 1, np.uint64)
+    key_off[1:] = np.cumsum(lens)
+    pick = lambda name: np.array([getattr(a if s == 0 else b, name)[e]  # noqa: E731
+                                  for e, s in zip(idx, src)]) if idx else \
+        getattr(a, name)[:0]
+    out = EncodedLog(crdt_type=a.crdt_type, n_dcs=a.n_dcs, key_off=key_off,
+                     key_type=a.key_type, oc=pick("oc").reshape(-1, a.n_dcs).astype(np.uint64),
+                     oc_mask=None if a.oc_mask is None else
+                     pick("oc_mask").reshape(len(idx), -1).astype(np.uint64),
+                     op_id=pick("op_id").astype(np.uint32), txid=pick("txid").astype(np.uint64))
+    if tags:
+        out.tag, out.add_tok = pick("tag").astype(np.uint32), pick("add_tok").astype(np.uint64)
+        ro, toks = [0], []
+        for e, s in zip(idx, src):
+            lg = a if s == 0 else b
+            t = lg.rem_tok[int(lg.rem_off[e]):int(lg.rem_off[e + 1])].tolist()
+            toks.extend(t)
+            ro.append(len(toks))
+        out.rem_off = np.array(ro, np.uint32)
+        out.rem_tok = np.array(toks if toks else [0], np.uint64)
+    else:
+        out.eff = pick("eff").astype(np.int64)
+    return out
+
+
+def test_oplog_gc_due_and_errors(eng):
+    with OpLog(eng, _abi.COUNTER_PN, 2, 4) as ol:
+        n = 120
+        keys = np.zeros(n, np.uint64)
+        oc = np.arange(2 * n, dtype=np.uint64).reshape(n, 2)
+        ids, due = ol.append(keys, oc, eff=np.ones(n, np.int64))
+        assert ids.tolist() == list(range(1, n + 1))
+        # op_insert_gc's trigger (:635): Length >= ListLen or NewId rem 50 == 0;
+        # the segment doubles 50 -> 100 -> 200 instead of forcing the GC.
+        assert np.flatnonzero(due).tolist() == [49, 50, 99, 100]
+        before = ol.stats()
+        with pytest.raises(Exception):
+            ol.append(np.array([1, 9], np.uint64), oc[:2], eff=np.ones(2, np.int64))
+        with pytest.raises(Exception):
+            ol.append(np.array([1], np.uint64), oc[:1], eff=np.ones(1, np.int64),
+                      same_op=np.ones(1, np.uint8))
+        assert ol.stats() == before  # rejected batches leave no trace
+        ids, _ = ol.append(np.array([1, 1, 0], np.uint64), oc[:3], eff=np.ones(3, np.int64),
+                           same_op=np.array([0, 1, 0], np.uint8))
+        assert ids.tolist() == [1, 1, 121]
+        view = ol.flush()
+        assert dl(eng, view.key_len, np.uint64, 4).tolist() == [121, 2, 0, 0]
