@@ -68,6 +68,23 @@ class AgnSsCache(C.Structure):
     ]
 
 
+class AgnKeyRead(C.Structure):
+    _fields_ = [
+        ("key", C.c_uint64), ("R", P), ("R_mask", P), ("sct", P), ("sct_mask", P),
+        ("txid", C.c_uint64), ("base_value", C.c_int64), ("n_base", C.c_uint32),
+        ("_pad", C.c_uint32), ("base_tag", P), ("base_tok", P),
+    ]
+
+
+class AgnKeyResult(C.Structure):
+    _fields_ = [
+        ("value", C.c_int64), ("hole", C.c_int64), ("lastct", P), ("lastct_mask", P),
+        ("count", C.c_uint32), ("flags", C.c_uint32), ("err_pos", C.c_uint32),
+        ("out_cap", C.c_uint32), ("out_n", C.c_uint32), ("_pad", C.c_uint32),
+        ("out_tag", P), ("out_tok", P),
+    ]
+
+
 class AgnLogRecords(C.Structure):
     _fields_ = [
         ("n", C.c_uint64), ("kind", P), ("txid", P), ("key", P), ("commit_dc", P),
@@ -127,6 +144,11 @@ PROTOTYPES = {
     "agn_oplog_append": (C.c_int, [P, C.c_uint64, P, P, P, P, P, P, P, P, P, P, P, P]),
     "agn_oplog_flush": (C.c_int, [P, C.POINTER(AgnLog), P]),
     "agn_oplog_prune": (C.c_int, [P, P, P, P, P, P]),
+    "agn_oplog_read": (C.c_int, [P, C.POINTER(AgnRead), C.POINTER(AgnResult), P]),
+    "agn_batcher_create": (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(P)]),
+    "agn_batcher_destroy": (C.c_int, [P]),
+    "agn_batcher_read": (C.c_int, [P, C.POINTER(AgnKeyRead), C.POINTER(AgnKeyResult)]),
+    "agn_batcher_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "agn_oplog_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                   C.POINTER(C.c_uint64)]),
     "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),

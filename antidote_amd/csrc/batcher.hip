@@ -1,0 +1,335 @@
+// batcher.hip — micro-batching read queue over an agn_oplog
+// (include/antidote_gpu.h, "micro-batching read queue").
+//
+// The reference serves reads per key: each of up to READ_CONCURRENCY = 20
+// read servers per partition (include/antidote.hrl:28) calls
+// materializer_vnode:read/6 (src/clocksi_readitem_server.erl:272) and runs
+// materialize/4 on its own copy of the key's ops.  On the GPU one key is
+// 1/4 of a wave of work, so calls are coalesced: callers enqueue a request
+// and block; one worker thread per batcher packs up to max_batch requests
+// into one pinned buffer, does one H2D copy, one agn_oplog_read (the
+// materialize kernel over the resident log, held shared) and one D2H copy,
+// then wakes the callers.  Requests that arrive while a batch runs form the
+// next batch, so the batch size adapts to the offered load.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+
+using namespace agn;
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Pending {
+    const agn_key_read *rd;
+    agn_key_result *out;
+    Clock::time_point t;
+    int rc = AGN_OK;
+    bool done = false;
+    char err[256] = "";
+};
+
+inline size_t al(size_t b) { return (b + 255) & ~size_t(255); }
+
+}  // namespace
+
+struct agn_batcher {
+    agn_oplog *log = nullptr;
+    agn_ctx *ctx = nullptr;
+    uint32_t crdt = 0, D = 0, W = 0;
+    int sparse_log = 0;
+    uint64_t K = 0;
+    uint32_t max_batch = 0, max_wait_us = 0;
+
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<Pending *> q;
+    bool stop = false;
+    std::thread worker;
+
+    hipStream_t stream = nullptr;
+    char *dbuf = nullptr, *hbuf = nullptr;  // device / pinned [in | out]
+    size_t cap = 0;
+    std::atomic<uint64_t> n_batches{0}, n_reads{0};
+};
+
+namespace {
+
+int grow(agn_batcher *B, size_t bytes) {
+    if (bytes <= B->cap) return AGN_OK;
+    size_t c = std::max(bytes, 2 * B->cap);
+    if (B->dbuf) AGN_HIP(hipFree(B->dbuf));
+    if (B->hbuf) AGN_HIP(hipHostFree(B->hbuf));
+    B->dbuf = B->hbuf = nullptr;
+    B->cap = 0;
+    AGN_HIP(hipMalloc((void **)&B->dbuf, c));
+    AGN_HIP(hipHostMalloc((void **)&B->hbuf, c, hipHostMallocDefault));
+    B->cap = c;
+    return AGN_OK;
+}
+
+// One batch: pack, copy in, materialize over the resident log, copy out, unpack.
+int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
+    const uint64_t n = b.size();
+    const uint32_t D = B->D, W = B->W;
+    const bool tags = B->crdt != AGN_COUNTER_PN;
+    bool sparse = B->sparse_log != 0, any_sct = false;
+    uint64_t nb = 0;
+    for (Pending *p : b) {
+        sparse = sparse || p->rd->R_mask || p->rd->sct_mask;
+        any_sct = any_sct || p->rd->sct;
+        nb += tags ? p->rd->n_base : 0;
+    }
+    std::vector<uint64_t> keys(n);
+    std::vector<uint32_t> lens(n);
+    for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
+    uint64_t ncap = 0;
+    if (tags) {
+        oplog_key_lens(B->log, n, keys.data(), lens.data());
+        for (uint64_t i = 0; i < n; ++i) ncap += (uint64_t)lens[i] + b[i]->rd->n_base;
+    }
+    // Layout: in = keys R Rm sct sctm sign txid base_value base_off base_tag base_tok cap_off
+    //         out = value hole lastct lastct_mask count flags err_pos out_n out_tag out_tok
+    size_t off = 0;
+    auto slot = [&](size_t bytes) { size_t o = off; off = al(off + bytes); return o; };
+    const size_t o_keys = slot(n * 8), o_R = slot(n * D * 8), o_Rm = slot(sparse ? n * W * 8 : 0),
+                 o_sct = slot(any_sct ? n * D * 8 : 0),
+                 o_sctm = slot(any_sct && sparse ? n * W * 8 : 0), o_sign = slot(any_sct ? n : 0),
+                 o_txid = slot(n * 8), o_bv = slot(tags ? 0 : n * 8),
+                 o_boff = slot(tags ? (n + 1) * 8 : 0), o_btag = slot(tags ? nb * 4 : 0),
+                 o_btok = slot(tags ? nb * 8 : 0), o_cap = slot(tags ? (n + 1) * 8 : 0);
+    const size_t in_bytes = off;
+    const size_t o_val = slot(n * 8), o_hole = slot(n * 8), o_ct = slot(n * D * 8),
+                 o_ctm = slot(sparse ? n * W * 8 : 0), o_cnt = slot(n * 4), o_flg = slot(n * 4),
+                 o_epos = slot(n * 4), o_outn = slot(tags ? n * 4 : 0),
+                 o_otag = slot(tags ? ncap * 4 : 0), o_otok = slot(tags ? ncap * 8 : 0);
+    int rc = grow(B, off);
+    if (rc) return rc;
+    char *h = B->hbuf, *d = B->dbuf;
+    std::memset(h, 0, in_bytes);
+    auto H = [&](size_t o) { return h + o; };
+    uint64_t full[4] = {0, 0, 0, 0};
+    for (uint32_t x = 0; x < D; ++x) full[x >> 6] |= 1ull << (x & 63);
+    uint64_t bpos = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const agn_key_read *r = b[i]->rd;
+        ((uint64_t *)H(o_keys))[i] = r->key;
+        std::memcpy(H(o_R) + i * D * 8, r->R, D * 8);
+        if (sparse) std::memcpy(H(o_Rm) + i * W * 8, r->R_mask ? r->R_mask : full, W * 8);
+        if (any_sct) {
+            if (r->sct) {
+                std::memcpy(H(o_sct) + i * D * 8, r->sct, D * 8);
+                if (sparse) std::memcpy(H(o_sctm) + i * W * 8, r->sct_mask ? r->sct_mask : full, W * 8);
+            } else {
+                ((uint8_t *)H(o_sign))[i] = 1;
+            }
+        }
+        ((uint64_t *)H(o_txid))[i] = r->txid;
+        if (tags) {
+            ((uint64_t *)H(o_boff))[i] = bpos;
+            if (r->n_base) {
+                std::memcpy(H(o_btag) + bpos * 4, r->base_tag, r->n_base * 4);
+                std::memcpy(H(o_btok) + bpos * 8, r->base_tok, r->n_base * 8);
+            }
+            bpos += r->n_base;
+        } else {
+            ((int64_t *)H(o_bv))[i] = r->base_value;
+        }
+    }
+    if (tags) {
+        ((uint64_t *)H(o_boff))[n] = bpos;
+        uint64_t *co = (uint64_t *)H(o_cap);
+        co[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + b[i]->rd->n_base;
+    }
+    AGN_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, B->stream));
+
+    agn_read req;
+    std::memset(&req, 0, sizeof req);
+    req.n_req = n;
+    req.keys = (const uint64_t *)(d + o_keys);
+    req.R = (const uint64_t *)(d + o_R);
+    req.R_mask = sparse ? (const uint64_t *)(d + o_Rm) : nullptr;
+    if (any_sct) {
+        req.sct = (const uint64_t *)(d + o_sct);
+        req.sct_mask = sparse ? (const uint64_t *)(d + o_sctm) : nullptr;
+        req.sct_ignore = (const uint8_t *)(d + o_sign);
+    }
+    req.txid = (const uint64_t *)(d + o_txid);
+    req.req_type = B->crdt;
+    if (tags) {
+        req.base_off = (const uint64_t *)(d + o_boff);
+        req.base_tag = (const uint32_t *)(d + o_btag);
+        req.base_tok = (const uint64_t *)(d + o_btok);
+    } else {
+        req.base_value = (const int64_t *)(d + o_bv);
+    }
+    agn_result res;
+    std::memset(&res, 0, sizeof res);
+    res.value = (int64_t *)(d + o_val);
+    res.hole = (int64_t *)(d + o_hole);
+    res.lastct = (uint64_t *)(d + o_ct);
+    res.lastct_mask = sparse ? (uint64_t *)(d + o_ctm) : nullptr;
+    res.count = (uint32_t *)(d + o_cnt);
+    res.flags = (uint32_t *)(d + o_flg);
+    res.err_pos = (uint32_t *)(d + o_epos);
+    if (tags) {
+        res.out_off = (const uint64_t *)(d + o_cap);
+        res.out_n = (uint32_t *)(d + o_outn);
+        res.out_tag = (uint32_t *)(d + o_otag);
+        res.out_tok = (uint64_t *)(d + o_otok);
+    }
+    rc = agn_oplog_read(B->log, &req, &res, B->stream);
+    if (rc) return rc;
+    AGN_HIP(hipMemcpyAsync(h + in_bytes, d + in_bytes, off - in_bytes, hipMemcpyDeviceToHost,
+                           B->stream));
+    AGN_HIP(hipStreamSynchronize(B->stream));
+    for (uint64_t i = 0; i < n; ++i) {
+        agn_key_result *o = b[i]->out;
+        o->value = tags ? 0 : ((const int64_t *)H(o_val))[i];
+        o->hole = ((const int64_t *)H(o_hole))[i];
+        std::memcpy(o->lastct, H(o_ct) + i * D * 8, D * 8);
+        if (o->lastct_mask) std::memcpy(o->lastct_mask, sparse ? H(o_ctm) + i * W * 8 : (char *)full, W * 8);
+        o->count = ((const uint32_t *)H(o_cnt))[i];
+        o->flags = ((const uint32_t *)H(o_flg))[i];
+        o->err_pos = ((const uint32_t *)H(o_epos))[i];
+        if (tags) {
+            const uint32_t m = ((const uint32_t *)H(o_outn))[i];
+            const uint64_t s = ((const uint64_t *)H(o_cap))[i];
+            o->out_n = m;
+            if (m > o->out_cap) {
+                b[i]->rc = AGN_ECAPACITY;
+                std::snprintf(b[i]->err, sizeof b[i]->err, "batcher_read: %u pairs, out_cap %u", m,
+                              o->out_cap);
+                continue;
+            }
+            if (m) {
+                std::memcpy(o->out_tag, H(o_otag) + s * 4, m * 4);
+                std::memcpy(o->out_tok, H(o_otok) + s * 8, m * 8);
+            }
+        }
+    }
+    return AGN_OK;
+}
+
+void worker_main(agn_batcher *B) {
+    (void)use_device(B->ctx);
+    std::unique_lock<std::mutex> lk(B->mu);
+    for (;;) {
+        B->cv_work.wait(lk, [&] { return B->stop || !B->q.empty(); });
+        if (B->q.empty()) break;  // stop requested and drained
+        const auto deadline = B->q.front()->t + std::chrono::microseconds(B->max_wait_us);
+        while (!B->stop && B->q.size() < B->max_batch && Clock::now() < deadline)
+            B->cv_work.wait_until(lk, deadline);
+        const size_t n = std::min<size_t>(B->q.size(), B->max_batch);
+        std::vector<Pending *> batch(B->q.begin(), B->q.begin() + n);
+        B->q.erase(B->q.begin(), B->q.begin() + n);
+        lk.unlock();
+        int rc = run_batch(B, batch);
+        if (rc)
+            for (Pending *p : batch) {
+                p->rc = rc;
+                std::snprintf(p->err, sizeof p->err, "%s", agn_last_error());
+            }
+        B->n_batches.fetch_add(1, std::memory_order_relaxed);
+        B->n_reads.fetch_add(n, std::memory_order_relaxed);
+        lk.lock();
+        for (Pending *p : batch) p->done = true;
+        B->cv_done.notify_all();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int agn_batcher_create(agn_oplog *log, uint32_t max_batch, uint32_t max_wait_us,
+                       agn_batcher **out) {
+    if (!out || !log) return fail(AGN_EINVAL, "batcher_create: null argument");
+    *out = nullptr;
+    if (max_batch == 0) return fail(AGN_EINVAL, "batcher_create: max_batch = 0");
+    agn_batcher *B = new (std::nothrow) agn_batcher;
+    if (!B) return fail(AGN_ENOMEM, "batcher_create");
+    B->log = log;
+    B->ctx = oplog_ctx(log);
+    oplog_shape(log, &B->crdt, &B->D, &B->sparse_log, &B->K);
+    B->W = n_words(B->D);
+    B->max_batch = max_batch;
+    B->max_wait_us = max_wait_us;
+    int rc = use_device(B->ctx);
+    if (rc == AGN_OK && hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = fail(AGN_EHIP, "batcher_create: stream");
+    if (rc) {
+        delete B;
+        return rc;
+    }
+    try {
+        B->worker = std::thread(worker_main, B);
+    } catch (...) {
+        (void)hipStreamDestroy(B->stream);
+        delete B;
+        return fail(AGN_ENOMEM, "batcher_create: worker thread");
+    }
+    *out = B;
+    return AGN_OK;
+}
+
+int agn_batcher_destroy(agn_batcher *B) {
+    if (!B) return AGN_OK;
+    {
+        std::lock_guard<std::mutex> g(B->mu);
+        B->stop = true;
+    }
+    B->cv_work.notify_all();
+    if (B->worker.joinable()) B->worker.join();
+    (void)use_device(B->ctx);
+    if (B->dbuf) (void)hipFree(B->dbuf);
+    if (B->hbuf) (void)hipHostFree(B->hbuf);
+    if (B->stream) (void)hipStreamDestroy(B->stream);
+    delete B;
+    return AGN_OK;
+}
+
+int agn_batcher_read(agn_batcher *B, const agn_key_read *rd, agn_key_result *out) {
+    if (!B || !rd || !out) return fail(AGN_EINVAL, "batcher_read: null argument");
+    if (rd->key >= B->K) return fail(AGN_EINVAL, "batcher_read: key %llu >= n_keys",
+                                     (unsigned long long)rd->key);
+    if (!rd->R || !out->lastct) return fail(AGN_EINVAL, "batcher_read: R / lastct required");
+    if (B->crdt != AGN_COUNTER_PN) {
+        if (rd->n_base && (!rd->base_tag || !rd->base_tok))
+            return fail(AGN_EINVAL, "batcher_read: base pairs missing");
+        if (out->out_cap && (!out->out_tag || !out->out_tok))
+            return fail(AGN_EINVAL, "batcher_read: out_tag / out_tok missing");
+    }
+    Pending p;
+    p.rd = rd;
+    p.out = out;
+    p.t = Clock::now();
+    std::unique_lock<std::mutex> lk(B->mu);
+    if (B->stop) return fail(AGN_EINVAL, "batcher_read: batcher is shutting down");
+    B->q.push_back(&p);
+    if (B->q.size() == 1 || B->q.size() >= B->max_batch) B->cv_work.notify_one();
+    B->cv_done.wait(lk, [&] { return p.done; });
+    if (p.rc) return fail(p.rc, "%s", p.err);
+    return AGN_OK;
+}
+
+int agn_batcher_stats(agn_batcher *B, uint64_t *batches, uint64_t *reads) {
+    if (!B) return fail(AGN_EINVAL, "batcher_stats: null batcher");
+    if (batches) *batches = B->n_batches.load();
+    if (reads) *reads = B->n_reads.load();
+    return AGN_OK;
+}
+
+}  // extern "C"

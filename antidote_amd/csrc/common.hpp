@@ -91,6 +91,11 @@ inline unsigned resident_grid(K kernel, unsigned threads, uint64_t work_blocks) 
     return (unsigned)(b < 1 ? 1 : b);
 }
 
+// oplog.hip internals used by the read batcher.
+void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, uint64_t *K);
+void oplog_key_lens(const agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t *out);
+agn_ctx *oplog_ctx(const agn_oplog *L);
+
 // Launchers (defined in the .hip files).
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t s);

@@ -27,6 +27,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <new>
+#include <shared_mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -212,6 +215,13 @@ struct agn_oplog {
     uint32_t crdt = 0, D = 0, W = 0, init_slots = AGN_OPS_THRESHOLD;
     bool sparse = false, tags = false;
     uint64_t K = 0;
+
+    // Locking: `wmu` guards the host side (metadata + staging: append),
+    // `rw` the device arenas — shared by readers (agn_oplog_read) for the
+    // whole of their kernel, exclusive for flush / prune, which move and free
+    // segments.  Order: wmu before rw.
+    mutable std::mutex wmu;
+    std::shared_mutex rw;
 
     // host metadata per key
     std::vector<uint64_t> start, tstart;
@@ -503,6 +513,13 @@ int agn_oplog_destroy(agn_oplog *L) {
     return AGN_OK;
 }
 
+static int oplog_append_locked(agn_oplog *L, uint64_t n, const uint64_t *keys,
+                               const uint8_t *same_op, const uint64_t *oc,
+                               const uint64_t *oc_mask, const uint64_t *txid, const int64_t *eff,
+                               const uint32_t *tag, const uint64_t *add_tok,
+                               const uint32_t *rem_off, const uint64_t *rem_tok,
+                               uint32_t *out_op_id, uint8_t *out_gc_due);
+
 int agn_oplog_append(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint8_t *same_op,
                      const uint64_t *oc, const uint64_t *oc_mask, const uint64_t *txid,
                      const int64_t *eff, const uint32_t *tag, const uint64_t *add_tok,
@@ -510,6 +527,21 @@ int agn_oplog_append(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint8
                      uint8_t *out_gc_due) {
     if (!L) return fail(AGN_EINVAL, "oplog_append: null oplog");
     if (n == 0) return AGN_OK;
+    std::lock_guard<std::mutex> g(L->wmu);
+    try {
+        return oplog_append_locked(L, n, keys, same_op, oc, oc_mask, txid, eff, tag, add_tok,
+                                   rem_off, rem_tok, out_op_id, out_gc_due);
+    } catch (const std::bad_alloc &) {
+        return fail(AGN_ENOMEM, "oplog_append: host staging");
+    }
+}
+
+static int oplog_append_locked(agn_oplog *L, uint64_t n, const uint64_t *keys,
+                               const uint8_t *same_op, const uint64_t *oc,
+                               const uint64_t *oc_mask, const uint64_t *txid, const int64_t *eff,
+                               const uint32_t *tag, const uint64_t *add_tok,
+                               const uint32_t *rem_off, const uint64_t *rem_tok,
+                               uint32_t *out_op_id, uint8_t *out_gc_due) {
     if (!keys || !oc) return fail(AGN_EINVAL, "oplog_append: keys / oc required");
     if (L->sparse && !oc_mask) return fail(AGN_EINVAL, "oplog_append: sparse log needs oc_mask");
     if (L->tags ? (!tag || !add_tok || !rem_off || (rem_off[n] > rem_off[0] && !rem_tok)) : !eff)
@@ -572,8 +604,12 @@ int agn_oplog_flush(agn_oplog *L, agn_log *view, void *stream) {
     if (!L) return fail(AGN_EINVAL, "oplog_flush: null oplog");
     int rc = use_device(L->ctx);
     if (rc) return rc;
+    std::lock_guard<std::mutex> g(L->wmu);
+    std::unique_lock<std::shared_mutex> x(L->rw);
     rc = do_flush(L, (hipStream_t)stream);
     if (rc) return rc;
+    // Readers on other streams must see the scattered entries.
+    AGN_HIP(hipStreamSynchronize((hipStream_t)stream));
     if (view) fill_view(L, view);
     return AGN_OK;
 }
@@ -585,6 +621,8 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     if (L->sparse && !threshold_mask) return fail(AGN_EINVAL, "oplog_prune: sparse log needs threshold_mask");
     int rc = use_device(L->ctx);
     if (rc) return rc;
+    std::lock_guard<std::mutex> g(L->wmu);
+    std::unique_lock<std::shared_mutex> x(L->rw);
     hipStream_t st = (hipStream_t)stream;
     rc = do_flush(L, st);
     if (rc) return rc;
@@ -710,8 +748,53 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     return AGN_OK;
 }
 
+int agn_oplog_read(agn_oplog *L, const agn_read *req, agn_result *out, void *stream) {
+    if (!L) return fail(AGN_EINVAL, "oplog_read: null oplog");
+    int rc = use_device(L->ctx);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    {
+        // Read-your-writes: update/2 is a sync_command that precedes the read.
+        std::lock_guard<std::mutex> g(L->wmu);
+        if (!L->s_key.empty() || !L->moves.empty() || !L->dirty_keys.empty()) {
+            std::unique_lock<std::shared_mutex> x(L->rw);
+            rc = do_flush(L, st);
+            if (rc) return rc;
+            AGN_HIP(hipStreamSynchronize(st));
+        }
+    }
+    std::shared_lock<std::shared_mutex> r(L->rw);
+    agn_log view;
+    fill_view(L, &view);
+    rc = agn_materialize(L->ctx, &view, req, out, stream);
+    if (rc) return rc;
+    AGN_HIP(hipStreamSynchronize(st));
+    return AGN_OK;
+}
+
+}  // extern "C"
+
+namespace agn {
+void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, uint64_t *K) {
+    *crdt = L->crdt;
+    *D = L->D;
+    *sparse = L->sparse;
+    *K = L->K;
+}
+// Current length (entries, staged included) of each key: an upper bound on
+// its live set/register pairs for the read that follows.
+void oplog_key_lens(const agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t *out) {
+    std::lock_guard<std::mutex> g(L->wmu);
+    for (uint64_t i = 0; i < n; ++i) out[i] = L->len[keys[i]];
+}
+agn_ctx *oplog_ctx(const agn_oplog *L) { return L->ctx; }
+}  // namespace agn
+
+extern "C" {
+
 int agn_oplog_stats(const agn_oplog *L, uint64_t *entries, uint64_t *slots, uint64_t *tokens) {
     if (!L) return fail(AGN_EINVAL, "oplog_stats: null oplog");
+    std::lock_guard<std::mutex> g(L->wmu);
     if (entries) *entries = L->n_entries;
     if (slots) *slots = L->used;
     if (tokens) *tokens = L->n_tokens;

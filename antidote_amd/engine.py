@@ -313,10 +313,70 @@ class OpLog:
         check(self.eng.lib.agn_oplog_prune(self.h, prune_ptr, thr_ptr, thr_mask_ptr, flags_ptr,
                                            stream), "agn_oplog_prune")
 
+    def read(self, dreq, dres, stream=None):
+        """agn_oplog_read: batched materialize/4 over the resident log (blocks)."""
+        rs = dreq.struct if isinstance(dreq, DeviceArrays) else dreq
+        os_ = dres.struct if isinstance(dres, DeviceArrays) else dres
+        check(self.eng.lib.agn_oplog_read(self.h, C.byref(rs), C.byref(os_), stream),
+              "agn_oplog_read")
+
     def stats(self):
         e, s, t = C.c_uint64(), C.c_uint64(), C.c_uint64()
         check(self.eng.lib.agn_oplog_stats(self.h, C.byref(e), C.byref(s), C.byref(t)))
         return {"entries": e.value, "slots": s.value, "tokens": t.value}
+
+
+class Batcher:
+    """agn_batcher: per-key materializer_vnode:read/6 calls from many threads
+    coalesced into batched kernels.  `read` blocks the calling thread (ctypes
+    releases the GIL for the duration)."""
+
+    def __init__(self, oplog: OpLog, max_batch: int = 1024, max_wait_us: int = 0):
+        self.oplog, self.lib = oplog, oplog.eng.lib
+        self.h = C.c_void_p()
+        check(self.lib.agn_batcher_create(oplog.h, max_batch, max_wait_us, C.byref(self.h)),
+              "agn_batcher_create")
+
+    def close(self):
+        if self.h:
+            self.lib.agn_batcher_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def read(self, key, R, R_mask=None, sct=None, sct_mask=None, txid=0, base_value=0,
+             base_tag=None, base_tok=None, out_cap=0):
+        """One read/6; returns a dict of the key's result."""
+        D = self.oplog.n_dcs
+        W = n_words(D)
+        arr = lambda a: None if a is None else np.ascontiguousarray(a, np.uint64)  # noqa: E731
+        R, R_mask, sct, sct_mask = arr(R), arr(R_mask), arr(sct), arr(sct_mask)
+        rd = _abi.AgnKeyRead()
+        rd.key, rd.R, rd.R_mask, rd.sct, rd.sct_mask = key, _ptr(R), _ptr(R_mask), _ptr(sct), \
+            _ptr(sct_mask)
+        rd.txid, rd.base_value = txid, base_value
+        if base_tag is not None:
+            base_tag = np.ascontiguousarray(base_tag, np.uint32)
+            base_tok = np.ascontiguousarray(base_tok, np.uint64)
+            rd.n_base, rd.base_tag, rd.base_tok = len(base_tag), _ptr(base_tag), _ptr(base_tok)
+        ct, ctm = np.zeros(D, np.uint64), np.zeros(W, np.uint64)
+        otag, otok = np.zeros(max(out_cap, 1), np.uint32), np.zeros(max(out_cap, 1), np.uint64)
+        o = _abi.AgnKeyResult()
+        o.lastct, o.lastct_mask, o.out_cap = ct.ctypes.data, ctm.ctypes.data, out_cap
+        o.out_tag, o.out_tok = otag.ctypes.data, otok.ctypes.data
+        check(self.lib.agn_batcher_read(self.h, C.byref(rd), C.byref(o)), "agn_batcher_read")
+        return {"value": o.value, "hole": o.hole, "lastct": ct, "lastct_mask": ctm,
+                "count": o.count, "flags": o.flags, "err_pos": o.err_pos, "out_n": o.out_n,
+                "out_tag": otag[:o.out_n], "out_tok": otok[:o.out_n]}
+
+    def stats(self):
+        b, r = C.c_uint64(), C.c_uint64()
+        check(self.lib.agn_batcher_stats(self.h, C.byref(b), C.byref(r)))
+        return {"batches": b.value, "reads": r.value}
 
 
 def gen_host(cfg: _abi.AgnGenCfg):

@@ -184,9 +184,12 @@ int agn_state_capacity(const agn_log *host_log, const agn_read *host_req,
  * counter of ets:update_counter (:630).  update/2 calls are staged on the
  * host and moved to HBM by agn_oplog_flush in one batched transfer + scatter
  * kernel (the micro-batch of a partition's writes); reads then run on the
- * flushed view.  Single writer: append / flush / prune of one oplog must be
- * serialised by the caller (the vnode process); views are invalidated by the
- * next append, flush or prune. */
+ * flushed view.  Thread safety (SURVEY §8(b) Threading): one writer (the
+ * vnode process: append / flush / prune) and any number of concurrent
+ * readers through agn_oplog_read / agn_batcher; the engine holds the device
+ * log shared for the duration of each read kernel and exclusive while a
+ * flush or prune moves segments.  A view returned by agn_oplog_flush is for
+ * single-threaded use and is invalidated by the next flush or prune. */
 #define AGN_OPS_THRESHOLD 50 /* src/materializer_vnode.erl:41 */
 #define AGN_RESIZE_THRESHOLD 5 /* :44 */
 typedef struct agn_oplog agn_oplog;
@@ -227,6 +230,50 @@ int agn_oplog_prune(agn_oplog *log, const uint8_t *prune, const uint64_t *thresh
                     const uint64_t *threshold_mask, uint32_t *out_flags, void *stream);
 /* Host-side accounting: entries in use, allocated slots, removal tokens. */
 int agn_oplog_stats(const agn_oplog *log, uint64_t *entries, uint64_t *slots, uint64_t *tokens);
+/* Batched materialize/4 over the oplog's current contents (req / out as
+ * agn_materialize, device pointers, req->keys indexing the oplog's keys).
+ * Staged appends are flushed first (read-your-writes: update/2 is a
+ * sync_command that precedes the read); blocks until the kernel is done. */
+int agn_oplog_read(agn_oplog *log, const agn_read *req, agn_result *out, void *stream);
+
+/* ---- micro-batching read queue ------------------------------------------
+ * materializer_vnode:read/6 arrives per key from up to 20 read servers per
+ * partition (clocksi_readitem_server:return/6, src/clocksi_readitem_server.erl
+ * :272; READ_CONCURRENCY, include/antidote.hrl:28).  An agn_batcher
+ * coalesces those calls: agn_batcher_read blocks the calling thread until
+ * its request has run in a batch of up to max_batch reads, launched when
+ * max_batch reads wait or the oldest has waited max_wait_us.  One worker
+ * thread and one HIP stream per batcher; any number of calling threads. */
+typedef struct agn_batcher agn_batcher;
+typedef struct agn_key_read { /* one read/6 (host pointers) */
+    uint64_t key;
+    const uint64_t *R;          /* [D] */
+    const uint64_t *R_mask;     /* [W] or NULL (all DCs present) */
+    const uint64_t *sct;        /* [D] base SnapshotCommitTime, NULL = ignore */
+    const uint64_t *sct_mask;   /* [W] or NULL */
+    uint64_t txid;              /* 0 = ignore */
+    int64_t base_value;         /* counter_pn base */
+    uint32_t n_base;            /* set/register base pairs */
+    uint32_t _pad;
+    const uint32_t *base_tag;
+    const uint64_t *base_tok;
+} agn_key_read;
+typedef struct agn_key_result { /* caller-owned host memory */
+    int64_t value, hole;
+    uint64_t *lastct;           /* [D] */
+    uint64_t *lastct_mask;      /* [W] or NULL (then the batch must be dense) */
+    uint32_t count, flags, err_pos;
+    uint32_t out_cap;           /* set/register: room in out_tag / out_tok */
+    uint32_t out_n;             /* live pairs (> out_cap => AGN_ECAPACITY) */
+    uint32_t _pad;
+    uint32_t *out_tag;
+    uint64_t *out_tok;
+} agn_key_result;
+int agn_batcher_create(agn_oplog *log, uint32_t max_batch, uint32_t max_wait_us,
+                       agn_batcher **out);
+int agn_batcher_destroy(agn_batcher *b);
+int agn_batcher_read(agn_batcher *b, const agn_key_read *rd, agn_key_result *out);
+int agn_batcher_stats(agn_batcher *b, uint64_t *batches, uint64_t *reads);
 
 /* ---- base-snapshot selection: vector_orddict:get_smaller/2 --------------
  * (src/vector_orddict.erl:74-87, called from
