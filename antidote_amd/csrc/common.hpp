@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/antidote_gpu.h"
 
@@ -57,6 +58,25 @@ __device__ inline uint64_t uniform_u64(uint64_t v) {
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
+}
+
+// XCD-aware block order.  The dispatcher hands block b to XCD b mod 8, and
+// every XCD has its own L2; with the identity order, the 16-32 consecutive
+// requests that share one 128-byte line of a per-request array (key_off,
+// value, hole, count, flags) are spread over all eight L2s, so each L2 reads
+// the line and writes it back partially.  This bijection gives XCD x the
+// contiguous logical range [x*q + min(x,r), ...) instead (q = nb/8, r = nb%8).
+#define AGN_XCDS 8u
+__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t q = nb / AGN_XCDS, r = nb % AGN_XCDS;
+    const uint32_t x = b % AGN_XCDS, idx = b / AGN_XCDS;
+    return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
+}
+
+// A/B knob AGN_XCD_REMAP=0|1 (default on).
+inline bool xcd_remap() {
+    const char *v = getenv("AGN_XCD_REMAP");
+    return !(v && v[0] == '0');
 }
 
 // Grid sizing for the streaming kernels: enough waves to fill 256 CUs.

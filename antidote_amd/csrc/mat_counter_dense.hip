@@ -5,7 +5,13 @@
 //   * the read clock R and SCT are wave-uniform: explicit noalias kernel
 //     arguments + readfirstlane keep them in SGPRs (s_load, no VGPRs);
 //   * no presence masks (every DC present), so "+1 encoding" and per-DC
-//     branches disappear; each OpSSCommit row is loaded with 16-byte loads;
+//     branches disappear;
+//   * even D: each chunk of 64 entries (OpSSCommit rows, effects, op ids)
+//     streams into LDS by non-temporal LDS-DMA (global_load_lds), the
+//     fastest HBM read idiom measured on the box (7.2 TB/s against 6.0 for
+//     16-byte VGPR loads, profiles/r01/ab_read_probe.log); the op id that
+//     defines NewLastOp is then read from LDS instead of a dependent load
+//     (scan_key_glds; odd D keeps 8-byte VGPR row loads, scan_key);
 //   * cold (SCT = ignore) and warm reads run separate loop bodies, so the
 //     cold body does one D-wide compare per op, exactly the reference's
 //     VC compare count;
@@ -13,10 +19,13 @@
 //   * one wave per request and no loop: the grid is the whole batch, so the
 //     wave dispatcher overlaps the dependent round trips of different keys
 //     (measured against cross-key software pipelines and grouped streams:
-//     profiles/r01/ab_counter_key_per_wave.log, ab_grid_oversubscription.log);
-//   * per-key side values (key_type, sct_ignore, base value, the op_id that
-//     defines NewLastOp) are scalar loads, never vector loads + vmcnt(0).
-// HBM bytes per op: 8*D + 8; per key: 8 + 16*D + 32.
+//     profiles/r01/ab_counter_key_per_wave.log, ab_grid_oversubscription.log),
+//     in XCD-aware block order (xcd_block: consecutive requests share the
+//     lines of the per-request arrays inside one L2);
+//   * per-key side values (key_type, sct_ignore, base value) are scalar
+//     loads, never vector loads + vmcnt(0).
+// HBM bytes per op: 8*D + 8; per key: 8 + 16*D + 32;
+// the LDS-DMA path also reads the chunk's 4-byte op ids (+4 per op).
 #include <cstdlib>
 
 #include "common.hpp"
@@ -104,8 +113,112 @@ struct DenseArgs {
     uint64_t n_req;
     uint64_t n_entries;
     uint32_t req_type;
-    uint32_t _pad;
+    uint32_t xcd;  // 1: XCD-aware block order (xcd_block)
 };
+
+typedef __attribute__((address_space(3))) void *lds_ptr;
+
+// LDS words per wave of the LDS-DMA path: rows (DCP*64 u64, reused as the
+// LastOpCt stage), effects (64 u64), op ids (64 u32).
+template <int D>
+struct GldsLds {
+    static constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;
+    static constexpr int ROWS = DCP * AGN_WAVE, EFF = ROWS, OPID = EFF + AGN_WAVE,
+                         WORDS = OPID + AGN_WAVE / 2;
+};
+
+// scan_key for even D through LDS-DMA: each chunk of 64 log entries is
+// fetched by global_load_lds (non-temporal) into the wave's LDS slice --
+// D/2 x 1 KiB of OpSSCommit rows (image linear: row of lane l at 8*D*l
+// bytes), the effects and the op ids as 4-byte pieces -- then every lane
+// reads its row back with ds_read_b128.  Addresses past the end of the log
+// are clamped (those lanes are idle).  Returns the op id that defines
+// NewLastOp, read from LDS: fetching the chunk's 256 B of op ids with the
+// rows (+5.4 % bytes) removes the dependent round trip a scalar load of the
+// one id costs after the scan (measured 8.09 -> 7.29 ms on cfg2,
+// profiles/r01/ab_counter_glds.log).  Only DMA loads are in flight, so the
+// one vmcnt(0) per chunk drains nothing else.
+template <int D, bool WARM>
+__device__ __forceinline__ int64_t scan_key_glds(
+    const uint64_t *__restrict__ oc, const int64_t *__restrict__ eff,
+    const uint32_t *__restrict__ op_id, const uint64_t *__restrict__ txid, uint64_t txr,
+    uint64_t off, uint64_t n, uint64_t n_entries, const uint64_t (&r)[D],
+    const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum, uint32_t &cnt,
+    int64_t &first_excl, int64_t &first_err, uint64_t *lds) {
+    using L = GldsLds<D>;
+    const int lane = lane_id();
+    const uint64_t lim_oc = n_entries * D - 2u, lim_e = n_entries * 2u - 1u,
+                   lim_id = n_entries - 1u;
+    const uint32_t *ids = reinterpret_cast<const uint32_t *>(lds + L::OPID);
+    int64_t hid = -1;
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        const uint64_t pos = b + (uint64_t)lane;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);
+        const uint64_t cb = (off + b) * D;
+#pragma unroll
+        for (int j = 0; j < D / 2; ++j) {
+            uint64_t q = cb + (uint64_t)(j * AGN_WAVE + lane) * 2u;
+            q = q < lim_oc ? q : lim_oc;
+            __builtin_amdgcn_global_load_lds((const void *)(oc + q), (lds_ptr)(lds + j * 2 * AGN_WAVE),
+                                             16, 0, 2 /* nt */);
+        }
+        const uint32_t *e32 = reinterpret_cast<const uint32_t *>(eff);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {  // i64 effects as 2 x 64 dwords
+            uint64_t q = (off + b) * 2u + (uint64_t)(j * AGN_WAVE + lane);
+            q = q < lim_e ? q : lim_e;
+            __builtin_amdgcn_global_load_lds((const void *)(e32 + q),
+                                             (lds_ptr)(lds + L::EFF + j * AGN_WAVE / 2), 4, 0, 2);
+        }
+        {
+            uint64_t q = off + b + (uint64_t)lane;
+            q = q < lim_id ? q : lim_id;
+            __builtin_amdgcn_global_load_lds((const void *)(op_id + q), (lds_ptr)(lds + L::OPID), 4,
+                                             0, 2);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA has landed
+        __builtin_amdgcn_wave_barrier();
+        uint64_t o[D];
+        const u64x2 *lr = reinterpret_cast<const u64x2 *>(lds + (uint64_t)lane * D);
+#pragma unroll
+        for (int j = 0; j < D / 2; ++j) {
+            const u64x2 x = lr[j];
+            o[2 * j] = x.x;
+            o[2 * j + 1] = x.y;
+        }
+        const int64_t ev = (int64_t)lds[L::EFF + lane];
+        bool okR = true, leS = true;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            okR = okR && (o[j] <= r[j]);
+            if (WARM) leS = leS && (o[j] <= s[j]);
+        }
+        bool nip = WARM ? !leS : true;  // belongs_to_snapshot_op (ignore -> true)
+        if (txid != nullptr) nip = nip || (txid[e] == txr);
+        const bool incl = valid && nip && okR;
+        const bool excl = valid && nip && !okR;
+        if (first_excl < 0) {
+            const uint64_t bx = ballot(excl);
+            if (bx) {
+                first_excl = (int64_t)b + (int64_t)__builtin_ctzll(bx);
+                hid = (int64_t)ids[__builtin_ctzll(bx)];
+            }
+        }
+        if (first_excl < 0 && b + AGN_WAVE >= n) hid = (int64_t)ids[(n - 1) - b];  // get_first_id
+#pragma unroll
+        for (int j = 0; j < D; ++j) ct[j] = (incl && o[j] > ct[j]) ? o[j] : ct[j];
+        const bool bad = incl && ev == AGN_EFFECT_INVALID;
+        cnt += (uint32_t)__builtin_popcountll(ballot(incl));
+        if (first_err < 0) {
+            const uint64_t be = ballot(bad);
+            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+        }
+        sum += (incl && !bad) ? ev : 0;
+        __builtin_amdgcn_wave_barrier();  // LDS reads done before the next chunk's DMA
+    }
+    return hid;
+}
 
 // Process the key's ops in chunks of 64 (lane = op).  `pre` holds the first
 // chunk's row + effect when the caller prefetched them (software pipelining
@@ -165,7 +278,7 @@ __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
 // slots full and the HBM queue deep, while each wave's dependent round trips
 // (metadata -> rows -> NewLastOp id) overlap with other waves' instead of
 // serialising inside one.  Side values are scalar loads (no vmcnt drains).
-template <int D, bool ANY_WARM, int WPB>
+template <int D, bool ANY_WARM, int WPB, bool GLDS>
 __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
     const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
@@ -179,10 +292,13 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     uint32_t *__restrict__ o_err) {
     constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
     constexpr int V = DCP;                                          // op slots per lane
-    __shared__ uint64_t stage[WPB][DCP][AGN_WAVE];
+    constexpr int LW = GLDS ? GldsLds<D>::WORDS : DCP * AGN_WAVE;
+    __shared__ uint64_t lds_all[WPB][LW];  // GLDS: chunk rows/effects/ids; then the ct stage
+
     const int lane = lane_id();
     const int w = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
-    const uint64_t i = uniform_u64((uint64_t)blockIdx.x * WPB + (uint64_t)w);
+    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t i = uniform_u64((uint64_t)blk * WPB + (uint64_t)w);
     if (i >= a.n_req) return;
     const uint64_t key = keys ? uniform_u64(keys[i]) : i;
     const uint64_t off = uniform_u64(key_off[key]);
@@ -206,29 +322,42 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     const uint64_t *tx = (txr != 0ull) ? log_txid : nullptr;
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
-    if (!ANY_WARM || sct_ign)
-        scan_key<D, false, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                                  first_err, nullptr, 0);
-    else
-        scan_key<D, ANY_WARM, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                                     first_err, nullptr, 0);
+    int64_t hid = -1;
+    if constexpr (GLDS && D % 2 == 0) {
+        if (!ANY_WARM || sct_ign)
+            hid = scan_key_glds<D, false>(oc, eff, op_id, tx, txr, off, n, a.n_entries, r, s, ct,
+                                          sum, cnt, first_excl, first_err, lds_all[w]);
+        else
+            hid = scan_key_glds<D, ANY_WARM>(oc, eff, op_id, tx, txr, off, n, a.n_entries, r, s,
+                                             ct, sum, cnt, first_excl, first_err, lds_all[w]);
+    } else {
+        if (!ANY_WARM || sct_ign)
+            scan_key<D, false, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                      first_err, nullptr, 0);
+        else
+            scan_key<D, ANY_WARM, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt,
+                                         first_excl, first_err, nullptr, 0);
+    }
     // NewLastOp id and base value: scalar loads, issued before the reductions
-    const uint64_t hole_e = first_excl >= 0 ? off + (uint64_t)first_excl : off + n - 1;
-    const int64_t hid = n ? (int64_t)op_id[uniform_u64(hole_e)] : 0;
+    if (hid < 0) {
+        const uint64_t hole_e = first_excl >= 0 ? off + (uint64_t)first_excl : off + n - 1;
+        hid = n ? (int64_t)op_id[uniform_u64(hole_e)] : 0;
+    }
     const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)base_value[i]) : 0;
 
     const int64_t total = wave_sum_dpp(sum);
     // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots of
     // one DC -> xor-shuffle across the 64/DCP lanes that share it
+    uint64_t(*stage)[AGN_WAVE] = reinterpret_cast<uint64_t(*)[AGN_WAVE]>(lds_all[w]);
 #pragma unroll
-    for (int j = 0; j < D; ++j) stage[w][j][lane] = ct[j];
+    for (int j = 0; j < D; ++j) stage[j][lane] = ct[j];
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const int c = lane % DCP, g = lane / DCP;
     uint64_t m = 0;
     if (c < D) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) m = umax64(m, stage[w][c][g * V + v]);
+        for (int v = 0; v < V; ++v) m = umax64(m, stage[c][g * V + v]);
     }
 #pragma unroll
     for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
@@ -249,26 +378,41 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     }
 }
 
-template <int D, int WPB>
-int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, 0};
+// LDS-DMA row path (even D: 16-byte aligned chunks); AGN_COUNTER_GLDS=0 selects
+// the VGPR-load path for A/B.
+inline bool counter_glds() {
+    const char *v = getenv("AGN_COUNTER_GLDS");
+    return !(v && v[0] == '0');
+}
+
+template <int D, int WPB, bool GLDS>
+int launch_key_g(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u};
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);
     if (req.sct)
-        hipLaunchKernelGGL((k_counter_key<D, true, WPB>), dim3((unsigned)nb), dim3(64 * WPB), 0,
-                           st, a, req.keys, log.key_off, log.key_len, log.key_type, log.oc, log.op_id,
-                           log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
+        hipLaunchKernelGGL((k_counter_key<D, true, WPB, GLDS>), dim3((unsigned)nb), dim3(64 * WPB),
+                           0, st, a, req.keys, log.key_off, log.key_len, log.key_type, log.oc,
+                           log.op_id, log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
                            req.base_value, out.value, out.hole, out.lastct, out.count,
                            out.flags, out.err_pos);
     else
-        hipLaunchKernelGGL((k_counter_key<D, false, WPB>), dim3((unsigned)nb), dim3(64 * WPB), 0,
-                           st, a, req.keys, log.key_off, log.key_len, log.key_type, log.oc, log.op_id,
-                           log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
-                           req.base_value, out.value, out.hole, out.lastct, out.count,
-                           out.flags, out.err_pos);
+        hipLaunchKernelGGL((k_counter_key<D, false, WPB, GLDS>), dim3((unsigned)nb),
+                           dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
+                           log.key_type, log.oc, log.op_id, log.eff, log.txid, req.R, req.sct,
+                           req.sct_ignore, req.txid, req.base_value, out.value, out.hole,
+                           out.lastct, out.count, out.flags, out.err_pos);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
+}
+
+template <int D, int WPB>
+int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    if constexpr (D % 2 == 0) {
+        if (counter_glds()) return launch_key_g<D, WPB, true>(log, req, out, st);
+    }
+    return launch_key_g<D, WPB, false>(log, req, out, st);
 }
 
 int dense_wpb() {

@@ -184,7 +184,7 @@ __device__ __forceinline__ Side load_side(const agn_log &log, uint64_t off, uint
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, int CAP, int WPB, int RB,
           bool WARM, bool SLOW>
 __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, agn_result out,
-                                                   uint32_t *wl, uint32_t *wl_n) {
+                                                   uint32_t *wl, uint32_t *wl_n, uint32_t xcd) {
     using S = Shape<DPL, LPO>;
     constexpr int OPI = S::OPI;
     __shared__ CandLds<CAP> Lall[WPB];
@@ -197,7 +197,8 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     const uint64_t n_items = SLOW ? (uint64_t)uniform_u64(*wl_n) : req.n_req;
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
 
-    for (uint64_t it = (uint64_t)blockIdx.x * WPB + (uint64_t)w; it < n_items; it += nw) {
+    const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    for (uint64_t it = (uint64_t)blk * WPB + (uint64_t)w; it < n_items; it += nw) {
         const uint64_t i = SLOW ? (uint64_t)__builtin_amdgcn_readfirstlane(wl[it]) : it;
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
         const uint64_t off = uniform_u64(log.key_off[key]);
@@ -503,13 +504,13 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
             hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH,
                                        WARM, false>),
                                dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, wl + 1,
-                               wl);
+                               wl, xcd_remap() ? 1u : 0u);
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
             hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM,
                                        true>),
-                               dim3(256), dim3(64), 0, st, log, req, out, wl + 1, wl);
+                               dim3(256), dim3(64), 0, st, log, req, out, wl + 1, wl, 0u);
             e = hipGetLastError();
         }
         if (e != hipSuccess) rc = fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));

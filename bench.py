@@ -447,8 +447,9 @@ def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
 
 def probe_read_gbs(eng, dl, nbytes, sp, torch):
     """The box's practical HBM read ceiling: tools/libagn_probe.so streams the
-    OpSSCommit array (16-byte coalesced loads, every byte once) on the same
-    stream; reported beside the spec peak so box-to-box HBM variance can be
+    OpSSCommit array (non-temporal LDS-DMA loads, 4 KiB per wave, every byte
+    once: the fastest read idiom measured, profiles/r01/ab_read_probe.log) on
+    the same stream; reported beside the spec peak so box-to-box HBM variance can be
     told apart from kernel changes."""
     path = os.path.join(ROOT, "tools", "libagn_probe.so")
     if not os.path.exists(path):
@@ -465,7 +466,7 @@ def probe_read_gbs(eng, dl, nbytes, sp, torch):
     e.record()
     torch.cuda.synchronize()
     scratch.free()
-    return nbytes / (b.elapsed_time(e) / 5 * 1e-3) / 1e9
+    return (nbytes // 8192 * 8192) / (b.elapsed_time(e) / 5 * 1e-3) / 1e9  # whole 8 KiB blocks
 
 
 def gst_bench(eng, torch, dist, world, rank, sp):

@@ -1,29 +1,42 @@
 // bwprobe.hip — measurement infrastructure (not the product): the practical
-// HBM read ceiling of the box the bench runs on.  One streaming pass of
-// 16-byte coalesced loads over a buffer (each byte read once), XOR-folded so
-// the loads cannot be elided.  bench.py reports the materialize kernel's
-// bytes/s both against the 8 TB/s spec peak and against this probe.
+// HBM read ceiling of the box the bench runs on.  The fastest read idiom
+// measured here (scripts/ab_probe.py over tools/bwprobe_ab.hip,
+// profiles/r01/ab_read_probe.log): one-shot waves, each streaming 4 KiB with
+// four non-temporal LDS-DMA loads (global_load_lds_dwordx4 nt); every byte is
+// read once.  bench.py reports the materialize kernel's bytes/s both against
+// the 8 TB/s spec peak and against this probe.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 
-__global__ __launch_bounds__(256) void k_read(const u64x2 *__restrict__ p, uint64_t n,
+__global__ __launch_bounds__(128) void k_read(const u64x2 *__restrict__ p, uint64_t n,
                                              uint64_t *__restrict__ out) {
+    __shared__ u64x2 st[2][256];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * 2 + wv;
+    if (w * 256 + 255 >= n) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_global_load_lds((const void *)(p + w * 256 + j * 64 + lane),
+                                         (__attribute__((address_space(3))) void *)&st[wv][j * 64],
+                                         16, 0, 2 /* nt */);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
     uint64_t acc = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const u64x2 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-        acc ^= a.x ^ a.y ^ b.x ^ b.y ^ c.x ^ c.y ^ d.x ^ d.y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u64x2 x = st[wv][lane * 4 + j];
+        acc ^= x.x ^ x.y;
     }
-    for (; i < n; i += stride) acc ^= p[i].x ^ p[i].y;
     if (acc == 0x9E3779B97F4A7C15ull) out[0] = acc;  // practically never taken
 }
 
 extern "C" int agn_probe_read(const void *buf, uint64_t bytes, void *scratch, void *stream) {
-    const uint64_t n = bytes / 16;
-    hipLaunchKernelGGL(k_read, dim3(256 * 16), dim3(256), 0, (hipStream_t)stream,
+    const uint64_t n = bytes / 16;  // whole 8 KiB blocks; the tail (< 8 KiB) is not read
+    const uint64_t nb = n / 512;
+    if (nb == 0 || nb > 0x7fffffffull) return -1;
+    hipLaunchKernelGGL(k_read, dim3((unsigned)nb), dim3(128), 0, (hipStream_t)stream,
                        (const u64x2 *)buf, n, (uint64_t *)scratch);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
