@@ -659,9 +659,13 @@ int agn_gen_dev(agn_ctx *ctx, const agn_gen_cfg *cfg, agn_log *log, agn_read *re
         uint32_t *ro = (uint32_t *)log->rem_off;
         hipLaunchKernelGGL(k_gen, dim3(blocks), dim3(256), 0, s, c, *log, *req, 0, scratch, ro + 1);
         size_t tmp_bytes = 0;
-        hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, ro + 1, ro + 1, (int)E, s);
-        void *tmp = dmalloc<uint8_t>(tmp_bytes ? tmp_bytes : 1, err);
-        if (!err) hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, ro + 1, ro + 1, (int)E, s);
+        if (hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, ro + 1, ro + 1, (int)E, s) !=
+            hipSuccess)
+            err = fail(AGN_EHIP, "gen: removal-offset scan sizing failed");
+        void *tmp = err ? nullptr : dmalloc<uint8_t>(tmp_bytes ? tmp_bytes : 1, err);
+        if (!err && hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, ro + 1, ro + 1, (int)E, s) !=
+                        hipSuccess)
+            err = fail(AGN_EHIP, "gen: removal-offset scan failed");
         if (!err) (void)hipMemsetAsync(ro, 0, sizeof(uint32_t), s);
         uint32_t total = 0;
         if (!err) (void)hipMemcpyAsync(&total, ro + E, sizeof total, hipMemcpyDeviceToHost, s);

@@ -6,12 +6,13 @@
 //     arguments + readfirstlane keep them in SGPRs (s_load, no VGPRs);
 //   * no presence masks (every DC present), so "+1 encoding" and per-DC
 //     branches disappear;
-//   * even D: each chunk of 64 entries (OpSSCommit rows, effects, op ids)
-//     streams into LDS by non-temporal LDS-DMA (global_load_lds), the
-//     fastest HBM read idiom measured on the box (7.2 TB/s against 6.0 for
-//     16-byte VGPR loads, profiles/r01/ab_read_probe.log); the op id that
-//     defines NewLastOp is then read from LDS instead of a dependent load
-//     (scan_key_glds; odd D keeps 8-byte VGPR row loads, scan_key);
+//   * rows are 16-byte VGPR loads (scan_key); an opt-in variant for even D
+//     (AGN_COUNTER_GLDS=1, scan_key_glds) streams each chunk of 64 entries
+//     (OpSSCommit rows, effects, op ids) into LDS by non-temporal LDS-DMA
+//     (global_load_lds), the fastest pure-read idiom measured (7.1-7.2 TB/s
+//     against 6.0 for 16-byte VGPR loads, profiles/r01/ab_read_probe.log),
+//     and reads the NewLastOp op id from LDS instead of a dependent load --
+//     faster on some boxes, slower on others (counter_glds below);
 //   * cold (SCT = ignore) and warm reads run separate loop bodies, so the
 //     cold body does one D-wide compare per op, exactly the reference's
 //     VC compare count;
@@ -378,11 +379,14 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     }
 }
 
-// LDS-DMA row path (even D: 16-byte aligned chunks); AGN_COUNTER_GLDS=0 selects
-// the VGPR-load path for A/B.
+// LDS-DMA row path (even D: 16-byte aligned chunks): opt-in, AGN_COUNTER_GLDS=1.
+// Its speed is box-dependent: on two MI355X boxes it beat the VGPR-load path
+// by 7-10 % (cfg2 7.29-7.55 vs 8.16-8.44 ms), on three others it lost by
+// 6-14 % (8.86-9.28 vs 7.95-8.39 ms), consistently across processes on one
+// box (profiles/r01/ab_counter_glds*.log); the VGPR path is the robust default.
 inline bool counter_glds() {
     const char *v = getenv("AGN_COUNTER_GLDS");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
 }
 
 template <int D, int WPB, bool GLDS>

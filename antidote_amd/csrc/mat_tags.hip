@@ -248,7 +248,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         }
         wave_sync();
 
-        int64_t first_excl = -1, first_err = -1;
+        int64_t first_excl = -1, first_err = -1, hid = 0;
         uint32_t cnt = 0;
 
         if (n != 0) {
@@ -321,7 +321,12 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                     const bool excl = valid && nip && !okR;
                     if (first_excl < 0) {
                         const uint64_t bx = ballot(excl && sub == 0);
-                        if (bx) first_excl = (int64_t)b + (int64_t)(__builtin_ctzll(bx) / LPO);
+                        if (bx) {
+                            first_excl = (int64_t)b + (int64_t)(__builtin_ctzll(bx) / LPO);
+                            // its op id is in the chunk's side fields: no dependent load
+                            hid = (int64_t)(uint32_t)__shfl((int)cs.id,
+                                                            (int)(first_excl - (int64_t)c0));
+                        }
                     }
                     if (incl) {
 #pragma unroll
@@ -335,6 +340,8 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                         incl_e = (bi >> (((uint32_t)lane % (uint32_t)OPI) * LPO)) & 1ull;
                 }
 
+                if (first_excl < 0 && c0 + AGN_WAVE >= n)  // get_first_id (:49-63)
+                    hid = (int64_t)(uint32_t)__shfl((int)cs.id, (int)(nvalid - 1u));
                 // ---- chunk resolution (lane = entry c0 + lane)
                 const uint64_t pos = c0 + (uint64_t)lane;
                 const bool opstart = pos == 0 || cs.id_prev != cs.id;
@@ -467,9 +474,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         }
 
         if (lane == 0) {
-            int64_t hole;
-            if (first_excl >= 0) hole = (int64_t)log.op_id[off + (uint64_t)first_excl] - 1;
-            else hole = n ? (int64_t)log.op_id[off + n - 1] : 0;  // get_first_id (:49-63)
+            const int64_t hole = first_excl >= 0 ? hid - 1 : hid;  // hid = 0 for n = 0
             uint32_t fl = 0;
             if (cnt) fl |= AGN_F_NEWSS;
             if (ct_ign) fl |= AGN_F_CT_IGNORE;

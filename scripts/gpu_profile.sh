@@ -1,5 +1,6 @@
 # Round profile: bench lines for cfg2/3/4 (+GST), rocprofv3 kernel-trace stats
-# and FETCH_SIZE / WRITE_SIZE passes (one counter per run) for each config.
+# and FETCH_SIZE / WRITE_SIZE passes (one counter per run) for each config,
+# plus a FETCH_SIZE calibration of the 16-byte and 4-byte LDS-DMA widths.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -12,6 +13,9 @@ step() {
   return 0
 }
 : > gpurun_out/steps.txt
+export AGN_PROBE_GIB=4 AGN_PROBE_ROUNDS=3
+step calib 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_calib -o run -- python3 scripts/ab_probe.py 4 10
+unset AGN_PROBE_GIB AGN_PROBE_ROUNDS
 step bench2 400 python -u bench.py --config 2 --gst
 step bench3 400 python -u bench.py --config 3
 step bench4 400 python -u bench.py --config 4

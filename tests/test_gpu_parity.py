@@ -53,27 +53,37 @@ def test_kat_system_seq_gpu(eng, c):
 
 
 # ------------------------------------------------------------------ randomised differential
+# counter_pn runs through every counter kernel: the dense fast path (auto),
+# its opt-in LDS-DMA row path (glds, even D only) and the general kernel
+COUNTER_IMPLS = ("auto", "glds", "general")
 DIFF = []
 for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
     for D in (1, 2, 3, 5, 8, 12, 16, 17, 33, 64, 100, 256):
         for sparse in (False, True):
-            DIFF.append((crdt, D, sparse))
+            impls = COUNTER_IMPLS if crdt == _abi.COUNTER_PN else ("auto",)
+            for impl in impls:
+                DIFF.append((crdt, D, sparse, impl))
 
 
-@pytest.fixture(params=["auto", "general"])
-def counter_impl(request, monkeypatch):
-    """Run counter cases through the dense fast path (auto) and the general kernel."""
-    if request.param == "general":
+def _set_impl(monkeypatch, impl):
+    monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
-    else:
-        monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    elif impl == "glds":
+        monkeypatch.setenv("AGN_COUNTER_GLDS", "1")
+
+
+@pytest.fixture(params=COUNTER_IMPLS)
+def counter_impl(request, monkeypatch):
+    """Run counter cases through each counter kernel (see COUNTER_IMPLS)."""
+    _set_impl(monkeypatch, request.param)
     return request.param
 
 
-@pytest.mark.parametrize("crdt,D,sparse", DIFF)
-def test_random_vs_oracle(eng, oracle_lib, crdt, D, sparse, counter_impl):
-    if crdt != _abi.COUNTER_PN and counter_impl == "general":
-        pytest.skip("impl switch only applies to counter_pn")
+@pytest.mark.parametrize("crdt,D,sparse,impl", DIFF)
+def test_random_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sparse, impl):
+    _set_impl(monkeypatch, impl)
     K = 300 if D <= 64 else 120
     nmax = 150 if D <= 16 else 70
     log, req, cap = random_case(7919 * crdt + 31 * D + sparse, crdt, K, D, nmax, sparse=sparse,
