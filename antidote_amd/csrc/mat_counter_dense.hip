@@ -221,32 +221,25 @@ __device__ __forceinline__ int64_t scan_key_glds(
     return hid;
 }
 
-// Process the key's ops in chunks of 64 (lane = op).  `pre` holds the first
-// chunk's row + effect when the caller prefetched them (software pipelining
-// across keys); later chunks are loaded here.
-template <int D, bool WARM, bool NT>
+// Process the key's ops in chunks of 64 (lane = op), rows by 16-byte VGPR
+// loads.  The op id that defines NewLastOp is one scalar load after the scan:
+// loading every lane's op id with its row instead (+4 B per op, no dependent
+// load) measured 2.7 % slower (profiles/r01/ab_counter_ids_wpb.log).
+template <int D, bool WARM>
 __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
                                          const int64_t *__restrict__ eff,
                                          const uint64_t *__restrict__ txid, uint64_t txr,
                                          uint64_t off, uint64_t n, const uint64_t (&r)[D],
                                          const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum,
-                                         uint32_t &cnt, int64_t &first_excl, int64_t &first_err,
-                                         const uint64_t (*pre_o)[D], int64_t pre_ev) {
+                                         uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
     const int lane = lane_id();
     for (uint64_t b = 0; b < n; b += AGN_WAVE) {
         const uint64_t pos = b + (uint64_t)lane;
         const bool valid = pos < n;
         const uint64_t e = off + (valid ? pos : 0ull);  // in-bounds for idle lanes
         uint64_t o[D];
-        int64_t ev;
-        if (b == 0 && pre_o != nullptr) {
-#pragma unroll
-            for (int j = 0; j < D; ++j) o[j] = (*pre_o)[j];
-            ev = pre_ev;
-        } else {
-            load_row<D, NT>(oc + e * D, o);
-            ev = ld<NT>(eff + e);
-        }
+        load_row<D, false>(oc + e * D, o);
+        const int64_t ev = eff[e];
         bool okR = true, leS = true;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
@@ -333,11 +326,11 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
                                              ct, sum, cnt, first_excl, first_err, lds_all[w]);
     } else {
         if (!ANY_WARM || sct_ign)
-            scan_key<D, false, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                                      first_err, nullptr, 0);
+            scan_key<D, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                               first_err);
         else
-            scan_key<D, ANY_WARM, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt,
-                                         first_excl, first_err, nullptr, 0);
+            scan_key<D, ANY_WARM>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                  first_err);
     }
     // NewLastOp id and base value: scalar loads, issued before the reductions
     if (hid < 0) {
@@ -419,20 +412,22 @@ int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, h
     return launch_key_g<D, WPB, false>(log, req, out, st);
 }
 
+// Waves (= requests) per block: 1 measured 1.4-3.4 % faster than 2 and
+// 0-1.6 % faster than 4 on cfg2 (profiles/r01/ab_counter_wpb.log).
 int dense_wpb() {
-    const char *v = getenv("AGN_COUNTER_WPB");  // A/B knob: waves per block
-    const int w = v ? atoi(v) : 2;
-    return (w == 1 || w == 2 || w == 4 || w == 8) ? w : 2;
+    const char *v = getenv("AGN_COUNTER_WPB");  // A/B knob
+    const int w = v ? atoi(v) : 1;
+    return (w == 1 || w == 2 || w == 4 || w == 8) ? w : 1;
 }
 
 template <int D>
 int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
     switch (dense_wpb()) {
-        case 1: return launch_key<D, 1>(log, req, out, st);
         case 4: return launch_key<D, 4>(log, req, out, st);
         case 8: return launch_key<D, 8>(log, req, out, st);
-        default: return launch_key<D, 2>(log, req, out, st);
+        case 2: return launch_key<D, 2>(log, req, out, st);
+        default: return launch_key<D, 1>(log, req, out, st);
     }
 }
 

@@ -12,7 +12,7 @@
 // before the add.  Every pair is judged on its own, so repeated tokens keep
 // the fold's multiset semantics.
 //
-// Kernel structure (one wave per key, 4 independent waves per block):
+// Kernel structure (one wave per key, one wave per block, grid = batch):
 //   * the key is processed in chunks of 64 log entries (lane = entry for the
 //     per-entry fields, LPO lanes x DPL DCs per op for the clock rows);
 //   * the snapshot filter streams the OpSSCommit rows through a two-deep
@@ -490,7 +490,9 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     }
 }
 
-constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 4, RBATCH = 2;
+// FAST_WPB: one wave per block measured 0.7-1.4 % faster than 4 (cfg3/cfg4,
+// profiles/r01/ab_tags_wpb_unbiased.log)
+constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 1, RBATCH = 2;
 
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM>
 int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
@@ -504,7 +506,8 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
         // one wave per key: the grid is the batch (the wave dispatcher then
         // overlaps keys; AGN_TAGS_GRID=<blocks> caps it for A/B)
         const char *ge = getenv("AGN_TAGS_GRID");
-        const unsigned blocks = grid_for(req.n_req, FAST_WPB, ge ? (unsigned)atoi(ge) : 0x7fffffffu);
+        const unsigned blocks =
+            grid_for(req.n_req, FAST_WPB, ge ? (unsigned)atoi(ge) : 0x7fffffffu);
         if (e == hipSuccess) {
             hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH,
                                        WARM, false>),

@@ -135,9 +135,17 @@ def main():
         world = int(os.environ["WORLD_SIZE"])
     import torch
     import torch.distributed as dist
+    # AGN_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with several ranks on
+    # one GPU (RCCL refuses two ranks on one device); the driver's runs use RCCL
+    backend = os.environ.get("AGN_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from antidote_amd import _abi
     from antidote_amd.engine import Engine

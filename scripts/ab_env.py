@@ -41,29 +41,42 @@ for c in a.cfg or [2]:
     cap = None
     if cfg["crdt_type"] != 1:
         cap = np.arange(K + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
-    res = {x: eng.alloc_result(K, cfg["n_dcs"], sparse=False, cap_off=cap) for x in VARS}
+    # one shared result buffer (per-variant buffers biased the first variant's
+    # timing by 1-3 %), variant order rotated every round
+    res = eng.alloc_result(K, cfg["n_dcs"], sparse=False, cap_off=cap)
     n_rem = 0
     if cfg["crdt_type"] != 1:
         E = K * cfg["ops_per_key"]
         n_rem = int(eng.download(type("B", (), {"ptr": dl.rem_off})(), np.uint32, (E + 1,))[-1])
+    names = list(VARS)
     times = {x: [] for x in VARS}
+
+    def setenv(env):
+        for k in KNOBS:
+            if k in env:
+                os.environ[k] = env[k]
+            else:
+                os.environ.pop(k, None)
+
     for rnd in range(a.rounds):
-        for x, env in VARS.items():
-            for k in KNOBS:
-                if k in env:
-                    os.environ[k] = env[k]
-                else:
-                    os.environ.pop(k, None)
+        order = names[rnd % len(names):] + names[:rnd % len(names)]
+        for x in order:
+            setenv(VARS[x])
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             b.record()
-            eng.materialize(dl, dr, res[x], stream=sp)
+            eng.materialize(dl, dr, res, stream=sp)
             e.record()
             torch.cuda.synchronize()
             if rnd >= 2:
                 times[x].append(b.elapsed_time(e))
+    outs = {}
+    for x in names:
+        setenv(VARS[x])
+        eng.materialize(dl, dr, res, stream=sp)
+        torch.cuda.synchronize()
+        outs[x] = eng.fetch_result(res)
     for k in KNOBS:
         os.environ.pop(k, None)
-    outs = {x: eng.fetch_result(res[x]) for x in VARS}
     first = next(iter(VARS))
     fields = FIELDS if cfg["crdt_type"] == 1 else FIELDS[1:] + ("out_n", "out_tag", "out_tok")
     n_live = 0 if cfg["crdt_type"] == 1 else int(outs[first].out_n.astype(np.int64).sum())
@@ -76,6 +89,5 @@ for c in a.cfg or [2]:
               f"{byts / ms / 1e6 / 8000:.3f} of 8 TB/s  {byts / ms / 1e6 / pr:.3f} of probe "
               f"({pr:.0f})  same={same}", flush=True)
     eng.free_gen(dl, dr)
-    for r in res.values():
-        for bb in r.bufs.values():
-            bb.free()
+    for bb in res.bufs.values():
+        bb.free()
