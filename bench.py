@@ -66,6 +66,9 @@ def parse():
                          "synthetic partition log")
     ap.add_argument("--gc", action="store_true",
                     help="also time the op-log GC (agn_prune_ops) over the whole log")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the host-staged read path (keys + R from pinned host "
+                         "memory, results back to pinned host memory; PCIe-inclusive)")
     return ap.parse_args()
 
 
@@ -216,6 +219,7 @@ def main():
     gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch) if a.gc else None
     warm = warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.steps) if a.warm else None
     ingest = ingest_bench(eng, cfg, sp, torch) if a.ingest else None
+    e2e = e2e_bench(eng, dl, dr, res, cfg, n_keys, torch) if a.e2e else None
 
     gst = None
     if a.gst:
@@ -271,6 +275,8 @@ def main():
             line["warm"] = warm
         if ingest:
             line["ingest"] = ingest
+        if e2e:
+            line["e2e"] = e2e
         print(json.dumps(line), flush=True)
 
     eng.free_gen(dl, dr)
@@ -341,6 +347,98 @@ def ingest_bench(eng, cfg, sp, torch, n_txn=10_000_000, n_keys=1_000_000):
         bb.free()
     return {"records": n, "ops_out": emitted, "ms": ms, "records_per_s": n / (ms * 1e-3),
             "ops_per_s": emitted / (ms * 1e-3), "n_keys": n_keys, "n_dcs": D}
+
+
+def e2e_bench(eng, dl, dr, res, cfg, n_keys, torch, chunk=1 << 20, reps=3):
+    """Host-staged read path (what the NIF boundary hands over, SURVEY.md
+    §8(b)): the request keys and read clocks R start in pinned host memory,
+    the results (value, NewLastOp, LastOpCt, Count, flags, error position) end
+    in pinned host memory.  Chunks of `chunk` requests flow through a
+    two-slot ring on three streams (H2D copy -> agn_materialize -> D2H copy),
+    so PCIe transfers in both directions overlap the kernel.  The op log stays
+    resident in HBM (engine-owned, as at update/2 time).  Counter only."""
+    from antidote_amd import _abi
+    if cfg["crdt_type"] != 1:
+        return None
+    D = cfg["n_dcs"]
+    pin = dict(pin_memory=True)
+    # host inputs: request i reads key i with the generator's R row
+    keys_h = torch.arange(n_keys, dtype=torch.int64).pin_memory()
+    R_h = torch.from_numpy(eng.download(type("B", (), {"ptr": dr.R})(), np.uint64,
+                                        (n_keys, D)).view(np.int64)).pin_memory()
+    out_spec = {"value": 1, "hole": 1, "lastct": D, "count32": 1, "flags32": 1, "err32": 1}
+    host = {"value": torch.empty(n_keys, dtype=torch.int64, **pin),
+            "hole": torch.empty(n_keys, dtype=torch.int64, **pin),
+            "lastct": torch.empty((n_keys, D), dtype=torch.int64, **pin),
+            "count32": torch.empty(n_keys, dtype=torch.int32, **pin),
+            "flags32": torch.empty(n_keys, dtype=torch.int32, **pin),
+            "err32": torch.empty(n_keys, dtype=torch.int32, **pin)}
+    dev = torch.device("cuda", torch.cuda.current_device())
+    slots = []
+    for _ in range(2):
+        s = {"keys": torch.empty(chunk, dtype=torch.int64, device=dev),
+             "R": torch.empty((chunk, D), dtype=torch.int64, device=dev)}
+        for k, w in out_spec.items():
+            s[k] = torch.empty((chunk, w) if w > 1 else chunk, dtype=host[k].dtype, device=dev)
+        slots.append(s)
+    s_in, s_k, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    n_chunks = (n_keys + chunk - 1) // chunk
+
+    def run():
+        ev_comp = [None, None]   # slot's kernel done (input slot reusable)
+        ev_out = [None, None]    # slot's results copied out (result slot reusable)
+        for c in range(n_chunks):
+            sl, s = c % 2, slots[c % 2]
+            a, b = c * chunk, min(n_keys, (c + 1) * chunk)
+            m = b - a
+            with torch.cuda.stream(s_in):
+                if ev_comp[sl] is not None:
+                    s_in.wait_event(ev_comp[sl])
+                s["keys"][:m].copy_(keys_h[a:b], non_blocking=True)
+                s["R"][:m].copy_(R_h[a:b], non_blocking=True)
+                ev_in = torch.cuda.Event()
+                ev_in.record(s_in)
+            s_k.wait_event(ev_in)
+            if ev_out[sl] is not None:
+                s_k.wait_event(ev_out[sl])
+            rq = _abi.AgnRead()
+            C.memmove(C.addressof(rq), C.addressof(dr), C.sizeof(_abi.AgnRead))
+            rq.n_req, rq.keys, rq.R = m, s["keys"].data_ptr(), s["R"].data_ptr()
+            rs = _abi.AgnResult()
+            rs.value, rs.hole, rs.lastct = (s[k].data_ptr() for k in ("value", "hole", "lastct"))
+            rs.count, rs.flags, rs.err_pos = (s[k].data_ptr() for k in ("count32", "flags32",
+                                                                         "err32"))
+            eng.materialize(dl, rq, rs, stream=s_k.cuda_stream)
+            ev_comp[sl] = torch.cuda.Event()
+            ev_comp[sl].record(s_k)
+            with torch.cuda.stream(s_out):
+                s_out.wait_event(ev_comp[sl])
+                for k in out_spec:
+                    host[k][a:b].copy_(s[k][:m], non_blocking=True)
+                ev_out[sl] = torch.cuda.Event()
+                ev_out[sl].record(s_out)
+        torch.cuda.synchronize()
+
+    run()
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run()
+        times.append(time.perf_counter() - t0)
+    ms = float(np.median(times)) * 1e3
+    ref = eng.fetch_result(res)
+    same = bool(np.array_equal(ref.value, host["value"].numpy()) and
+                np.array_equal(ref.hole, host["hole"].numpy()) and
+                np.array_equal(ref.lastct.view(np.int64), host["lastct"].numpy()) and
+                np.array_equal(ref.count.view(np.int32), host["count32"].numpy()) and
+                np.array_equal(ref.flags.view(np.int32), host["flags32"].numpy()))
+    up = n_keys * (8 + 8 * D)
+    down = n_keys * (8 + 8 + 8 * D + 4 + 4 + 4)
+    ops = n_keys * cfg["ops_per_key"]
+    return {"ms": ms, "ops_per_s": ops / (ms * 1e-3), "h2d_bytes": up, "d2h_bytes": down,
+            "pcie_GBps": (up + down) / (ms * 1e-3) / 1e9, "chunk_keys": chunk,
+            "n_chunks": n_chunks, "same_as_device_resident": same,
+            "note": "keys + R from pinned host, results to pinned host; 3 streams, 2-slot ring"}
 
 
 def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
