@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK = 0
 EINVAL, EHIP, ENOMEM, ECAPACITY, ENOTSUP, ERCCL, ENODEV = -1, -2, -3, -4, -5, -6, -7
@@ -41,7 +41,11 @@ class AgnLog(C.Structure):
         ("key_off", P), ("key_len", P), ("key_type", P), ("oc", P), ("oc_mask", P),
         ("op_id", P), ("txid", P), ("eff", P),
         ("tag", P), ("add_tok", P), ("rem_off", P), ("rem_tok", P),
+        ("key_id0", P),
     ]
+
+
+ID0_NONE = 0xFFFFFFFF
 
 
 class AgnRead(C.Structure):
@@ -126,6 +130,7 @@ PROTOTYPES = {
     "agn_materialize_host": (C.c_int, [P, C.POINTER(AgnLog), C.POINTER(AgnRead),
                                        C.POINTER(AgnResult)]),
     "agn_state_capacity": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead), P]),
+    "agn_log_index_ids": (C.c_int, [P, C.POINTER(AgnLog), P, P]),
     "agn_select_base": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, P, P, P, P]),
     "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
     "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),

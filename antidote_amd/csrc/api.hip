@@ -190,6 +190,15 @@ int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_r
     return launch_tags(*log, *req, *out, s);
 }
 
+int agn_log_index_ids(agn_ctx *ctx, const agn_log *log, uint32_t *out, void *stream) {
+    if (!log || !out) return fail(AGN_EINVAL, "index_ids: null argument");
+    if (log->n_keys && !log->key_off) return fail(AGN_EINVAL, "index_ids: key_off required");
+    if (log->n_entries && !log->op_id) return fail(AGN_EINVAL, "index_ids: op_id required");
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    return launch_index_ids(*log, out, (hipStream_t)stream);
+}
+
 int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_off) {
     if (!log || !req || !cap_off) return fail(AGN_EINVAL, "null argument");
     cap_off[0] = 0;
@@ -271,6 +280,7 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     if (log->rem_off && log->key_len)  // segmented log: the token arena's high-water mark
         for (uint64_t e = 0; e <= E; ++e) n_rem = std::max<uint64_t>(n_rem, log->rem_off[e]);
     dl.rem_tok = st.up(log->rem_tok, n_rem);
+    dl.key_id0 = st.up(log->key_id0, K);
     agn_read dr = *req;
     dr.keys = st.up(req->keys, Q);
     dr.R = st.up(req->R, Q * D);
@@ -376,6 +386,7 @@ int agn_log_ingest(agn_ctx *ctx, const agn_log_records *recs, uint32_t crdt_type
     out->crdt_type = crdt_type;
     out->n_dcs = n_dcs;
     out->n_keys = n_keys;
+    out->key_id0 = nullptr;  // fresh op ids: no index until agn_log_index_ids
     if (recs->n == 0) {
         AGN_HIP(hipMemsetAsync((void *)out->key_off, 0, (n_keys + 1) * 8, (hipStream_t)stream));
         if (out_totals) AGN_HIP(hipMemsetAsync(out_totals, 0, 16, (hipStream_t)stream));
@@ -455,6 +466,7 @@ int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
     out->n_dcs = log->n_dcs;
     out->n_keys = log->n_keys;
     out->key_type = log->key_type;
+    out->key_id0 = nullptr;  // pruning leaves id gaps: rebuild with agn_log_index_ids
     return launch_prune_ops(*log, prune, threshold, threshold_mask, *out, out_flags, out_totals,
                             (hipStream_t)stream);
 }
@@ -680,10 +692,14 @@ int agn_gen_dev(agn_ctx *ctx, const agn_gen_cfg *cfg, agn_log *log, agn_read *re
     if (K == 0) (void)hipMemsetAsync((void *)log->key_off, 0, sizeof(uint64_t), s);
     hipLaunchKernelGGL(k_gen, dim3(blocks), dim3(256), 0, s, c, *log, *req, 1, scratch, nullptr);
     hipError_t he = hipGetLastError();
+    // the consecutive-id index (ids 1..N per key), as an engine-built log carries it
+    log->key_id0 = dmalloc<uint32_t>(K, err);
+    if (!err && he == hipSuccess && K) err = launch_index_ids(*log, (uint32_t *)log->key_id0, s);
     (void)hipStreamSynchronize(s);
     (void)hipFree(scratch);
-    if (he != hipSuccess) return fail(AGN_EHIP, "k_gen: %s", hipGetErrorString(he));
-    return AGN_OK;
+    if (he != hipSuccess) err = fail(AGN_EHIP, "k_gen: %s", hipGetErrorString(he));
+    if (err) agn_gen_free_dev(ctx, log, req);
+    return err;
 }
 
 int agn_gen_free_dev(agn_ctx *ctx, agn_log *log, agn_read *req) {
@@ -694,7 +710,8 @@ int agn_gen_free_dev(agn_ctx *ctx, agn_log *log, agn_read *req) {
                           log ? log->op_id : nullptr, log ? log->txid : nullptr,
                           log ? log->eff : nullptr, log ? log->tag : nullptr,
                           log ? log->add_tok : nullptr, log ? log->rem_off : nullptr,
-                          log ? log->rem_tok : nullptr, req ? req->keys : nullptr,
+                          log ? log->rem_tok : nullptr, log ? log->key_id0 : nullptr,
+                          req ? req->keys : nullptr,
                           req ? req->R : nullptr, req ? req->R_mask : nullptr,
                           req ? req->sct : nullptr, req ? req->sct_mask : nullptr,
                           req ? req->sct_ignore : nullptr, req ? req->txid : nullptr,

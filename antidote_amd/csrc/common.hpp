@@ -119,6 +119,7 @@ agn_ctx *oplog_ctx(const agn_oplog *L);
 // Launchers (defined in the .hip files).
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t s);
+int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st);
 int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                          hipStream_t s);
 int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,

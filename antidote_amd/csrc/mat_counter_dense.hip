@@ -110,6 +110,25 @@ __device__ __forceinline__ uint32_t byte_of(const uint8_t *__restrict__ p, uint6
     return (w >> ((uint32_t)(idx & 3u) * 8u)) & 0xffu;
 }
 
+// Per-key metadata as branch-free scalar loads, so key_off, the segment
+// length and the id base share one round trip (a conditional load would be
+// scheduled after the previous one's wait): absent arrays are replaced by an
+// in-bounds dummy address whose value is discarded.
+struct KeyMeta {
+    uint64_t off, n;
+    uint32_t id0;
+};
+__device__ __forceinline__ KeyMeta key_meta(uint64_t key, const uint64_t *__restrict__ key_off,
+                                            const uint64_t *__restrict__ key_len,
+                                            const uint32_t *__restrict__ key_id0) {
+    const uint64_t *lp = key_len ? key_len + key : key_off + key + 1;
+    const uint32_t *ip = key_id0 ? key_id0 + key : reinterpret_cast<const uint32_t *>(key_off + key);
+    const uint64_t off = uniform_u64(key_off[key]);
+    const uint64_t l = uniform_u64(*lp);
+    const uint32_t id = __builtin_amdgcn_readfirstlane(*ip);
+    return KeyMeta{off, key_len ? l : l - off, key_id0 ? id : AGN_ID0_NONE};
+}
+
 struct DenseArgs {
     uint64_t n_req;
     uint64_t n_entries;
@@ -272,11 +291,23 @@ __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
 // slots full and the HBM queue deep, while each wave's dependent round trips
 // (metadata -> rows -> NewLastOp id) overlap with other waves' instead of
 // serialising inside one.  Side values are scalar loads (no vmcnt drains).
-template <int D, bool ANY_WARM, int WPB, bool GLDS>
+// R, key_off, the segment length and the consecutive-id base (key_id0) are
+// issued as one group of scalar loads, and with key_id0 the NewLastOp id
+// needs no load after the scan: +0.9 % against the previous prologue
+// (profiles/r01/ab_counter_prologue.log).  Where the rest of the gap to the
+// read ceiling goes (diagnostic builds, scripts/build_diag.sh,
+// profiles/r01/ab_counter_attribution.log): not latency -- two requests per
+// wave with both keys' rows in flight (2x bytes per wave slot) measured
+// +0.2 %, dropping the metadata loads 0.3 % -- but the per-key result
+// writes: 92 B per key (1.9 % of the bytes) cost 9 % of the kernel time
+// (writing 16 B instead: 8.33 -> 7.57 ms), full 128 B record lines 1 %,
+// non-temporal stores +7 % worse.  The HBM read/write turnaround, not the
+// instruction stream, is the remaining bound.
+template <int D, bool ANY_WARM, int WPB, bool GLDS, bool KEYS>
 __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
     const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
-    const uint64_t *__restrict__ oc,
+    const uint32_t *__restrict__ key_id0, const uint64_t *__restrict__ oc,
     const uint32_t *__restrict__ op_id, const int64_t *__restrict__ eff,
     const uint64_t *__restrict__ log_txid, const uint64_t *__restrict__ R,
     const uint64_t *__restrict__ sct, const uint8_t *__restrict__ sct_ignore,
@@ -294,9 +325,14 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t i = uniform_u64((uint64_t)blk * WPB + (uint64_t)w);
     if (i >= a.n_req) return;
-    const uint64_t key = keys ? uniform_u64(keys[i]) : i;
-    const uint64_t off = uniform_u64(key_off[key]);
-    const uint64_t n = uniform_u64(key_len ? key_len[key] : key_off[key + 1] - off);
+    uint64_t r[D], s[D], ct[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) r[j] = uniform_u64(R[i * D + j]);  // issued with the key's metadata
+    // KEYS = false (identity key map): R and the key's metadata in one round trip
+    const uint64_t key = KEYS ? uniform_u64(keys[i]) : i;
+    const KeyMeta km = key_meta(key, key_off, key_len, key_id0);
+    const uint64_t off = km.off, n = km.n;
+    const uint32_t id0 = km.id0;  // consecutive-id base (agn_log_index_ids)
     if (n != 0 && key_type != nullptr && byte_of(key_type, key) != (a.req_type & 0xffu)) {
         if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
             o_flags[i] = AGN_F_ERR_CORRUPTED;
@@ -304,11 +340,9 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
         }
         return;
     }
-    uint64_t r[D], s[D], ct[D];
     const bool sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && byte_of(sct_ignore, i));
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        r[j] = uniform_u64(R[i * D + j]);
         s[j] = sct_ign ? 0ull : uniform_u64(sct[i * D + j]);
         ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
     }
@@ -334,8 +368,11 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     }
     // NewLastOp id and base value: scalar loads, issued before the reductions
     if (hid < 0) {
-        const uint64_t hole_e = first_excl >= 0 ? off + (uint64_t)first_excl : off + n - 1;
-        hid = n ? (int64_t)op_id[uniform_u64(hole_e)] : 0;
+        const uint64_t pos = first_excl >= 0 ? (uint64_t)first_excl : n - 1;
+        if (id0 != AGN_ID0_NONE)  // op_id[off + pos] == id0 + pos (agn_log_index_ids)
+            hid = n ? (int64_t)((uint64_t)id0 + pos) : 0;
+        else
+            hid = n ? (int64_t)op_id[uniform_u64(off + pos)] : 0;
     }
     const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)base_value[i]) : 0;
 
@@ -372,6 +409,12 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     }
 }
 
+// agn_log.key_id0, unless AGN_COUNTER_ID0=0 (A/B knob: always load the op id)
+inline const uint32_t *id0_index(const agn_log &log) {
+    const char *v = getenv("AGN_COUNTER_ID0");
+    return (v && v[0] == '0') ? nullptr : log.key_id0;
+}
+
 // LDS-DMA row path (even D: 16-byte aligned chunks): opt-in, AGN_COUNTER_GLDS=1.
 // Its speed is box-dependent: on two MI355X boxes it beat the VGPR-load path
 // by 7-10 % (cfg2 7.29-7.55 vs 8.16-8.44 ms), on three others it lost by
@@ -382,26 +425,32 @@ inline bool counter_glds() {
     return v && v[0] == '1';
 }
 
-template <int D, int WPB, bool GLDS>
-int launch_key_g(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+template <int D, int WPB, bool GLDS, bool KEYS>
+int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u};
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);
     if (req.sct)
-        hipLaunchKernelGGL((k_counter_key<D, true, WPB, GLDS>), dim3((unsigned)nb), dim3(64 * WPB),
-                           0, st, a, req.keys, log.key_off, log.key_len, log.key_type, log.oc,
-                           log.op_id, log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
-                           req.base_value, out.value, out.hole, out.lastct, out.count,
-                           out.flags, out.err_pos);
-    else
-        hipLaunchKernelGGL((k_counter_key<D, false, WPB, GLDS>), dim3((unsigned)nb),
+        hipLaunchKernelGGL((k_counter_key<D, true, WPB, GLDS, KEYS>), dim3((unsigned)nb),
                            dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
-                           log.key_type, log.oc, log.op_id, log.eff, log.txid, req.R, req.sct,
-                           req.sct_ignore, req.txid, req.base_value, out.value, out.hole,
-                           out.lastct, out.count, out.flags, out.err_pos);
+                           log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
+                           req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
+                           out.hole, out.lastct, out.count, out.flags, out.err_pos);
+    else
+        hipLaunchKernelGGL((k_counter_key<D, false, WPB, GLDS, KEYS>), dim3((unsigned)nb),
+                           dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
+                           log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
+                           req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
+                           out.hole, out.lastct, out.count, out.flags, out.err_pos);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
+}
+
+template <int D, int WPB, bool GLDS>
+int launch_key_g(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    return req.keys ? launch_key_k<D, WPB, GLDS, true>(log, req, out, st)
+                    : launch_key_k<D, WPB, GLDS, false>(log, req, out, st);
 }
 
 template <int D, int WPB>
@@ -413,25 +462,49 @@ int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, h
 }
 
 // Waves (= requests) per block: 1 measured 1.4-3.4 % faster than 2 and
-// 0-1.6 % faster than 4 on cfg2 (profiles/r01/ab_counter_wpb.log).
-int dense_wpb() {
-    const char *v = getenv("AGN_COUNTER_WPB");  // A/B knob
-    const int w = v ? atoi(v) : 1;
-    return (w == 1 || w == 2 || w == 4 || w == 8) ? w : 1;
-}
-
+// 0-1.6 % faster than 4 on cfg2 (profiles/r01/ab_counter_wpb.log), so only
+// WPB = 1 is instantiated.
 template <int D>
 int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
-    switch (dense_wpb()) {
-        case 4: return launch_key<D, 4>(log, req, out, st);
-        case 8: return launch_key<D, 8>(log, req, out, st);
-        case 2: return launch_key<D, 2>(log, req, out, st);
-        default: return launch_key<D, 1>(log, req, out, st);
+    return launch_key<D, 1>(log, req, out, st);
+}
+
+// agn_log_index_ids: one wave per key, lanes over the segment's positions.
+__global__ __launch_bounds__(256) void k_index_ids(const uint64_t *__restrict__ key_off,
+                                                  const uint64_t *__restrict__ key_len,
+                                                  const uint32_t *__restrict__ op_id,
+                                                  uint64_t n_keys, uint32_t *__restrict__ out) {
+    const uint64_t k = uniform_u64((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (k >= n_keys) return;
+    const int lane = lane_id();
+    const uint64_t off = key_off[k];
+    const uint64_t n = key_len ? key_len[k] : key_off[k + 1] - off;
+    if (n == 0) {
+        if (lane == 0) out[k] = AGN_ID0_NONE;
+        return;
     }
+    const uint64_t id0 = op_id[off];
+    bool ok = id0 + (n - 1) < (uint64_t)AGN_ID0_NONE;  // id0 + p fits and is never NONE
+    for (uint64_t b = 0; ok && b < n; b += AGN_WAVE) {
+        const uint64_t p = b + (uint64_t)lane;
+        const bool bad = p < n && (uint64_t)op_id[off + p] != id0 + p;
+        ok = ballot(bad) == 0;
+    }
+    if (lane == 0) out[k] = ok ? (uint32_t)id0 : AGN_ID0_NONE;
 }
 
 }  // namespace
+
+int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st) {
+    const uint64_t nb = (log.n_keys + 3) / 4;
+    if (nb == 0) return AGN_OK;
+    if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "index_ids: too many keys");
+    hipLaunchKernelGGL(k_index_ids, dim3((unsigned)nb), dim3(256), 0, st, log.key_off,
+                       log.key_len, log.op_id, log.n_keys, out);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
 
 // Dense fast path applies when every clock is dense and D <= 8; returns
 // AGN_ENOTSUP otherwise so the caller uses the general kernel.

@@ -112,6 +112,19 @@ class Engine:
             setattr(s, name, b.ptr)
         return d
 
+    def index_ids(self, dlog, stream=None) -> DevBuf:
+        """Build agn_log.key_id0 (consecutive op-id base per key, agn_log_index_ids)
+        for a device log and attach it; returns the buffer (owned by dlog when
+        dlog is DeviceArrays)."""
+        ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
+        b = self.empty(max(1, int(ls.n_keys)) * 4)
+        check(self.lib.agn_log_index_ids(self.ctx, C.byref(ls), b.ptr, stream),
+              "agn_log_index_ids")
+        ls.key_id0 = b.ptr
+        if isinstance(dlog, DeviceArrays):
+            dlog.bufs["key_id0"] = b
+        return b
+
     def alloc_log_like(self, log: EncodedLog) -> DeviceArrays:
         """Device arrays with the sizes (and presence) of `log`'s (agn_prune_ops output)."""
         s = _abi.AgnLog()

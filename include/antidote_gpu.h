@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AGN_ABI_VERSION 2
+#define AGN_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 #define AGN_OK 0
@@ -97,7 +97,16 @@ typedef struct agn_log {
     const uint32_t *rem_off;  /* [n_entries+1] CSR into rem_tok (with key_len: contiguous
                                  within a key, rem_off[key_off[k]+key_len[k]] = end) */
     const uint64_t *rem_tok;  /* removed (set) / overridden (register) tokens */
+    /* ABI v3, optional (NULL = read op_id): per key, the op id of the segment's
+     * first entry when its ids are consecutive (op_id[off+p] == key_id0 + p
+     * for every p < len), else AGN_ID0_NONE.  Ids stay consecutive from
+     * op_insert_gc's ets:update_counter (src/materializer_vnode.erl:630) until
+     * a GC prune leaves gaps (:576-585); built by agn_log_index_ids.  Lets the
+     * counter kernel derive NewLastOp without a dependent op_id load. */
+    const uint32_t *key_id0;
 } agn_log;
+
+#define AGN_ID0_NONE 0xFFFFFFFFu
 
 /* ---- a batch of reads: one materialize/4 per requested key ------------- */
 typedef struct agn_read {
@@ -169,6 +178,12 @@ int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req,
  * materialize/4 whose ops list arrives as an Erlang term. */
 int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req,
                          agn_result *out);
+
+/* agn_log.key_id0 for a device log: out[k] = op_id[off_k] when the ids of
+ * key k's segment are consecutive, else AGN_ID0_NONE (also for empty keys).
+ * The caller owns out ([n_keys] u32, device) and sets log.key_id0 = out; the
+ * index must be rebuilt whenever op ids change (append past a gap, prune). */
+int agn_log_index_ids(agn_ctx *ctx, const agn_log *log, uint32_t *out, void *stream);
 
 /* Upper bound of live pairs per request for set/register types:
  * writes cap_off[n_req+1] (host pointers): cap = #adding entries of the key
