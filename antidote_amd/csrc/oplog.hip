@@ -134,13 +134,15 @@ __global__ void __launch_bounds__(256) k_scatter_rows(uint64_t *__restrict__ oc,
 }
 
 __global__ void __launch_bounds__(256) k_keys(uint64_t *__restrict__ key_off,
-                                              uint64_t *__restrict__ key_len, uint64_t n,
+                                              uint64_t *__restrict__ key_len,
+                                              uint32_t *__restrict__ key_id0, uint64_t n,
                                               const uint64_t *__restrict__ kv) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint64_t k = kv[3 * i];
-    key_off[k] = kv[3 * i + 1];
-    key_len[k] = kv[3 * i + 2];
+    const uint64_t k = kv[4 * i];
+    key_off[k] = kv[4 * i + 1];
+    key_len[k] = kv[4 * i + 2];
+    key_id0[k] = (uint32_t)kv[4 * i + 3];
 }
 
 // Per-key entry and token counts of a CSR log (prune output).
@@ -227,6 +229,7 @@ struct agn_oplog {
     std::vector<uint64_t> start, tstart;
     std::vector<uint32_t> cap, len, counter, tcap, tlen;
     std::vector<uint32_t> dlen, dtlen;  // lengths the device already holds
+    std::vector<uint32_t> id0;          // agn_log.key_id0 of each segment (host copy)
     std::vector<uint8_t> dirty;
     std::vector<uint64_t> dirty_keys;
     std::vector<int64_t> move_of;  // index into moves, -1 = none pending
@@ -238,6 +241,7 @@ struct agn_oplog {
     Arena a;
     uint64_t dcap = 0, tdcap = 0;  // allocated slots
     uint64_t *key_off = nullptr, *key_len = nullptr;
+    uint32_t *key_id0 = nullptr;  // consecutive-id index, kept with key_off / key_len
     hipEvent_t up_done = nullptr;
     bool up_pending = false;
     void *pinned = nullptr;
@@ -344,6 +348,7 @@ void fill_view(const agn_oplog *L, agn_log *v) {
     v->add_tok = L->a.add;
     v->rem_off = L->a.rem_off;
     v->rem_tok = L->a.tok;
+    v->key_id0 = L->key_id0;
 }
 
 int do_flush(agn_oplog *L, hipStream_t st) {
@@ -372,7 +377,7 @@ int do_flush(agn_oplog *L, hipStream_t st) {
                  o_tlen = slot(n * 4), o_opid = slot(n * 4), o_tag = slot(L->tags ? n * 4 : 0),
                  o_eff = slot(L->tags ? 0 : n * 8), o_oc = slot(n * D * 8),
                  o_mask = slot(L->sparse ? n * W * 8 : 0), o_tok = slot(L->s_tok.size() * 8),
-                 o_keys = slot(nk * 24);
+                 o_keys = slot(nk * 32);
     rc = ensure_pinned(L, off);
     if (rc) return rc;
     char *h = (char *)L->pinned;
@@ -397,9 +402,10 @@ int do_flush(agn_oplog *L, hipStream_t st) {
         uint64_t *kv = (uint64_t *)(h + o_keys);
         for (uint64_t j = 0; j < nk; ++j) {
             const uint64_t k = L->dirty_keys[j];
-            kv[3 * j] = k;
-            kv[3 * j + 1] = L->start[k];
-            kv[3 * j + 2] = L->len[k];
+            kv[4 * j] = k;
+            kv[4 * j + 1] = L->start[k];
+            kv[4 * j + 2] = L->len[k];
+            kv[4 * j + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
         }
     }
     char *d = nullptr;
@@ -421,8 +427,8 @@ int do_flush(agn_oplog *L, hipStream_t st) {
             L->a.oc, D, n, (const uint64_t *)(d + o_dst), (const uint64_t *)(d + o_oc));
     }
     if (nk)
-        k_keys<<<(unsigned)((nk + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, nk,
-                                                              (const uint64_t *)(d + o_keys));
+        k_keys<<<(unsigned)((nk + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, L->key_id0,
+                                                              nk, (const uint64_t *)(d + o_keys));
     AGN_HIP(hipGetLastError());
     AGN_HIP(hipFreeAsync(d, st));
     for (uint64_t k : L->dirty_keys) {
@@ -478,6 +484,7 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
         L->tstart.assign(n_keys, 0);
         for (auto *v : {&L->cap, &L->len, &L->counter, &L->tcap, &L->tlen, &L->dlen, &L->dtlen})
             v->assign(n_keys, 0);
+        L->id0.assign(n_keys, AGN_ID0_NONE);
         L->dirty.assign(n_keys, 0);
         L->move_of.assign(n_keys, -1);
     } catch (...) {
@@ -489,6 +496,8 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
     if (e == hipSuccess) e = hipMalloc((void **)&L->key_len, std::max<uint64_t>(n_keys, 1) * 8);
     if (e == hipSuccess) e = hipMemset(L->key_off, 0, std::max<uint64_t>(n_keys, 1) * 8);
     if (e == hipSuccess) e = hipMemset(L->key_len, 0, std::max<uint64_t>(n_keys, 1) * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->key_id0, std::max<uint64_t>(n_keys, 1) * 4);
+    if (e == hipSuccess) e = hipMemset(L->key_id0, 0xff, std::max<uint64_t>(n_keys, 1) * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L->up_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         agn_oplog_destroy(L);
@@ -505,7 +514,7 @@ int agn_oplog_destroy(agn_oplog *L) {
     Arena &a = L->a;
     for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
                     (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok,
-                    (void *)L->key_off, (void *)L->key_len})
+                    (void *)L->key_off, (void *)L->key_len, (void *)L->key_id0})
         if (p) (void)hipFree(p);
     if (L->pinned) (void)hipHostFree(L->pinned);
     if (L->up_done) (void)hipEventDestroy(L->up_done);
@@ -588,6 +597,13 @@ static int oplog_append_locked(agn_oplog *L, uint64_t n, const uint64_t *keys,
         L->s_tlen.push_back(tl);
         L->s_dst.push_back(0);
         L->s_tdst.push_back(0);
+        // consecutive ids (op_id[p] == id0 + p) survive appends until a
+        // same_op entry or a gap; AGN_ID0_NONE itself is never an id base
+        const uint32_t p = L->len[k];
+        if (p == 0) L->id0[k] = id;
+        else if (L->id0[k] != AGN_ID0_NONE && (uint64_t)id != (uint64_t)L->id0[k] + p)
+            L->id0[k] = AGN_ID0_NONE;
+        if (id == AGN_ID0_NONE) L->id0[k] = AGN_ID0_NONE;
         ++L->len[k];
         L->tlen[k] += tl;
         if (!L->dirty[k]) {
@@ -729,6 +745,18 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
                                                     L->tags ? d_start + K : nullptr, L->key_off,
                                                     L->key_len);
     e = hipGetLastError();
+    // pruning leaves id gaps: rebuild the consecutive-id index of every key
+    if (e == hipSuccess) {
+        agn_log nv;
+        std::memset(&nv, 0, sizeof nv);
+        nv.n_keys = K;
+        nv.key_off = L->key_off;
+        nv.key_len = L->key_len;
+        nv.op_id = b.op_id;
+        if (launch_index_ids(nv, L->key_id0, st) != AGN_OK) e = hipErrorLaunchFailure;
+    }
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(L->id0.data(), L->key_id0, K * 4, hipMemcpyDeviceToHost, st);
     // ns must outlive the async H2D above.
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFreeAsync(d_start, st);

@@ -111,6 +111,18 @@ def expect_counter_ids(log, got, start=None):
             assert got[e] == nxt, (k, e)
 
 
+def check_id_index(eng, view, K):
+    """The op log keeps agn_log.key_id0 (the consecutive-op-id index) in step
+    with its segments, through appends, same_op entries and prunes."""
+    from test_id_index import expected_index
+    assert view.key_id0
+    off = dl(eng, view.key_off, np.uint64, K)
+    ln = dl(eng, view.key_len, np.uint64, K)
+    top = int(max((int(off[k]) + int(ln[k]) for k in range(K)), default=0))
+    ids = dl(eng, view.op_id, np.uint32, top)
+    assert np.array_equal(dl(eng, view.key_id0, np.uint32, K), expected_index(off, ln, ids))
+
+
 def materialize_view(eng, oracle_lib, view, log, req, sparse):
     cap = state_capacity(log, req)
     dreq = eng.upload_read(req, sparse=sparse)
@@ -183,6 +195,7 @@ def test_oplog_append_materialize(eng, oracle_lib, crdt, D, sparse, init):
         expect_counter_ids(log, got)
         log2 = renumbered(log, got)
         view = ol.flush()
+        check_id_index(eng, view, log.n_keys)
         st = ol.stats()
         assert st["entries"] == log.n_entries and st["slots"] >= log.n_entries
         assert not materialize_view(eng, oracle_lib, view, log2, req, sparse)
@@ -207,6 +220,7 @@ def test_oplog_prune_then_append(eng, oracle_lib, crdt, D, sparse, init):
         assert np.array_equal(eng.download(fl, np.uint32, (log.n_keys,)), wflags)
         assert ol.stats()["entries"] == n_out
         view = ol.flush()
+        check_id_index(eng, view, log.n_keys)
         segs = segments(eng, view, log.n_keys, D, W, tags, sparse)
         for k in range(log.n_keys):
             w = csr_key(want, k, tags)
@@ -241,6 +255,7 @@ def test_oplog_prune_then_append(eng, oracle_lib, crdt, D, sparse, init):
         expect_counter_ids(more, got2, counters)
         both = concat(pruned, renumbered(more, got2))
         view = ol.flush()
+        check_id_index(eng, view, log.n_keys)
         assert not materialize_view(eng, oracle_lib, view, both, req2, sparse)
         for b in (bp, bt, btm, fl):
             if b is not None:
