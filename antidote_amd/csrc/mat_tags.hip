@@ -544,8 +544,27 @@ int launch_full(const agn_log &log, const agn_read &req, const agn_result &out, 
                 : launch_shape<DPL, LPO, SPARSE, false, SET, false>(log, req, out, st);
 }
 
+// Dense clocks wider than 8 DCs run 4 DCs per lane: 83 VGPRs (5 waves/SIMD)
+// against 116 (4 waves/SIMD) with 8 per lane -- cfg3 -3.8/-4.7 %, cfg4
+// -0.7/-1.3 % on two boxes; 2 per lane (69 VGPRs, but LDS caps the CU at 22
+// waves) lost 12 % / 9 % to the extra sub-iterations
+// (profiles/r01/ab_tags_dpl.log).  AGN_TAGS_DPL8=1 (A/B knob) keeps 8.
+inline bool tags_dpl8() {
+    const char *v = getenv("AGN_TAGS_DPL8");
+    return v && v[0] == '1';
+}
+
 template <bool SPARSE, bool SET>
 int dispatch(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    if constexpr (!SPARSE) {
+        const uint32_t D = log.n_dcs;
+        if (D > 8 && D <= 128 && !tags_dpl8()) {
+            if (D <= 16) return launch_full<4, 4, false, SET>(log, req, out, st);
+            if (D <= 32) return launch_full<4, 8, false, SET>(log, req, out, st);
+            if (D <= 64) return launch_full<4, 16, false, SET>(log, req, out, st);
+            return launch_full<4, 32, false, SET>(log, req, out, st);
+        }
+    }
 #define AGN_L(DPL, LPO) launch_full<DPL, LPO, SPARSE, SET>(log, req, out, st)
     AGN_DISPATCH_SHAPES(log.n_dcs, AGN_L)
 #undef AGN_L

@@ -21,8 +21,13 @@ K = cfg["n_keys"]
 eng = Engine(0)
 # extra libraries: name=path arguments (default: prev=tools/libagn_prev.so)
 LIBS = {}
+ENV_VARS = {}
 for a in (sys.argv[2:] or ["prev=tools/libagn_prev.so"]):
     name, path = a.split("=", 1)
+    if path.startswith("env:"):  # name=env:KEY=VAL: the current library with an env knob
+        k, v = path[4:].split("=", 1)
+        ENV_VARS[name] = {k: v}
+        continue
     lib = C.CDLL(os.path.join(ROOT, path), mode=os.RTLD_LOCAL)
     _abi.bind(lib, {k: v for k, v in _abi.PROTOTYPES.items() if hasattr(lib, k)})
     ctx = C.c_void_p()
@@ -38,9 +43,10 @@ if cfg["crdt_type"] != 1:
     cap = np.arange(K + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
 res = eng.alloc_result(K, cfg["n_dcs"], sparse=False, cap_off=cap)
 rec = eng.empty(K * 128) if any(n.startswith("rec") for n in LIBS) else None
-ENVS = ("AGN_COUNTER_ID0", "AGN_COUNTER_KPW", "AGN_COUNTER_GLDS")
+ENVS = {"AGN_COUNTER_ID0", "AGN_COUNTER_GLDS"} | {k for e in ENV_VARS.values() for k in e}
 VARS = {"cur": ("cur", {})}
 VARS.update({n: (n, {}) for n in LIBS})
+VARS.update({n: ("cur", e) for n, e in ENV_VARS.items()})
 
 
 def run(lib):

@@ -100,6 +100,24 @@ def test_random_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sparse, impl):
     assert not bad, bad[:10]
 
 
+@pytest.mark.parametrize("dpl8", [False, True])
+@pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])
+@pytest.mark.parametrize("D", [12, 16, 40, 64, 128])
+def test_tags_dense_shapes_vs_oracle(eng, oracle_lib, monkeypatch, dpl8, crdt, D):
+    """Dense D > 8 tag kernel shapes: 4 DCs per lane (default) and the
+    8-per-lane shape (AGN_TAGS_DPL8=1)."""
+    if dpl8:
+        monkeypatch.setenv("AGN_TAGS_DPL8", "1")
+    else:
+        monkeypatch.delenv("AGN_TAGS_DPL8", raising=False)
+    log, req, cap = random_case(4409 * crdt + D, crdt, 150 if D < 100 else 60, D, 150, warm=0.4,
+                                txid=0.3,
+                                invalid=0.02, corrupt=0.03, base=0.4,
+                                multi=0.15 if crdt == _abi.SET_AW else 0.0)
+    _, _, bad = _oracle_vs_gpu(eng, oracle_lib, crdt, D, log, req)
+    assert not bad, bad[:10]
+
+
 def test_long_keys_vs_oracle(eng, oracle_lib, counter_impl):
     """Keys far longer than a wave (1000+ ops, like large_list_test) and
     set_aw state that forces table compaction."""
