@@ -131,6 +131,8 @@ PROTOTYPES = {
                                        C.POINTER(AgnResult)]),
     "agn_state_capacity": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead), P]),
     "agn_log_index_ids": (C.c_int, [P, C.POINTER(AgnLog), P, P]),
+    "agn_tune": (C.c_int, [P, C.POINTER(AgnLog), C.POINTER(AgnRead), C.POINTER(AgnResult), P,
+                           C.c_int, C.POINTER(C.c_int), P]),
     "agn_select_base": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, P, P, P, P]),
     "agn_gst_min": (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64, P, P, P, P]),
     "agn_gst_finalize": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P]),

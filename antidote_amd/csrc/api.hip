@@ -190,6 +190,27 @@ int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_r
     return launch_tags(*log, *req, *out, s);
 }
 
+int agn_tune(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out,
+             void *stream, int rounds, int *choice, float *ms) {
+    if (!choice) return fail(AGN_EINVAL, "tune: null choice");
+    *choice = -1;
+    int rc = validate(log, req, out);
+    if (rc) return rc;
+    rc = use_device(ctx);
+    if (rc) return rc;
+    if (req->n_req == 0) return AGN_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (rounds < 1) rounds = 1;
+    rc = tune_counter_dense(*log, *req, *out, s, rounds, choice, ms);
+    if (rc != AGN_ENOTSUP) return rc;
+    *choice = -1;  // one kernel for this shape: plain materialize
+    rc = log->crdt_type == AGN_COUNTER_PN ? launch_counter(*log, *req, *out, s)
+                                          : launch_tags(*log, *req, *out, s);
+    if (rc) return rc;
+    AGN_HIP(hipStreamSynchronize(s));
+    return AGN_OK;
+}
+
 int agn_log_index_ids(agn_ctx *ctx, const agn_log *log, uint32_t *out, void *stream) {
     if (!log || !out) return fail(AGN_EINVAL, "index_ids: null argument");
     if (log->n_keys && !log->key_off) return fail(AGN_EINVAL, "index_ids: key_off required");

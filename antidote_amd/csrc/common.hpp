@@ -122,6 +122,8 @@ int launch_counter(const agn_log &log, const agn_read &req, const agn_result &ou
 int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st);
 int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                          hipStream_t s);
+int tune_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
+                       hipStream_t st, int rounds, int *choice, float *ms);
 int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
                 hipStream_t s);
 int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,

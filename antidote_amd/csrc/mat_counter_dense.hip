@@ -27,6 +27,7 @@
 //     loads, never vector loads + vmcnt(0).
 // HBM bytes per op: 8*D + 8; per key: 8 + 16*D + 32;
 // the LDS-DMA path also reads the chunk's 4-byte op ids (+4 per op).
+#include <atomic>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -415,14 +416,26 @@ inline const uint32_t *id0_index(const agn_log &log) {
     return (v && v[0] == '0') ? nullptr : log.key_id0;
 }
 
-// LDS-DMA row path (even D: 16-byte aligned chunks): opt-in, AGN_COUNTER_GLDS=1.
-// Its speed is box-dependent: on two MI355X boxes it beat the VGPR-load path
-// by 7-10 % (cfg2 7.29-7.55 vs 8.16-8.44 ms), on three others it lost by
-// 6-14 % (8.86-9.28 vs 7.95-8.39 ms), consistently across processes on one
-// box (profiles/r01/ab_counter_glds*.log); the VGPR path is the robust default.
+// LDS-DMA row path (even D: 16-byte aligned chunks).  Its speed is
+// box-dependent: on two MI355X boxes it beat the VGPR-load path by 7-10 %
+// (cfg2 7.29-7.55 vs 8.16-8.44 ms), on three others it lost by 6-14 %
+// (8.86-9.28 vs 7.95-8.39 ms), consistently across processes on one box
+// (profiles/r01/ab_counter_glds*.log).  So the choice is made per process and
+// device by agn_tune (timing both bit-identical variants on the caller's
+// batch); until then the VGPR path runs.  AGN_COUNTER_GLDS=0/1 forces it.
+constexpr int kMaxDev = 64;
+std::atomic<int> g_glds_choice[kMaxDev];  // 0: untuned / VGPR rows, 1: LDS-DMA rows
+
+inline int cur_dev() {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    return d >= 0 && d < kMaxDev ? d : 0;
+}
+
 inline bool counter_glds() {
     const char *v = getenv("AGN_COUNTER_GLDS");
-    return v && v[0] == '1';
+    if (v && (v[0] == '0' || v[0] == '1')) return v[0] == '1';
+    return g_glds_choice[cur_dev()].load(std::memory_order_relaxed) == 1;
 }
 
 template <int D, int WPB, bool GLDS, bool KEYS>
@@ -506,6 +519,51 @@ int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st) {
     return AGN_OK;
 }
 
+// agn_tune for the dense counter path: alternate the VGPR-row and LDS-DMA-row
+// kernels over the caller's batch (`rounds` launches each, on `st`), keep each
+// variant's fastest launch, and select LDS-DMA for this device only when it
+// is at least 3 % faster (the VGPR path is the robust default).  Both write
+// the same results, so `out` holds the batch's results afterwards.
+template <int D>
+int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st,
+               int rounds, int *choice, float *ms) {
+    hipEvent_t e0, e1;
+    AGN_HIP(hipEventCreate(&e0));
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return fail(AGN_EHIP, "tune: hipEventCreate");
+    }
+    float best[2] = {3.4e38f, 3.4e38f};
+    int rc = AGN_OK;
+    for (int r = 0; r < rounds && rc == AGN_OK; ++r) {
+        for (int v = 0; v < 2 && rc == AGN_OK; ++v) {
+            const int var = (r & 1) ? 1 - v : v;  // alternate which variant goes first
+            if (hipEventRecord(e0, st) != hipSuccess) { rc = fail(AGN_EHIP, "tune: record"); break; }
+            rc = var ? launch_key_g<D, 1, true>(log, req, out, st)
+                     : launch_key_g<D, 1, false>(log, req, out, st);
+            if (rc) break;
+            float t = 0.f;
+            if (hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&t, e0, e1) != hipSuccess) {
+                rc = fail(AGN_EHIP, "tune: event timing");
+                break;
+            }
+            best[var] = t < best[var] ? t : best[var];
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc;
+    const int c = best[1] < 0.97f * best[0] ? 1 : 0;
+    g_glds_choice[cur_dev()].store(c, std::memory_order_relaxed);
+    *choice = c;
+    if (ms) {
+        ms[0] = best[0];
+        ms[1] = best[1];
+    }
+    return AGN_OK;
+}
+
 // Dense fast path applies when every clock is dense and D <= 8; returns
 // AGN_ENOTSUP otherwise so the caller uses the general kernel.
 int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
@@ -520,6 +578,24 @@ int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_resu
         case 6: return launch_dense<6>(log, req, out, st);
         case 7: return launch_dense<7>(log, req, out, st);
         case 8: return launch_dense<8>(log, req, out, st);
+        default: return AGN_ENOTSUP;
+    }
+}
+
+// Tunable only for the dense counter path with even D (the LDS-DMA variant
+// exists there); AGN_ENOTSUP otherwise, before anything is launched.
+int tune_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
+                       hipStream_t st, int rounds, int *choice, float *ms) {
+    if (log.crdt_type != AGN_COUNTER_PN || log.oc_mask || req.R_mask || req.sct_mask ||
+        out.lastct_mask || req.n_req == 0)
+        return AGN_ENOTSUP;
+    const char *impl = getenv("AGN_COUNTER_IMPL");
+    if (impl && impl[0] == 'g') return AGN_ENOTSUP;  // general kernel forced
+    switch (log.n_dcs) {
+        case 2: return tune_dense<2>(log, req, out, st, rounds, choice, ms);
+        case 4: return tune_dense<4>(log, req, out, st, rounds, choice, ms);
+        case 6: return tune_dense<6>(log, req, out, st, rounds, choice, ms);
+        case 8: return tune_dense<8>(log, req, out, st, rounds, choice, ms);
         default: return AGN_ENOTSUP;
     }
 }

@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-keys", type=int, default=-1,
                     help="CPU-baseline sample size in keys (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="extra multi-thread CPU run")
+    ap.add_argument("--tune-rounds", type=int, default=3,
+                    help="agn_tune launches per kernel variant before timing (0 = no tuning)")
     ap.add_argument("--gst", action="store_true", help="also time a GST epoch + RCCL min-allreduce")
     ap.add_argument("--warm", action="store_true",
                     help="also time the warm read path through the device snapshot cache "
@@ -177,6 +179,19 @@ def main():
 
     for _ in range(a.warmup):
         eng.materialize(dl, dr, res, stream=sp)
+    # agn_tune (untimed, like warmup): pick this box's faster of the
+    # bit-identical row-load variants of the path, if it has two
+    tune = None
+    if a.tune_rounds > 0:
+        choice, tms = eng.tune(dl, dr, res, stream=sp, rounds=a.tune_rounds)
+        if choice >= 0:
+            forced = os.environ.get("AGN_COUNTER_GLDS", "")[:1]
+            if forced in ("0", "1"):       # the environment overrides the selection
+                choice = int(forced)
+            tune = {"selected": ["vgpr_rows", "lds_dma_rows"][choice],
+                    "forced_by_env": forced in ("0", "1"),
+                    "best_ms": {"vgpr_rows": tms[0], "lds_dma_rows": tms[1]},
+                    "rounds": a.tune_rounds}
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -264,6 +279,7 @@ def main():
                          "probe_read_GBps": probe,
                          "frac_of_probe": achieved / probe if probe else None},
             "cpu_baseline": cpu,
+            "kernel_variant": tune,
             "error_keys": err_keys, "mean_included_ops": float(count.mean()),
             "gen_s": t_gen,
         }

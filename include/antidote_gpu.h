@@ -179,6 +179,21 @@ int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req,
 int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req,
                          agn_result *out);
 
+/* Kernel-variant selection for this process and device: runs the batch
+ * (same arguments as agn_materialize) through each bit-identical kernel
+ * variant its shape has, `rounds` launches per variant alternated on
+ * `stream`, and selects the fastest for later agn_materialize calls of the
+ * same path.  Today that is the dense counter_pn path with even D: VGPR row
+ * loads vs non-temporal LDS-DMA rows, whose order differs between MI355X
+ * boxes; the environment variable AGN_COUNTER_GLDS=0/1
+ * overrides the selection.  Blocks until done; `out` then holds the batch's
+ * results.  *choice: -1 = nothing to tune (the batch ran once), 0 = VGPR
+ * rows, 1 = LDS-DMA rows; ms (may be NULL) receives the fastest launch of
+ * each variant in milliseconds ([2]).  Not part of the reference's API: an
+ * engine-setup call, e.g. on the first batch of a partition. */
+int agn_tune(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out,
+             void *stream, int rounds, int *choice, float *ms);
+
 /* agn_log.key_id0 for a device log: out[k] = op_id[off_k] when the ids of
  * key k's segment are consecutive, else AGN_ID0_NONE (also for empty keys).
  * The caller owns out ([n_keys] u32, device) and sets log.key_id0 = out; the

@@ -67,7 +67,8 @@ for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
 
 def _set_impl(monkeypatch, impl):
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
-    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    # "auto" = the VGPR-row dense kernel whatever agn_tune selected in this process
+    monkeypatch.setenv("AGN_COUNTER_GLDS", "0")
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
     elif impl == "glds":
@@ -142,6 +143,39 @@ def _oracle_vs_gpu(eng, oracle_lib, crdt, D, log, req, sparse=False):
         ls.oc_mask = None
     assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
     return res_g, res_o, compare(crdt, D, res_g, res_o, sparse, req.n_req)
+
+
+@pytest.mark.parametrize("crdt,D,sparse", [(_abi.COUNTER_PN, 8, False), (_abi.COUNTER_PN, 4, False),
+                                            (_abi.COUNTER_PN, 3, False), (_abi.COUNTER_PN, 8, True),
+                                            (_abi.SET_AW, 16, False)])
+def test_tune_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sparse):
+    """agn_tune times the path's kernel variants on the batch, leaves the
+    batch's results in `out` (bit-exact vs the oracle) and its selection then
+    drives agn_materialize (results unchanged)."""
+    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    log, req, cap = random_case(4243 + 7 * D + crdt, crdt, 400, D, 150, sparse=sparse, warm=0.4,
+                                txid=0.3, invalid=0.02, corrupt=0.03, base=0.4,
+                                identity=(D % 2 == 0))
+    res_o = alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)
+    ls, rs, os_ = log_struct(log), read_struct(req, sparse=sparse), result_struct(res_o)
+    if not sparse:
+        ls.oc_mask = None
+    assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
+    dl, dr = eng.upload_log(log), eng.upload_read(req, sparse=sparse)
+    res = eng.alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)
+    choice, ms = eng.tune(dl, dr, res, rounds=2)
+    tunable = crdt == _abi.COUNTER_PN and D % 2 == 0 and not sparse
+    assert choice in ((0, 1) if tunable else (-1,))
+    if tunable:
+        assert ms[0] > 0 and ms[1] > 0
+    bad = compare(crdt, D, eng.fetch_result(res), res_o, sparse, req.n_req)
+    assert not bad, bad[:10]
+    res2 = eng.alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)
+    eng.materialize(dl, dr, res2)
+    eng.sync()
+    bad = compare(crdt, D, eng.fetch_result(res2), res_o, sparse, req.n_req)
+    assert not bad, bad[:10]
 
 
 @pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])

@@ -109,7 +109,7 @@ IMPLS = ("auto", "glds", "general")
 @pytest.mark.parametrize("D", [3, 8])
 def test_materialize_with_index_vs_oracle(eng, oracle_lib, monkeypatch, impl, D):
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
-    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    monkeypatch.setenv("AGN_COUNTER_GLDS", "0")  # "auto": VGPR rows, whatever agn_tune chose
     monkeypatch.delenv("AGN_COUNTER_ID0", raising=False)
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
