@@ -141,6 +141,12 @@ int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, const uint64
                     const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
                     const uint8_t *should_gc, const agn_result &res, const int64_t *handle,
                     uint8_t *prune, uint64_t *thr, uint64_t *thrm, hipStream_t st);
+int launch_prune_mark(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+                      const uint64_t *thr_mask, uint8_t *keep, uint64_t *cnt, uint64_t *rcnt,
+                      hipStream_t st);
+int launch_prune_scatter_seg(const agn_log &log, const agn_log &out, const uint8_t *prune,
+                             const uint8_t *keep, const uint64_t *tstart, uint32_t *flags,
+                             hipStream_t st);
 int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
                      const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
                      uint64_t *totals, hipStream_t st);

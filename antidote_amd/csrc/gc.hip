@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_prune_scatter(agn_log log, agn_log out,
                                                        const uint8_t *__restrict__ prune,
                                                        const uint8_t *__restrict__ keep,
                                                        const uint64_t *__restrict__ rbase,
-                                                       uint32_t *__restrict__ flags) {
+                                                       uint32_t *__restrict__ flags, int seg) {
     __shared__ uint64_t src[4][AGN_WAVE];
     const int w = threadIdx.x >> 6;
     const uint64_t k = (uint64_t)blockIdx.x * 4u + (uint64_t)w;
@@ -105,6 +105,15 @@ __global__ __launch_bounds__(256) void k_prune_scatter(agn_log log, agn_log out,
     const uint64_t noff = uniform_u64(out.key_off[k]);
     uint64_t written = 0, rwritten = 0;
     const uint64_t rb = rbase ? uniform_u64(rbase[k]) : 0ull;
+    if (seg) {  // segmented output: the key owns [noff, noff + cap + 1), ~0 = none
+        if (noff == ~0ull) {
+            if (lane == 0 && flags) flags[k] = (prune == nullptr || prune[k] != 0) ? AGN_GC_ALL_PRUNED : 0u;
+            return;
+        }
+        // the segment's first rem_off slot is its own token base (CSR: the
+        // previous key's end, written by that key)
+        if (lane == 0 && log.rem_off) ((uint32_t *)out.rem_off)[noff] = (uint32_t)rb;
+    }
     for (uint64_t b = 0; b < n; b += AGN_WAVE) {
         const uint64_t pos = b + (uint64_t)lane;
         const bool valid = pos < n;
@@ -233,7 +242,7 @@ int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *t
     }
     if (rc == AGN_OK && e == hipSuccess && K) {
         hipLaunchKernelGGL(k_prune_scatter, dim3(grid_for(K, 4, 0x7fffffffu)), dim3(256), 0, st,
-                           log, out, prune, keep, tags ? rbase : nullptr, flags);
+                           log, out, prune, keep, tags ? rbase : nullptr, flags, 0);
         e = hipGetLastError();
     }
     if (rc == AGN_OK && e == hipSuccess && totals) {
@@ -248,6 +257,33 @@ int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *t
     const hipError_t ef = hipFreeAsync(scratch, st);
     if (rc == AGN_OK && ef != hipSuccess) rc = fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
     return rc;
+}
+
+// Two-phase prune_ops into a fresh segmented arena (agn_oplog_prune): the
+// mark pass gives per-key kept entry / token counts, the caller sizes the new
+// segments from them (ETS resize policy), then the scatter pass copies the
+// kept entries straight into their segments -- no CSR intermediate and no
+// re-segmenting copy.  keep: [log.n_entries] bytes, cnt / rcnt: [n_keys].
+int launch_prune_mark(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+                      const uint64_t *thr_mask, uint8_t *keep, uint64_t *cnt, uint64_t *rcnt,
+                      hipStream_t st) {
+    if (log.n_keys == 0) return AGN_OK;
+    const bool sparse = log.oc_mask || thr_mask;
+    return sparse ? mark<true>(log, prune, thr, thr_mask, keep, cnt, rcnt, st)
+                  : mark<false>(log, prune, thr, thr_mask, keep, cnt, rcnt, st);
+}
+
+// out.key_off[k] = the key's new segment start (~0: no segment), tstart[k] =
+// its token segment start (tag logs); out.rem_off holds absolute token
+// positions like the arena's.
+int launch_prune_scatter_seg(const agn_log &log, const agn_log &out, const uint8_t *prune,
+                             const uint8_t *keep, const uint64_t *tstart, uint32_t *flags,
+                             hipStream_t st) {
+    if (log.n_keys == 0) return AGN_OK;
+    hipLaunchKernelGGL(k_prune_scatter, dim3(grid_for(log.n_keys, 4, 0x7fffffffu)), dim3(256), 0,
+                       st, log, out, prune, keep, log.rem_off ? tstart : nullptr, flags, 1);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
 }
 
 }  // namespace agn

@@ -20,9 +20,11 @@
 // move segments, scatter entries, update key_off/key_len.  The arenas grow by
 // doubling with stream-ordered alloc/copy/free.
 //
-// GC.  agn_oplog_prune runs the prune_ops stream compaction (gc.hip) into a
-// CSR, reads back the per-key lengths, applies the ETS resize policy
-// (snapshot_insert_gc, :540-558) and re-segments into a fresh arena.
+// GC.  agn_oplog_prune runs prune_ops (gc.hip) in two passes around one
+// host step: the mark pass (VC filter) gives each key's kept entry and token
+// counts, the host applies the ETS resize policy (snapshot_insert_gc,
+// :540-558) to size the new segments, and the scatter pass copies the kept
+// entries straight from the old arena into their segments of a fresh one.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -143,45 +145,6 @@ __global__ void __launch_bounds__(256) k_keys(uint64_t *__restrict__ key_off,
     key_off[k] = kv[4 * i + 1];
     key_len[k] = kv[4 * i + 2];
     key_id0[k] = (uint32_t)kv[4 * i + 3];
-}
-
-// Per-key entry and token counts of a CSR log (prune output).
-__global__ void __launch_bounds__(256) k_csr_lens(uint64_t K, const uint64_t *__restrict__ key_off,
-                                                  const uint32_t *__restrict__ rem_off,
-                                                  uint32_t *__restrict__ len,
-                                                  uint32_t *__restrict__ tlen) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= K) return;
-    const uint64_t s = key_off[k], e = key_off[k + 1];
-    len[k] = (uint32_t)(e - s);
-    if (tlen) tlen[k] = rem_off ? rem_off[e] - rem_off[s] : 0u;
-}
-
-// CSR (prune output) -> fresh segmented arena; one wave per key.
-__global__ void __launch_bounds__(256) k_reseg(Arena csr, Arena b, uint32_t D, uint32_t W,
-                                               uint64_t K, const uint64_t *__restrict__ csr_off,
-                                               const uint64_t *__restrict__ start,
-                                               const uint64_t *__restrict__ tstart,
-                                               uint64_t *__restrict__ key_off,
-                                               uint64_t *__restrict__ key_len) {
-    const uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= K) return;
-    const uint64_t dst = start[k];  // ~0: the key never had a segment
-    if (lane_id() == 0) key_off[k] = dst == ~0ull ? 0ull : dst;
-    if (dst == ~0ull) {
-        if (lane_id() == 0) key_len[k] = 0;
-        return;
-    }
-    const uint64_t s = csr_off[k];
-    const uint32_t len = (uint32_t)(csr_off[k + 1] - s);
-    uint64_t ts = 0;
-    uint32_t tl = 0;
-    if (csr.rem_off) {
-        ts = csr.rem_off[s];
-        tl = csr.rem_off[s + len] - (uint32_t)ts;
-    }
-    if (lane_id() == 0) key_len[k] = len;
-    copy_segment(csr, b, D, W, s, dst, len, ts, tstart ? tstart[k] : 0, tl, lane_id());
 }
 
 template <class T>
@@ -643,76 +606,56 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     rc = do_flush(L, st);
     if (rc) return rc;
     if (L->K == 0) return AGN_OK;
-    const uint64_t K = L->K, NE = std::max<uint64_t>(L->n_entries, 1), NT = std::max<uint64_t>(L->n_tokens, 1);
+    // keep bytes are indexed by arena position: the view's n_entries = used
+    const uint64_t K = L->K, NE = std::max<uint64_t>(L->used, 1);
     const uint32_t D = L->D, W = L->W;
-    if (L->n_entries > 0x7fffffffull) return fail(AGN_ENOTSUP, "oplog_prune: log too large for one pass");
+    if (L->used > 0x7fffffffull) return fail(AGN_ENOTSUP, "oplog_prune: log too large for one pass");
     agn_log view;
     fill_view(L, &view);
-    // 1. prune_ops into a compact CSR.
-    Arena c;
-    uint64_t *c_off = nullptr;
-    uint32_t *lens = nullptr;
-    hipError_t e = hipMallocAsync((void **)&c_off, (K + 1) * 8, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&c.oc, NE * D * 8, st);
-    if (e == hipSuccess && L->sparse) e = hipMallocAsync((void **)&c.mask, NE * W * 8, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&c.op_id, NE * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&c.txid, NE * 8, st);
-    if (e == hipSuccess && !L->tags) e = hipMallocAsync((void **)&c.eff, NE * 8, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.tag, NE * 4, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.add, NE * 8, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.rem_off, (NE + 1) * 4, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&c.tok, NT * 8, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&lens, 2 * K * 4, st);
+    // 1. mark pass (prune_ops' VC filter): keep byte per entry, kept entry and
+    //    token counts per key.
+    uint8_t *keep = nullptr;
+    uint64_t *cnts = nullptr;
+    hipError_t e = hipMallocAsync((void **)&keep, NE, st);
+    if (e == hipSuccess) e = hipMallocAsync((void **)&cnts, 2 * K * 8, st);
     auto release = [&]() {
-        for (void *p : {(void *)c_off, (void *)c.oc, (void *)c.mask, (void *)c.op_id, (void *)c.txid,
-                        (void *)c.eff, (void *)c.tag, (void *)c.add, (void *)c.rem_off,
-                        (void *)c.tok, (void *)lens})
-            if (p) (void)hipFreeAsync(p, st);
+        if (keep) (void)hipFreeAsync(keep, st);
+        if (cnts) (void)hipFreeAsync(cnts, st);
     };
     if (e != hipSuccess) {
         release();
-        return fail(AGN_ENOMEM, "oplog_prune: CSR scratch");
+        return fail(AGN_ENOMEM, "oplog_prune: scratch");
     }
-    agn_log out;
-    std::memset(&out, 0, sizeof out);
-    out.key_off = c_off;
-    out.oc = c.oc;
-    out.oc_mask = c.mask;
-    out.op_id = c.op_id;
-    out.txid = c.txid;
-    out.eff = c.eff;
-    out.tag = c.tag;
-    out.add_tok = c.add;
-    out.rem_off = c.rem_off;
-    out.rem_tok = c.tok;
-    rc = launch_prune_ops(view, prune, threshold, threshold_mask, out, out_flags, nullptr, st);
+    rc = launch_prune_mark(view, prune, threshold, threshold_mask, keep, cnts, cnts + K, st);
     if (rc) {
         release();
         return rc;
     }
-    k_csr_lens<<<(unsigned)((K + 255) / 256), 256, 0, st>>>(K, c_off, c.rem_off, lens,
-                                                            lens + K);
-    // 2. read back lengths and which keys were collected.
-    std::vector<uint32_t> nlen(2 * K);
+    // 2. read back the counts and which keys were collected.
+    std::vector<uint64_t> nlen(2 * K);
     std::vector<uint8_t> pr(prune ? K : 0);
-    e = hipMemcpyAsync(nlen.data(), lens, 2 * K * 4, hipMemcpyDeviceToHost, st);
+    e = hipMemcpyAsync(nlen.data(), cnts, 2 * K * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && prune) e = hipMemcpyAsync(pr.data(), prune, K, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         release();
         return fail(AGN_EHIP, "oplog_prune: read back: %s", hipGetErrorString(e));
     }
+    if (!L->tags)
+        for (uint64_t k = 0; k < K; ++k) nlen[K + k] = 0;
     // 3. new segments (resize policy on the collected keys), fresh arena.
-    std::vector<uint64_t> ns(2 * K);
+    std::vector<uint64_t> ns(2 * K), kv(2 * K);  // kv: new key_off | key_len
     uint64_t used = 0, tused = 0, ne = 0, nt = 0;
     for (uint64_t k = 0; k < K; ++k) {
-        const uint32_t l = nlen[k], tl = nlen[K + k];
+        const uint32_t l = (uint32_t)nlen[k], tl = (uint32_t)nlen[K + k];
         if ((!prune || pr[k]) && L->cap[k]) L->cap[k] = resize_list_len(l, L->cap[k]);
         if (L->tags && (!prune || pr[k]) && L->tcap[k])
             L->tcap[k] = std::max<uint32_t>(16u, std::max(tl, std::min(L->tcap[k], 2 * tl)));
         if (L->cap[k] && L->cap[k] < l) L->cap[k] = l;  // never below the kept length
         ns[k] = L->cap[k] ? used : ~0ull;
         ns[K + k] = L->tcap[k] ? tused : 0;
+        kv[k] = L->cap[k] ? used : 0ull;
+        kv[K + k] = L->cap[k] ? l : 0u;
         if (L->cap[k]) used += (uint64_t)L->cap[k] + 1;
         tused += L->tcap[k];
         L->len[k] = L->dlen[k] = l;
@@ -741,10 +684,26 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
         release();
         return fail(AGN_ENOMEM, "oplog_prune: new arena");
     }
-    k_reseg<<<(unsigned)((K + 3) / 4), 256, 0, st>>>(c, b, D, W, K, c_off, d_start,
-                                                    L->tags ? d_start + K : nullptr, L->key_off,
-                                                    L->key_len);
-    e = hipGetLastError();
+    // 4. scatter the kept entries straight into their new segments, then the
+    //    new key_off / key_len (the old view is read by the scatter first).
+    agn_log out;
+    std::memset(&out, 0, sizeof out);
+    out.key_off = d_start;
+    out.oc = b.oc;
+    out.oc_mask = b.mask;
+    out.op_id = b.op_id;
+    out.txid = b.txid;
+    out.eff = b.eff;
+    out.tag = b.tag;
+    out.add_tok = b.add;
+    out.rem_off = b.rem_off;
+    out.rem_tok = b.tok;
+    rc = launch_prune_scatter_seg(view, out, prune, keep, d_start + K, out_flags, st);
+    if (rc) e = hipErrorLaunchFailure;
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(L->key_off, kv.data(), K * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(L->key_len, kv.data() + K, K * 8, hipMemcpyHostToDevice, st);
     // pruning leaves id gaps: rebuild the consecutive-id index of every key
     if (e == hipSuccess) {
         agn_log nv;
@@ -757,7 +716,7 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(L->id0.data(), L->key_id0, K * 4, hipMemcpyDeviceToHost, st);
-    // ns must outlive the async H2D above.
+    // ns and kv must outlive the async H2D copies above.
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFreeAsync(d_start, st);
     release();

@@ -1,0 +1,62 @@
+"""Times agn_oplog_prune (engine-owned op log GC) on a synthetic counter log:
+K keys x N ops, D = 8 dense clocks increasing along each key's log, threshold
+per key = the clock of a random position, so the ops up to it are pruned.
+AGN_LIB selects the library (A/B against tools/libagn_prev.so).
+
+  python scripts/bench_oplog_prune.py [K] [N] [reps]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from antidote_amd import _abi  # noqa: E402
+from antidote_amd.engine import Engine, OpLog  # noqa: E402
+
+
+def main():
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 500_000
+    N = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    D = 8
+    rng = np.random.default_rng(7)
+    keys = np.repeat(np.arange(K, dtype=np.uint64), N)           # appended key-major
+    pos = np.tile(np.arange(N, dtype=np.uint64), K)
+    oc = (np.uint64(1_700_000_000_000_000) + pos[:, None] * np.uint64(1000)
+          + rng.integers(0, 500, (K * N, D), dtype=np.uint64))
+    eff = rng.integers(-1000, 1001, K * N, dtype=np.int64)
+    txid = np.zeros(K * N, np.uint64)
+    cut = rng.integers(0, N, K)
+    thr = oc.reshape(K, N, D)[np.arange(K), cut].copy()          # covers ops <= cut (mostly)
+    prune = np.ones(K, np.uint8)
+    eng = Engine(0)
+    bp, bt = eng.upload(prune), eng.upload(thr)
+    fl = eng.empty(4 * K)
+    times = []
+    for r in range(reps):
+        with OpLog(eng, _abi.COUNTER_PN, D, K, init_slots=N + 8) as ol:
+            ol.append(keys, oc, txid=txid, eff=eff)
+            ol.flush()
+            eng.sync()
+            t0 = time.perf_counter()
+            ol.prune(bp.ptr, bt.ptr, None, fl.ptr)
+            eng.sync()
+            times.append((time.perf_counter() - t0) * 1e3)
+            st = ol.stats()
+    kept = st["entries"]
+    ms = float(np.median(times))
+    # bytes the GC must move at least: read every row + effect + id + txid,
+    # write the kept ones
+    per = 8 * D + 8 + 4 + 8
+    alg = K * N * per + kept * per
+    print(json.dumps({"lib": os.path.basename(os.environ.get("AGN_LIB", "libantidote_gpu.so")),
+                      "keys": K, "ops_per_key": N, "n_dcs": D, "kept": int(kept),
+                      "ms_median": ms, "ms_all": times, "min_bytes": alg,
+                      "GBps_min_bytes": alg / ms / 1e6}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
