@@ -631,10 +631,16 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
         release();
         return rc;
     }
-    // 2. read back the counts and which keys were collected.
-    std::vector<uint64_t> nlen(2 * K);
+    // 2. read back the counts and which keys were collected.  Host staging
+    //    in the log's pinned buffer: counts | new starts | new key_off, len.
+    rc = ensure_pinned(L, 6 * K * 8);
+    if (rc) {
+        release();
+        return rc;
+    }
+    uint64_t *nlen = (uint64_t *)L->pinned, *ns = nlen + 2 * K, *kv = ns + 2 * K;
     std::vector<uint8_t> pr(prune ? K : 0);
-    e = hipMemcpyAsync(nlen.data(), cnts, 2 * K * 8, hipMemcpyDeviceToHost, st);
+    e = hipMemcpyAsync(nlen, cnts, 2 * K * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && prune) e = hipMemcpyAsync(pr.data(), prune, K, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
@@ -644,7 +650,6 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     if (!L->tags)
         for (uint64_t k = 0; k < K; ++k) nlen[K + k] = 0;
     // 3. new segments (resize policy on the collected keys), fresh arena.
-    std::vector<uint64_t> ns(2 * K), kv(2 * K);  // kv: new key_off | key_len
     uint64_t used = 0, tused = 0, ne = 0, nt = 0;
     for (uint64_t k = 0; k < K; ++k) {
         const uint32_t l = (uint32_t)nlen[k], tl = (uint32_t)nlen[K + k];
@@ -664,7 +669,7 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
         nt += tl;
     }
     for (uint64_t k = 0; k < K; ++k) L->start[k] = L->cap[k] ? ns[k] : 0;
-    L->tstart.assign(ns.begin() + K, ns.end());
+    L->tstart.assign(ns + K, ns + 2 * K);
     Arena b;
     uint64_t *d_start = nullptr;
     const uint64_t U = std::max<uint64_t>(used, 1), TU = std::max<uint64_t>(tused, 1);
@@ -679,7 +684,7 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.rem_off, U * 4, st);
     if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.tok, TU * 8, st);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(d_start, ns.data(), 2 * K * 8, hipMemcpyHostToDevice, st);
+        e = hipMemcpyAsync(d_start, ns, 2 * K * 8, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) {
         release();
         return fail(AGN_ENOMEM, "oplog_prune: new arena");
@@ -701,9 +706,9 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     rc = launch_prune_scatter_seg(view, out, prune, keep, d_start + K, out_flags, st);
     if (rc) e = hipErrorLaunchFailure;
     if (e == hipSuccess)
-        e = hipMemcpyAsync(L->key_off, kv.data(), K * 8, hipMemcpyHostToDevice, st);
+        e = hipMemcpyAsync(L->key_off, kv, K * 8, hipMemcpyHostToDevice, st);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(L->key_len, kv.data() + K, K * 8, hipMemcpyHostToDevice, st);
+        e = hipMemcpyAsync(L->key_len, kv + K, K * 8, hipMemcpyHostToDevice, st);
     // pruning leaves id gaps: rebuild the consecutive-id index of every key
     if (e == hipSuccess) {
         agn_log nv;
@@ -716,7 +721,7 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(L->id0.data(), L->key_id0, K * 4, hipMemcpyDeviceToHost, st);
-    // ns and kv must outlive the async H2D copies above.
+    // the pinned staging (ns, kv) must not be reused before the copies land
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFreeAsync(d_start, st);
     release();
