@@ -119,6 +119,21 @@ int agn_open(int device, agn_ctx **out) {
     AGN_HIP(hipGetDeviceProperties(&p, device));
     if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
         return fail(AGN_ENOTSUP, "built for gfx950, device is %s", p.gcnArchName);
+    // Stream-ordered scratch (prune, ingest, op-log arenas) comes from the
+    // device's default pool; keep freed blocks cached in it instead of
+    // unmapping them at every synchronize (release threshold 0), so GC and
+    // ingest calls do not remap gigabytes each time.  AGN_POOL_KEEP=0 (A/B
+    // knob) leaves the default.
+    {
+        const char *v = getenv("AGN_POOL_KEEP");
+        if (!(v && v[0] == '0')) {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+                uint64_t keep = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            }
+        }
+    }
     agn_ctx *c = new (std::nothrow) agn_ctx;
     if (!c) return fail(AGN_ENOMEM, "ctx");
     c->device = device;
