@@ -1,0 +1,55 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-experiment wrappers).
+#
+#   gpurun --timeout T -- bash scripts/gpu.sh 'name|seconds|command' ['name|seconds|command' ...]
+#
+# Each step runs from the repo root under its own `timeout -k 10 seconds`,
+# with stdout+stderr in gpurun_out/<name>.log; the first failing step ends
+# the script (no further GPU work after a fault, abort or time limit) and
+# prints the tail of its log.  Recipes used every round:
+#
+#   roundend  : the driver's tiers -- pytest -m gpu, smoke(), default bench
+#   trace     : rocprofv3 --kernel-trace --stats of the driver's exact bench
+#               command (profiles/rNN/kernel_stats_*.csv)
+#   pmc       : FETCH_SIZE / WRITE_SIZE passes (one counter block per run)
+#
+#   bash scripts/gpu.sh roundend        # expands to the three driver steps
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+: > gpurun_out/steps.txt
+
+run_step() {
+  local name=$1 t=$2 cmd=$3
+  echo "[$(date +%T)] $name: $cmd" | tee -a gpurun_out/steps.txt
+  timeout -k 10 "$t" bash -c "exec $cmd" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" | tee -a gpurun_out/steps.txt
+  if [ $rc -ne 0 ]; then
+    echo "stopping after $name (rc=$rc)"
+    tail -40 "gpurun_out/$name.log"
+    exit $rc
+  fi
+  tail -n 2 "gpurun_out/$name.log"
+}
+
+expand() {
+  case "$1" in
+    roundend)
+      echo "pytest_gpu|900|python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread"
+      echo "smoke|200|python -u -c 'import __graft_entry__ as g; g.smoke()'"
+      echo "bench|400|python -u bench.py";;
+    trace)
+      echo "trace|400|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5";;
+    *) echo "$1";;
+  esac
+}
+
+for spec in "$@"; do
+  while IFS= read -r line; do
+    [ -z "$line" ] && continue
+    IFS='|' read -r name t cmd <<< "$line"
+    run_step "$name" "$t" "$cmd"
+  done < <(expand "$spec")
+done
+echo "all steps ok"

@@ -260,6 +260,110 @@ add(kind="system_seq", name="object_log_state_test", src="test/singledc/object_l
     expect_state_tokens_per_elem=1)
 
 
+# --------------------------------------------------------------------------
+# System tests with a multi-DC / multi-key / multi-update transaction history
+# (kind "system_txn"; tests/kat_util.py system_txn_log gives the clock model).
+# A txn is {"dc", "dep": [txn indices] (the causal dependency clock passed to
+# update_*: the max of their commit times; [] = ignore), "updates", "key"}; a
+# read is {"key", "at": [txn indices] (read clock = max of their commit
+# times), "expect": the value the reference asserts}.
+def tx(dc, updates, dep=(), key="k"):
+    return {"dc": dc, "dep": list(dep), "updates": updates, "key": key}
+
+
+def rd_at(at, expect, key="k"):
+    return {"key": key, "at": list(at), "expect": expect}
+
+
+INC = [["increment", 1]]
+
+# inter_dc_repl_SUITE causality_test: add first, add second in DC1, remove
+# first in DC2 (each depending on the previous commit) -> [second]
+add(kind="system_txn", name="inter_dc_repl causality_test set_aw",
+    src="test/multidc/inter_dc_repl_SUITE.erl:122-139", type="set_aw",
+    txns=[tx("dc1", [["add", "first"]]), tx("dc1", [["add", "second"]], [0]),
+          tx("dc2", [["remove", "first"]], [1])],
+    reads=[rd_at([2], ["second"])])
+# inter_dc_repl_SUITE simple_replication_test: 3 increments in DC1, read on DC1
+# and DC2 at the last commit time -> 3
+add(kind="system_txn", name="inter_dc_repl simple_replication_test",
+    src="test/multidc/inter_dc_repl_SUITE.erl:87-100", type="counter_pn",
+    txns=[tx("dc1", INC) for _ in range(3)], reads=[rd_at([2], 3)])
+# inter_dc_repl_SUITE multiple_keys_test: 10 rounds of one increment on each of
+# 10 keys, one more increment on the base key; every derived key reads 10
+txns = [tx("dc1", INC, key=f"mk{n}") for _ in range(10) for n in range(1, 11)]
+txns.append(tx("dc1", INC, key="multiple_keys_test"))
+add(kind="system_txn", name="inter_dc_repl multiple_keys_test",
+    src="test/multidc/inter_dc_repl_SUITE.erl:103-118,187-206", type="counter_pn",
+    txns=txns, reads=[rd_at([len(txns) - 1], 10, key=f"mk{n}") for n in range(1, 11)])
+# multiple_dcs_SUITE simple_replication_test: 3 in DC1 -> 3; +1 in DC2 after
+# CommitTime, +1 in DC3 after CommitTime2 -> 5 on every DC
+add(kind="system_txn", name="multiple_dcs simple_replication_test",
+    src="test/multidc/multiple_dcs_SUITE.erl:89-117", type="counter_pn",
+    txns=[tx("dc1", INC), tx("dc1", INC), tx("dc1", INC), tx("dc2", INC, [2]),
+          tx("dc3", INC, [3])],
+    reads=[rd_at([2], 3), rd_at([4], 5)])
+# multiple_dcs_SUITE parallel_writes_test: 5 increments on each of 3 DCs
+# concurrently (no dependency), read at the merged max of the 3 commit times -> 15
+txns = [tx(f"dc{d}", INC) for _ in range(5) for d in (1, 2, 3)]
+add(kind="system_txn", name="multiple_dcs parallel_writes_test",
+    src="test/multidc/multiple_dcs_SUITE.erl:120-165", type="counter_pn",
+    txns=txns, reads=[rd_at([12, 13, 14], 15)])
+# multiple_dcs_SUITE blocking_test: +1 in DC1, +1 in DC2, read at
+# vectorclock:max of both commit times -> 2
+add(kind="system_txn", name="multiple_dcs blocking_test",
+    src="test/multidc/multiple_dcs_SUITE.erl:212-240", type="counter_pn",
+    txns=[tx("dc1", INC), tx("dc2", INC)], reads=[rd_at([0, 1], 2)])
+# multiple_dcs_SUITE replicated_set_test: 100 adds on DC1 -> lists:seq(1, 100)
+# (more than one 64-entry chunk of the tag kernel)
+add(kind="system_txn", name="multiple_dcs replicated_set_test",
+    src="test/multidc/multiple_dcs_SUITE.erl:243-266", type="set_aw",
+    txns=[tx("dc1", [["add", n]]) for n in range(1, 101)],
+    reads=[rd_at([99], list(range(1, 101)))])
+# pb_client_SUITE (antidotec PB client; one single-DC transaction per commit)
+add(kind="system_txn", name="pb_client pb_test_set_read_write",
+    src="test/singledc/pb_client_SUITE.erl:186-202", type="set_aw",
+    txns=[tx("dc1", [["add", "a"]])], reads=[rd_at([0], ["a"])])
+add(kind="system_txn", name="pb_client update_set_read_test add_all",
+    src="test/singledc/pb_client_SUITE.erl:259-282", type="set_aw",
+    txns=[tx("dc1", [["add_all", ["a", "b"]]])], reads=[rd_at([0], ["a", "b"])])
+add(kind="system_txn", name="pb_client static_transaction_test add_all",
+    src="test/singledc/pb_client_SUITE.erl:491-517", type="set_aw",
+    txns=[tx("dc1", [["add_all", ["a", "b"]]])], reads=[rd_at([0], ["a", "b"])])
+add(kind="system_txn", name="pb_client crdt_mvreg_test",
+    src="test/singledc/pb_client_SUITE.erl:305-321", type="register_mv",
+    txns=[tx("dc1", [["assign", "a"]])], reads=[rd_at([0], ["a"])])
+add(kind="system_txn", name="pb_client update_counter_crdt_and_read_test",
+    src="test/singledc/pb_client_SUITE.erl:237-256", type="counter_pn",
+    txns=[tx("dc1", [["increment", 15]])], reads=[rd_at([0], 15)])
+# CRDTs embedded in the map tests: the map's entry value is the embedded
+# CRDT's own value
+add(kind="system_txn", name="pb_client crdt_gmap_test embedded set_aw add_all",
+    src="test/singledc/pb_client_SUITE.erl:359,379", type="set_aw",
+    txns=[tx("dc1", [["add_all", ["Apple", "Banana"]]])],
+    reads=[rd_at([0], ["Apple", "Banana"])])
+add(kind="system_txn", name="pb_client crdt_gmap_test embedded register_mv",
+    src="test/singledc/pb_client_SUITE.erl:354,358,376,378", type="register_mv",
+    txns=[tx("dc1", [["assign", "42"]], key="a"), tx("dc1", [["assign", "Paul"]], key="c")],
+    reads=[rd_at([0], ["42"], key="a"), rd_at([1], ["Paul"], key="c")])
+# crdt_map_rr_test: one transaction assigns b1..b5, then removes them through
+# the map (map_rr remove = reset of the embedded register_mv); the asserted map
+# holds no b1..b5 entry (map_rr hides bottom = empty registers), keeps b = [X]
+# and i = [X], and d / e (set_aw add_all) = [Apple, Banana]
+add(kind="system_txn", name="pb_client crdt_map_rr_test embedded register_mv reset",
+    src="test/singledc/pb_client_SUITE.erl:401-458", type="register_mv",
+    txns=[tx("dc1", [["assign", "X1"], ["reset", None]], key="b1"),
+          tx("dc1", [["assign", "X4"], ["reset", None]], key="b4"),
+          tx("dc1", [["assign", "X"]], key="b"), tx("dc1", [["assign", "X"]], key="i")],
+    reads=[rd_at([0], [], key="b1"), rd_at([1], [], key="b4"), rd_at([2], ["X"], key="b"),
+           rd_at([3], ["X"], key="i")])
+add(kind="system_txn", name="pb_client crdt_map_rr_test embedded set_aw add_all",
+    src="test/singledc/pb_client_SUITE.erl:413-414,452-453", type="set_aw",
+    txns=[tx("dc1", [["add_all", ["Apple", "Banana"]]], key="d"),
+          tx("dc1", [["add_all", ["Apple", "Banana"]]], key="e")],
+    reads=[rd_at([0], ["Apple", "Banana"], key="d"), rd_at([1], ["Apple", "Banana"], key="e")])
+
+
 if __name__ == "__main__":
     with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump({"reference": "anshulahuja98/antidote @ 2025-01-12", "cases": CASES}, f,

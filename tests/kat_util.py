@@ -135,12 +135,21 @@ class Downstream:
 
     def effect(self, state, upd):
         op, arg = upd
+        if self.typ == po.COUNTER_PN:
+            # antidote_crdt_counter_pn downstream: increment N -> N, decrement N -> -N
+            return {"increment": arg, "decrement": -arg}[op]
         if self.typ == po.SET_AW:
-            cur = dict(state).get(arg, [])
-            if op == "add":
-                return [(arg, [self.token()], list(cur))]
-            return [(arg, [], list(cur))]
+            # add / remove carry one element, add_all / remove_all a list; the
+            # effect is one {Elem, AddTokens, ObservedTokens} part per distinct
+            # element, sorted by element
+            elems = sorted(set(arg)) if op in ("add_all", "remove_all") else [arg]
+            cur = dict(state)
+            adding = op in ("add", "add_all")
+            return [(e, [self.token()] if adding else [], list(cur.get(e, [])))
+                    for e in elems]
         if self.typ == po.REGISTER_MV:
+            if op == "reset":   # map_rr remove of an embedded register_mv
+                return ("reset", [t for _, t in state])
             return (arg, self.token(), [t for _, t in state])
         raise ValueError(op)
 
@@ -159,3 +168,46 @@ def system_seq_log(case):
         ops.insert(0, (i + 1, p))
         reads.append({"dc1": 10 * (i + 1)})
     return ops, reads, state
+
+
+def system_txn_log(case):
+    """Multi-DC transaction history of a system_txn KAT -> per-key op logs
+    (newest-first, like #snapshot_get_response.ops_list) and the reads.
+
+    Clock model (Clock-SI, SURVEY.md §3 call stacks 2/3): transaction i runs at
+    its DC x with snapshot ss = max(commit VCs of its dependencies) with
+    ss[x] = "now" = 10(i+1) - 5 (so it sees every earlier local commit), and
+    commits at (x, 10(i+1)); its commit VC is ss with x := 10(i+1).  All its
+    updates share the txid and commit time, and each update's effect observes
+    the state left by the transaction's earlier updates (read-your-writes of
+    the interactive coordinator).  A read "at" a list of transactions uses
+    the max of their commit VCs, i.e. check_read_key(..., CommitTime, static)."""
+    typ = TYPES[case["type"]]
+    ds = Downstream(typ)
+    states, logs, commit_vc = {}, {}, []
+    for i, tx in enumerate(case["txns"]):
+        x = tx["dc"]
+        ss = po.vc_max([commit_vc[j] for j in tx.get("dep") or []])
+        ss[x] = max(ss.get(x, 0), 10 * (i + 1) - 5)
+        key = tx.get("key", "k")
+        # the transaction's snapshot of the key: every earlier effect whose
+        # commit VC is covered by ss (the materializer's own rule, done on dicts)
+        st = po.crdt_new(typ)
+        for _, p in reversed(logs.get(key, [])):
+            oc = dict(p.snapshot_time)
+            oc[p.commit_time[0]] = p.commit_time[1]
+            if all(d in ss and t <= ss[d] for d, t in oc.items()):
+                st = po.crdt_update(typ, p.op_param, st)
+        for upd in tx["updates"]:
+            eff = ds.effect(st, upd)
+            st = po.crdt_update(typ, eff, st)
+            lg = logs.setdefault(key, [])
+            lg.insert(0, (len(lg) + 1, po.Payload(key, typ, eff, dict(ss), (x, 10 * (i + 1)),
+                                                  i + 1)))
+        cvc = dict(ss)
+        cvc[x] = 10 * (i + 1)
+        commit_vc.append(cvc)
+    reads = []
+    for r in case["reads"]:
+        reads.append((r.get("key", "k"), po.vc_max([commit_vc[j] for j in r["at"]]), r["expect"]))
+    return logs, reads

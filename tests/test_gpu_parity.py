@@ -50,6 +50,22 @@ def test_kat_system_seq_gpu(eng, c):
         want = po.materialize(typ, po.IGNORE, reads[i], po.SnapshotGetResponse(
             ops, len(ops), po.MaterializedSnapshot(0, po.crdt_new(typ)), po.IGNORE, True))
         assert g == want
+        exp = c["expect_after"]
+        want_v = exp[i] if isinstance(exp, list) else exp.get(str(i + 1))
+        if want_v is not None:
+            assert po.crdt_value(typ, g[1]) == want_v
+
+
+TXN = kats({"system_txn"})
+
+
+@pytest.mark.parametrize("c", TXN, ids=[c["name"] for c in TXN])
+def test_kat_system_txn_gpu(eng, oracle_lib, c):
+    """Multi-DC / multi-key / multi-update transaction KATs (inter_dc_repl,
+    multiple_dcs and pb_client suites) through the HIP path: the asserted
+    value and the full materialize/4 tuple of the dict restatement."""
+    from test_oracle_kats import system_txn_check
+    system_txn_check(c, gpu_fn(eng))
 
 
 # ------------------------------------------------------------------ randomised differential
@@ -340,6 +356,33 @@ def test_full_size_sampled_parity(eng, oracle_lib, spec):
                 assert n == int(w.out_n[0])
                 assert np.array_equal(full.out_tag[o:o + n], w.out_tag[:n])
                 assert np.array_equal(full.out_tok[o:o + n], w.out_tok[:n])
+    finally:
+        eng.free_gen(dl, dr)
+        for b in res.bufs.values():
+            b.free()
+
+
+CFG1 = dict(crdt_type=1, n_dcs=3, n_keys=10_000, ops_per_key=100, n_elems=0, seed=20250112)
+
+
+@pytest.mark.parametrize("warm", [0, 1], ids=["cold", "warm"])
+def test_cfg1_all_keys_parity(eng, oracle_lib, warm):
+    """BASELINE cfg1 (the reference's CPU-runnable case: counter_pn, 10k keys x
+    100 ops, 3-DC clocks): every key generated on the device and materialized
+    by the HIP path, bit-exact against the oracle on the host-generated log."""
+    cfg = _abi.AgnGenCfg(**{"key_base": 0, "key_stride": 1, **CFG1, "warm": warm})
+    dl, dr, res = _run_dev(eng, cfg)
+    try:
+        got = eng.fetch_result(res)
+        hl, hr = gen_host(cfg)
+        want = alloc_result(cfg.n_keys, cfg.n_dcs, sparse=False)
+        assert oracle_lib.oracle_materialize(C.byref(hl), C.byref(hr),
+                                             C.byref(result_struct(want)), 4) == 0
+        free_gen_host(hl, hr)
+        bad = compare(1, cfg.n_dcs, got, want, False, cfg.n_keys)
+        assert not bad, bad[:10]
+        inc = want.count.mean() / cfg.ops_per_key
+        assert 0.2 < inc < 0.8, inc
     finally:
         eng.free_gen(dl, dr)
         for b in res.bufs.values():

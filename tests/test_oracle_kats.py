@@ -7,7 +7,8 @@ import numpy as np
 import pytest
 
 from antidote_amd import _abi
-from kat_util import (TYPES, OneKeyRun, kats, oracle_fn, py_ops, system_seq_log, to_payload,
+from kat_util import (TYPES, OneKeyRun, kats, oracle_fn, py_ops, system_seq_log, system_txn_log,
+                      to_payload,
                       to_vc)
 from oracle import py_oracle as po
 
@@ -272,3 +273,30 @@ def test_system_seq(oracle_lib, c):
         _, res = run.run(oracle_fn(oracle_lib))
         cr = run.decode(res, 0)
         assert cr == r
+
+
+TXN = kats({"system_txn"})
+
+
+def system_txn_check(c, materialize_fn):
+    """Every read of a system_txn KAT: the dict restatement must give the
+    value the reference asserts, and the SoA path through materialize_fn (C
+    oracle or HIP engine) must give the restatement's full result tuple."""
+    typ = TYPES[c["type"]]
+    logs, reads = system_txn_log(c)
+    n_dcs = len({t["dc"] for t in c["txns"]})
+    for key, R, want in reads:
+        ops = logs.get(key, [])
+        r = po.materialize(typ, po.IGNORE, R, _resp(ops, po.IGNORE, [0, po.crdt_new(typ)]))
+        assert r[0] == "ok" and po.crdt_value(typ, r[1]) == want, (key, r)
+        run = OneKeyRun(c["type"], ops, n_dcs)
+        run.add_read(R)
+        _, res = run.run(materialize_fn)
+        got = run.decode(res, 0)
+        assert got == r, (key, got, r)
+        assert po.crdt_value(typ, got[1]) == want
+
+
+@pytest.mark.parametrize("c", TXN, ids=[c["name"] for c in TXN])
+def test_system_txn(oracle_lib, c):
+    system_txn_check(c, oracle_fn(oracle_lib))
