@@ -35,13 +35,16 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 CONFIGS = {
-    2: dict(name="cfg2 counter_pn materialize: 10M keys x 64 ops/key, 8-DC clocks, "
+    1: dict(name="cfg1 counter_pn materialize: {keys} keys x 100 ops/key, 3-DC clocks, random "
+                 "snapshot VCs (the reference's CPU-runnable case)", crdt_type=1, n_dcs=3,
+            n_keys=10_000, ops_per_key=100, n_elems=0, seed=20250112 + 0),
+    2: dict(name="cfg2 counter_pn materialize: {keys} keys x 64 ops/key, 8-DC clocks, "
                  "random snapshot VCs", crdt_type=1, n_dcs=8, n_keys=10_000_000,
             ops_per_key=64, n_elems=0, seed=20250112 + 1),
-    3: dict(name="cfg3 set_aw materialize: 1M keys x 256 add/remove ops, 16-DC clocks, "
+    3: dict(name="cfg3 set_aw materialize: {keys} keys x 256 add/remove ops, 16-DC clocks, "
                  "32 elems/key, order-aware tag resolution", crdt_type=2, n_dcs=16,
             n_keys=1_000_000, ops_per_key=256, n_elems=32, seed=20250112 + 2),
-    4: dict(name="cfg4 register_mv materialize: 1M keys x 100 ops (100M ops total over G GPUs), "
+    4: dict(name="cfg4 register_mv materialize: {keys} keys x 100 ops on this GPU (100M ops total over G GPUs), "
                  "64-DC clocks, concurrent-write pruning", crdt_type=3, n_dcs=64,
             n_keys=1_000_000, ops_per_key=100, n_elems=16, seed=20250112 + 3, strong=True),
 }
@@ -59,7 +62,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="extra multi-thread CPU run")
     ap.add_argument("--tune-rounds", type=int, default=3,
                     help="agn_tune launches per kernel variant before timing (0 = no tuning)")
-    ap.add_argument("--gst", action="store_true", help="also time a GST epoch + RCCL min-allreduce")
+    ap.add_argument("--gst", action="store_true",
+                    help="also time a GST epoch + RCCL min-allreduce (always on for N > 1)")
+    ap.add_argument("--post-gc", action="store_true",
+                    help="also time materialize of a pruned log (op ids with gaps, so the "
+                         "NewLastOp id comes from the op_id array instead of key_id0)")
     ap.add_argument("--warm", action="store_true",
                     help="also time the warm read path through the device snapshot cache "
                          "(agn_ss_lookup -> agn_materialize -> agn_ss_store)")
@@ -72,6 +79,49 @@ def parse():
                     help="also time the host-staged read path (keys + R from pinned host "
                          "memory, results back to pinned host memory; PCIe-inclusive)")
     return ap.parse_args()
+
+
+def fmt_keys(n):
+    for div, suf in ((1_000_000, "M"), (1_000, "k")):
+        if n >= div:
+            return f"{n / div:g}{suf}"
+    return str(n)
+
+
+def kernel_src_sha16():
+    """Hash of every source the device code is built from; a PMC traffic file
+    (profiles/pmc/*.json, scripts/pmc_traffic.py) is only used when it was
+    measured on a build of exactly these sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "antidote_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "antidote_amd", "csrc", "*.hpp")) +
+                   [os.path.join(ROOT, "include", "antidote_gpu.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def r_jitter(D):
+    """The read-clock jitter of the generator (antidote_amd/csrc/gen.hpp):
+    R[d] = max(oc of the ops before the cut) + U[0,4000] - J."""
+    J = 16000 // D if D >= 8 else 2000
+    return f"U[{-J},{4000 - J}]"
+
+
+def algorithmic_bytes_survey(cfg, n_keys, n_rem=0, n_live=0):
+    """SURVEY.md §8(d)'s byte formula, reported beside the kernel's own
+    count: counter_pn per op 8D + 12 (OpSSCommit row, effect, u32 op_id), per
+    key 32 + 16D; set_aw / register_mv per op 8D + 20 + 8 per removed token,
+    12 per live output pair, per key 32 + 16D."""
+    D, N = cfg["n_dcs"], cfg["ops_per_key"]
+    ops = n_keys * N
+    if cfg["crdt_type"] == 1:
+        return ops * (8 * D + 12) + n_keys * (32 + 16 * D)
+    return ops * (8 * D + 20) + 8 * n_rem + 12 * n_live + n_keys * (32 + 16 * D)
 
 
 def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0):
@@ -227,6 +277,7 @@ def main():
     ops_step = n_keys * cfg["ops_per_key"] * world
     value = ops_step * a.steps / elapsed
     bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live)
+    bytes_survey = algorithmic_bytes_survey(cfg, n_keys, n_rem, n_live)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
     probe = probe_read_gbs(eng, dl, n_keys * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
@@ -236,9 +287,12 @@ def main():
     ingest = ingest_bench(eng, cfg, sp, torch) if a.ingest else None
     e2e = e2e_bench(eng, dl, dr, res, cfg, n_keys, torch) if a.e2e else None
 
+    # N > 1: the GST epoch (local min -> RCCL min-allreduce -> finalize) always
+    # runs, untimed by the headline, so the scaling run exercises the collective
     gst = None
-    if a.gst:
-        gst = gst_bench(eng, torch, dist, world, rank, sp)
+    if a.gst or world > 1:
+        gst = gst_bench(eng, torch, dist, world, rank, sp, backend)
+    post_gc = post_gc_bench(eng, cfg, n_keys, rank, world, sp, torch, a.steps) if a.post_gc else None
 
     if rank == 0:
         cpu = None
@@ -254,13 +308,24 @@ def main():
                              f"{secs[1]:.1f} s of CPU time",
                    "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_cfg{a.config}.json")
+        traffic, traffic_src = None, None
+        sha = kernel_src_sha16()
+        pmc = os.path.join(ROOT, "profiles", "pmc", f"cfg{a.config}.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 p = json.load(f)
-            if p.get("n_keys") == n_keys:
+            if p.get("n_keys") == n_keys and p.get("kernel_src_sha16") == sha:
                 traffic = p.get("hbm_bytes_per_launch")
+                traffic_src = (f"profiles/pmc/cfg{a.config}.json: rocprofv3 FETCH_SIZE x2 + "
+                               f"WRITE_SIZE passes of {p.get('kernel')} on this kernel build "
+                               f"(sources sha {sha}), measured {p.get('measured', '?')}")
+            else:
+                traffic_src = (f"null: profiles/pmc/cfg{a.config}.json was measured on "
+                               f"sources {p.get('kernel_src_sha16')} / {p.get('n_keys')} keys, "
+                               f"this build is {sha} / {n_keys} keys")
+        else:
+            traffic_src = f"null: no PMC pass for cfg{a.config} (profiles/pmc/)"
+        workload = cfg["name"].format(keys=fmt_keys(n_keys))
         line = {
             "metric": "materialized ops/sec + VC compares/sec (1/2/4/8 GPU), % of HBM roofline",
             "value": value, "unit": "ops/s", "n_gpus": world, "steps": a.steps,
@@ -269,13 +334,19 @@ def main():
             "vs_baseline": None, "dtype": "u64",
             "data": "synthetic (device SplitMix64 generator, BASELINE.md §3)",
             "vc_compares_per_s": value,  # SCT = ignore: one D-wide compare per op
-            "config": {"workload": cfg["name"], "keys_per_gpu": n_keys,
+            "config": {"workload": workload, "keys_per_gpu": n_keys,
+                       "keys_total": n_keys * world,
                        "ops_per_key": cfg["ops_per_key"], "n_dcs": cfg["n_dcs"],
+                       "r_jitter": r_jitter(cfg["n_dcs"]),
                        "partitioning": "vnode p = key mod 64, gpu = p mod G; no collective",
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch,
+                         "algorithmic_bytes_survey": bytes_survey,
+                         "frac_survey_bytes": bytes_survey / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "kernel_src_sha16": sha,
                          "probe_read_GBps": probe,
                          "frac_of_probe": achieved / probe if probe else None},
             "cpu_baseline": cpu,
@@ -285,6 +356,8 @@ def main():
         }
         if gst:
             line["gst"] = gst
+        if post_gc:
+            line["post_gc"] = post_gc
         if gc:
             line["gc"] = gc
         if warm:
@@ -567,6 +640,80 @@ def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
             "frac": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def post_gc_bench(eng, cfg, n_keys, rank, world, sp, torch, steps):
+    """materialize/4 after a GC: the warm-generator log (each key has a base
+    snapshot SCT covering a random prefix of its ops) is pruned with SCT as
+    the threshold (prune_ops keeps the ops not covered by it, so op ids keep
+    gaps), re-indexed (agn_log_index_ids: keys whose kept ids are no longer
+    consecutive get AGN_ID0_NONE and the counter kernel loads the NewLastOp id
+    from op_id), then read warm (SCT, base) like the unpruned log.  Reports
+    both, timed alternately in this process."""
+    from antidote_amd import _abi
+    from antidote_amd.engine import DeviceArrays
+    D, N = cfg["n_dcs"], cfg["ops_per_key"]
+    g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=D, n_keys=n_keys, ops_per_key=N,
+                       n_elems=cfg["n_elems"], seed=cfg["seed"], key_base=rank,
+                       key_stride=world, warm=1)
+    wl, wr = eng.gen_dev(g, sp)
+    E = n_keys * N
+    s = _abi.AgnLog()
+    s.crdt_type, s.n_dcs, s.n_keys, s.n_entries = cfg["crdt_type"], D, n_keys, E
+    out = DeviceArrays(s)
+    spec = {"key_off": 8 * (n_keys + 1), "oc": 8 * E * D, "op_id": 4 * E}
+    if cfg["crdt_type"] == 1:
+        spec["eff"] = 8 * E
+    else:
+        n_rem = int(eng.download(type("B", (), {"ptr": wl.rem_off})(), np.uint32, (E + 1,))[-1])
+        spec.update({"tag": 4 * E, "add_tok": 8 * E, "rem_off": 4 * (E + 1),
+                     "rem_tok": 8 * max(n_rem, 1)})
+    for name, nb in spec.items():
+        out.bufs[name] = eng.empty(nb)
+        setattr(s, name, out.bufs[name].ptr)
+    tot = eng.empty(16)
+    eng.prune_ops(DeviceArrays(wl), None, wr.sct, None, out, None, tot.ptr, sp)
+    idx = eng.index_ids(out, sp)
+    kept = int(eng.download(tot, np.uint64, (2,), stream=sp)[0])
+    none_frac = float((eng.download(idx, np.uint32, (n_keys,), stream=sp) ==
+                       _abi.ID0_NONE).mean())
+    cap = (np.arange(n_keys + 1, dtype=np.uint64) * np.uint64(N)
+           if cfg["crdt_type"] != 1 else None)
+    res = eng.alloc_result(n_keys, D, sparse=False, cap_off=cap)
+    # post_gc_no_index: the same pruned log without agn_log.key_id0, i.e. every
+    # key takes the dependent op_id load of the NewLastOp position
+    noidx = _abi.AgnLog()
+    C.memmove(C.addressof(noidx), C.addressof(out.struct), C.sizeof(_abi.AgnLog))
+    noidx.key_id0 = None
+    logs = {"unpruned": wl, "post_gc": out.struct, "post_gc_no_index": noidx}
+    for lg in logs.values():
+        eng.materialize(lg, wr, res, sp)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ms = {k: 0.0 for k in logs}
+    for _ in range(steps):
+        for k, lg in logs.items():
+            b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            b.record(stream)
+            eng.materialize(lg, wr, res, sp)
+            e.record(stream)
+            e.synchronize()
+            ms[k] += b.elapsed_time(e) / steps
+    per_key = 8 + 8 * D + 8 * D + 8 * D + 32 + 8   # + SCT row and base value (warm)
+    per_op = 8 * D + 8
+    byts = {"unpruned": E * per_op + n_keys * per_key,
+            "post_gc": kept * per_op + n_keys * per_key,
+            "post_gc_no_index": kept * per_op + n_keys * per_key}
+    for b in list(out.bufs.values()) + list(res.bufs.values()) + [tot]:
+        b.free()
+    eng.free_gen(wl, wr)
+    return {k: {"ms": ms[k], "entries": E if k == "unpruned" else kept,
+                "ops_per_s": (E if k == "unpruned" else kept) / (ms[k] * 1e-3),
+                "algorithmic_bytes": byts[k],
+                "frac": byts[k] / (ms[k] * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            for k in logs} | {"keys_id0_none_frac": none_frac,
+                              "note": "warm reads (SCT + base); post_gc = the same log "
+                                      "pruned at SCT, op ids with gaps"}
+
+
 def probe_read_gbs(eng, dl, nbytes, sp, torch):
     """The box's practical HBM read ceiling: tools/libagn_probe.so streams the
     OpSSCommit array (non-temporal LDS-DMA loads, 4 KiB per wave, every byte
@@ -591,9 +738,12 @@ def probe_read_gbs(eng, dl, nbytes, sp, torch):
     return (nbytes // 8192 * 8192) / (b.elapsed_time(e) / 5 * 1e-3) / 1e9  # whole 8 KiB blocks
 
 
-def gst_bench(eng, torch, dist, world, rank, sp):
+def gst_bench(eng, torch, dist, world, rank, sp, backend="nccl"):
     """cfg5: P=4096 partitions x D=256, local min over this GPU's partitions +
-    RCCL ncclMin allreduce; single-epoch latency and batched 256-epoch rate."""
+    RCCL ncclMin allreduce; single-epoch latency and batched 256-epoch rate.
+    With N > 1 the exchange is agn_gst_allreduce (RCCL over xGMI); under the
+    gloo rehearsal backend (several ranks on one GPU, which RCCL refuses) the
+    same D+1 words are exchanged through torch.distributed on the host."""
     from antidote_amd import _abi
     from antidote_amd.engine import Engine
     D, P, E = 256, 4096, 256
@@ -602,15 +752,28 @@ def gst_bench(eng, torch, dist, world, rank, sp):
     clocks = (1_700_000_000_000_000 + rng.integers(0, 10 ** 9, (E, Pl, D))).astype(np.uint64)
     dc = eng.upload(clocks)
     out = eng.empty(E * (D + 1) * 8)
-    if world > 1:
+    rccl = world > 1 and backend == "nccl"
+    if rccl:
         uid = [Engine.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])
-    def one():
-        eng.gst_min(D, Pl, 1, dc.ptr, None, out.ptr, sp)
-        if world > 1:
+
+    def exchange():
+        if rccl:
             eng.gst_allreduce(out.ptr, D + 1, sp)
+        elif world > 1:
+            v = eng.download(out, np.uint64, (D + 1,), stream=sp)
+            t = torch.from_numpy(v.view(np.int64).copy())
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            buf = t.numpy().view(np.uint64)
+            eng.lib.agn_memcpy_h2d(eng.ctx, out.ptr, buf.ctypes.data, buf.nbytes, sp)
+            eng.sync(sp)
+
+    def one(defined=None):
+        eng.gst_min(D, Pl, 1, dc.ptr, defined, out.ptr, sp)
+        exchange()
         eng.gst_finalize(D, 1, out.ptr, sp)
+
     for _ in range(5):
         one()
     torch.cuda.synchronize()
@@ -619,6 +782,36 @@ def gst_bench(eng, torch, dist, world, rank, sp):
         one()
     torch.cuda.synchronize()
     lat = (time.perf_counter() - t0) / 50
+    # proof that the exchange combined every rank: the epoch's result must
+    # equal the min of every rank's local minima gathered through
+    # torch.distributed, then the "some partition undefined => 0" rule
+    # (stable_time_functions.erl:78-84) with one undefined partition on the
+    # last rank, so the flag word crosses ranks
+    verified = None
+    if world > 1:
+        verified = True
+        for undef_rank in (None, world - 1):
+            defined = np.ones(Pl, np.uint8)
+            if rank == undef_rank:
+                defined[Pl // 2] = 0
+            ddef = eng.upload(defined)
+            eng.gst_min(D, Pl, 1, dc.ptr, ddef.ptr, out.ptr, sp)
+            torch.cuda.synchronize()
+            local = eng.download(out, np.uint64, (D + 1,), stream=sp).copy()
+            exchange()
+            eng.gst_finalize(D, 1, out.ptr, sp)
+            torch.cuda.synchronize()
+            got = eng.download(out, np.uint64, (D + 1,), stream=sp)
+            t = torch.from_numpy(local.view(np.int64).copy())   # clocks < 2^63
+            if backend == "nccl":
+                t = t.cuda()
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            want = t.cpu().numpy().view(np.uint64).copy()
+            if want[D] == 0:
+                want[:D][want[:D] != np.uint64(_abi.U64_MAX)] = 0
+            verified = verified and bool(np.array_equal(got, want)) and \
+                (bool(want[D] == 0) == (undef_rank is not None))
+            ddef.free()
     b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     eng.gst_min(D, Pl, E, dc.ptr, None, out.ptr, sp)
     b.record()
@@ -631,7 +824,12 @@ def gst_bench(eng, torch, dist, world, rank, sp):
     dc.free()
     out.free()
     return {"epoch_latency_us": lat * 1e6, "batched_epochs": E, "batched_ms": ms,
-            "batched_GBps": byts / (ms * 1e-3) / 1e9, "partitions_per_gpu": Pl, "n_dcs": D}
+            "batched_GBps": byts / (ms * 1e-3) / 1e9, "partitions_per_gpu": Pl, "n_dcs": D,
+            "exchange": ("rccl" if rccl else "torch.distributed " + backend) if world > 1
+            else None,
+            "rccl_ranks": world if rccl else None,
+            "exchange_verified": verified,
+            "epoch": "agn_gst_min -> exchange (min, D+1 words) -> agn_gst_finalize"}
 
 
 if __name__ == "__main__":
