@@ -119,6 +119,7 @@ PROTOTYPES = {
     "agn_open": (C.c_int, [C.c_int, C.POINTER(P)]),
     "agn_close": (C.c_int, [P]),
     "agn_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "agn_pool_trim": (C.c_int, [P, C.c_uint64]),
     "agn_dev_alloc": (C.c_int, [P, C.c_size_t, C.POINTER(P)]),
     "agn_dev_free": (C.c_int, [P, P]),
     "agn_memcpy_h2d": (C.c_int, [P, P, P, C.c_size_t, P]),

@@ -17,10 +17,23 @@
 #include "common.hpp"
 #include "gen.hpp"
 
+namespace agn {
+// host-staged materialize (agn_materialize_host): a non-blocking stream plus
+// a device buffer and a pinned host buffer that only grow
+struct Stager {
+    hipStream_t s = nullptr;
+    char *d = nullptr, *h = nullptr;
+    size_t cap = 0;
+};
+}  // namespace agn
+
 struct agn_ctx {
     int device = 0;
     std::mutex comm_mu;
     ncclComm_t comm = nullptr;
+    // host-staged materialize: stagers (stream + buffers) reused across calls
+    std::mutex st_mu;
+    std::vector<agn::Stager *> st_all, st_free;
 };
 
 namespace agn {
@@ -46,6 +59,49 @@ int use_device(agn_ctx *ctx) {
     if (!ctx) return fail(AGN_EINVAL, "null context");
     AGN_HIP(hipSetDevice(ctx->device));
     return AGN_OK;
+}
+
+// ---- the library's memory pools (one per device) ---------------------------
+namespace {
+constexpr int kMaxDevices = 64;
+std::mutex g_pool_mu;
+hipMemPool_t g_pool[kMaxDevices] = {};
+int g_pool_users[kMaxDevices] = {};
+
+uint64_t pool_keep_bytes() {
+    const char *v = getenv("AGN_POOL_KEEP");
+    if (!v || !*v) return UINT64_MAX;
+    return strtoull(v, nullptr, 10);
+}
+
+hipError_t pool_of(int dev, hipMemPool_t *out) {
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (!g_pool[dev]) {
+        hipMemPoolProps props;
+        std::memset(&props, 0, sizeof props);
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t p = nullptr;
+        hipError_t e = hipMemPoolCreate(&p, &props);
+        if (e != hipSuccess) return e;
+        uint64_t keep = pool_keep_bytes();
+        (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+        g_pool[dev] = p;
+    }
+    *out = g_pool[dev];
+    return hipSuccess;
+}
+}  // namespace
+
+hipError_t pool_malloc(void **p, size_t bytes, hipStream_t st) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    hipMemPool_t pool = nullptr;
+    if (e == hipSuccess) e = pool_of(dev, &pool);
+    if (e != hipSuccess) return e;
+    return hipMallocFromPoolAsync(p, bytes ? bytes : 1, pool, st);
 }
 
 static bool is_tag_type(uint32_t t) { return t == AGN_SET_AW || t == AGN_REGISTER_MV; }
@@ -120,30 +176,49 @@ int agn_open(int device, agn_ctx **out) {
     if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
         return fail(AGN_ENOTSUP, "built for gfx950, device is %s", p.gcnArchName);
     // Stream-ordered scratch (prune, ingest, op-log arenas) comes from the
-    // device's default pool; keep freed blocks cached in it instead of
-    // unmapping them at every synchronize (release threshold 0), so GC and
-    // ingest calls do not remap gigabytes each time.  AGN_POOL_KEEP=0 (A/B
-    // knob) leaves the default.
-    {
-        const char *v = getenv("AGN_POOL_KEEP");
-        if (!(v && v[0] == '0')) {
-            hipMemPool_t pool;
-            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-                uint64_t keep = UINT64_MAX;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-            }
-        }
-    }
+    // library's own pool of this device (pool_malloc), created here so a
+    // failure shows at open; freed blocks stay cached in it (GC and ingest
+    // do not remap gigabytes per call) until agn_pool_trim / agn_close.
+    hipMemPool_t pool = nullptr;
+    if (pool_of(device, &pool) != hipSuccess) return fail(AGN_EHIP, "hipMemPoolCreate");
     agn_ctx *c = new (std::nothrow) agn_ctx;
     if (!c) return fail(AGN_ENOMEM, "ctx");
     c->device = device;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        ++g_pool_users[device];
+    }
     *out = c;
+    return AGN_OK;
+}
+
+int agn_pool_trim(agn_ctx *ctx, uint64_t keep_bytes) {
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    hipMemPool_t pool = nullptr;
+    if (pool_of(ctx->device, &pool) != hipSuccess) return fail(AGN_EHIP, "pool");
+    AGN_HIP(hipDeviceSynchronize());  // frees still queued on streams reach the pool
+    AGN_HIP(hipMemPoolTrimTo(pool, (size_t)keep_bytes));
     return AGN_OK;
 }
 
 int agn_close(agn_ctx *ctx) {
     if (!ctx) return AGN_OK;
     agn_comm_destroy(ctx);
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        last = --g_pool_users[ctx->device] == 0;
+    }
+    for (Stager *S : ctx->st_all) {
+        (void)hipStreamSynchronize(S->s);
+        if (S->d) (void)hipFree(S->d);
+        if (S->h) (void)hipHostFree(S->h);
+        (void)hipStreamDestroy(S->s);
+        delete S;
+    }
+    // the last context of a device hands the pool's cached blocks back
+    if (last) (void)agn_pool_trim(ctx, 0);
     delete ctx;
     return AGN_OK;
 }
@@ -253,40 +328,82 @@ int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_of
 }  // extern "C"
 
 // ---- host-staged materialize --------------------------------------------------
+// The per-key NIF entry (materialize/4 with the ops list as an Erlang term).
+// Each call borrows a stager of its context -- a non-blocking stream plus a
+// device buffer and a pinned host buffer that only grow -- packs every input
+// array into the pinned buffer, and does one H2D copy, the materialize kernel
+// and one D2H copy on that stream, then waits for that stream only.  Calls from
+// many threads run on different stagers concurrently; nothing allocates in
+// the steady state and nothing synchronizes the device.
 namespace {
-struct Staging {
-    std::vector<void *> bufs;
-    int err = AGN_OK;
-    template <class T>
-    T *up(const T *h, size_t n) {
-        if (!h || n == 0 || err) return nullptr;
-        void *d = nullptr;
-        if (hipMalloc(&d, n * sizeof(T)) != hipSuccess) { err = fail(AGN_ENOMEM, "staging"); return nullptr; }
-        bufs.push_back(d);
-        if (hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) {
-            err = fail(AGN_EHIP, "staging copy");
-            return nullptr;
+int stager_grow(Stager *S, size_t bytes) {
+    if (bytes <= S->cap) return AGN_OK;
+    const size_t c = std::max(bytes, 2 * S->cap);
+    if (S->d) (void)hipFree(S->d);
+    if (S->h) (void)hipHostFree(S->h);
+    S->d = S->h = nullptr;
+    S->cap = 0;
+    if (hipMalloc((void **)&S->d, c) != hipSuccess) return fail(AGN_ENOMEM, "staging: %zu B", c);
+    if (hipHostMalloc((void **)&S->h, c, hipHostMallocDefault) != hipSuccess)
+        return fail(AGN_ENOMEM, "staging: %zu B pinned", c);
+    S->cap = c;
+    return AGN_OK;
+}
+
+Stager *stager_get(agn_ctx *ctx) {
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        if (!ctx->st_free.empty()) {
+            Stager *S = ctx->st_free.back();
+            ctx->st_free.pop_back();
+            return S;
         }
-        return (T *)d;
+    }
+    Stager *S = new (std::nothrow) Stager;
+    if (!S) return nullptr;
+    if (hipStreamCreateWithFlags(&S->s, hipStreamNonBlocking) != hipSuccess) {
+        delete S;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(ctx->st_mu);
+    ctx->st_all.push_back(S);
+    return S;
+}
+
+void stager_put(agn_ctx *ctx, Stager *S) {
+    std::lock_guard<std::mutex> g(ctx->st_mu);
+    ctx->st_free.push_back(S);
+}
+
+// Packs host arrays into the stager: in(...) reserves an input slot (copied
+// H2D), out(...) an output slot (copied back D2H); device pointers are final
+// once layout() has sized the buffer.
+struct Pack {
+    struct In { const void *h; size_t bytes; size_t off; };
+    struct Out { void *h; size_t bytes; size_t off; };
+    std::vector<In> ins;
+    std::vector<Out> outs;
+    size_t off = 0, in_end = 0;
+    static size_t al(size_t b) { return (b + 255) & ~size_t(255); }
+    template <class T>
+    size_t in(const T *h, size_t n) {
+        if (!h || n == 0) return SIZE_MAX;
+        ins.push_back({h, n * sizeof(T), off});
+        off = al(off + n * sizeof(T));
+        return ins.back().off;
     }
     template <class T>
-    T *alloc(const T *h, size_t n) {
-        if (!h || n == 0 || err) return nullptr;
-        void *d = nullptr;
-        if (hipMalloc(&d, n * sizeof(T)) != hipSuccess) { err = fail(AGN_ENOMEM, "staging"); return nullptr; }
-        bufs.push_back(d);
-        return (T *)d;
-    }
-    template <class T>
-    void down(T *h, const T *d, size_t n) {
-        if (!h || !d || n == 0 || err) return;
-        if (hipMemcpy(h, d, n * sizeof(T), hipMemcpyDeviceToHost) != hipSuccess)
-            err = fail(AGN_EHIP, "staging copy back");
-    }
-    ~Staging() {
-        for (void *p : bufs) (void)hipFree(p);
+    size_t out(T *h, size_t n) {
+        if (!h) return SIZE_MAX;
+        if (in_end == 0) in_end = off;
+        outs.push_back({h, std::max<size_t>(n, 1) * sizeof(T), off});
+        off = al(off + std::max<size_t>(n, 1) * sizeof(T));
+        return outs.back().off;
     }
 };
+
+template <class T>
+T *at(const Stager *S, size_t o) { return o == SIZE_MAX ? nullptr : (T *)(S->d + o); }
 }  // namespace
 
 extern "C" {
@@ -299,66 +416,103 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     if (req->n_req == 0) return AGN_OK;
     const uint32_t D = log->n_dcs, W = n_words(D);
     const uint64_t E = log->n_entries, K = log->n_keys, Q = req->n_req;
-    Staging st;
-    agn_log dl = *log;
-    dl.key_off = st.up(log->key_off, K + 1);
-    dl.key_len = st.up(log->key_len, K);
-    dl.key_type = st.up(log->key_type, K);
-    dl.oc = st.up(log->oc, E * D);
-    dl.oc_mask = st.up(log->oc_mask, E * W);
-    dl.op_id = st.up(log->op_id, E);
-    dl.txid = st.up(log->txid, E);
-    dl.eff = st.up(log->eff, E);
-    dl.tag = st.up(log->tag, E);
-    dl.add_tok = st.up(log->add_tok, E);
-    dl.rem_off = st.up(log->rem_off, log->rem_off ? E + 1 : 0);
     uint64_t n_rem = log->rem_off ? log->rem_off[E] : 0;
     if (log->rem_off && log->key_len)  // segmented log: the token arena's high-water mark
         for (uint64_t e = 0; e <= E; ++e) n_rem = std::max<uint64_t>(n_rem, log->rem_off[e]);
-    dl.rem_tok = st.up(log->rem_tok, n_rem);
-    dl.key_id0 = st.up(log->key_id0, K);
-    agn_read dr = *req;
-    dr.keys = st.up(req->keys, Q);
-    dr.R = st.up(req->R, Q * D);
-    dr.R_mask = st.up(req->R_mask, Q * W);
-    dr.sct = st.up(req->sct, Q * D);
-    dr.sct_mask = st.up(req->sct_mask, Q * W);
-    dr.sct_ignore = st.up(req->sct_ignore, Q);
-    dr.txid = st.up(req->txid, Q);
-    dr.base_value = st.up(req->base_value, Q);
-    dr.base_off = st.up(req->base_off, req->base_off ? Q + 1 : 0);
     const uint64_t n_base = req->base_off ? req->base_off[Q] : 0;
-    dr.base_tag = st.up(req->base_tag, n_base);
-    dr.base_tok = st.up(req->base_tok, n_base);
-    agn_result dout = *out;
-    dout.value = st.alloc(out->value, Q);
-    dout.hole = st.alloc(out->hole, Q);
-    dout.lastct = st.alloc(out->lastct, Q * D);
-    dout.lastct_mask = st.alloc(out->lastct_mask, Q * W);
-    dout.count = st.alloc(out->count, Q);
-    dout.flags = st.alloc(out->flags, Q);
-    dout.err_pos = st.alloc(out->err_pos, Q);
     const uint64_t n_out = out->out_off ? out->out_off[Q] : 0;
-    dout.out_off = st.up(out->out_off, out->out_off ? Q + 1 : 0);
-    dout.out_n = st.alloc(out->out_n, Q);
-    dout.out_tag = st.alloc(out->out_tag, n_out ? n_out : 1);
-    dout.out_tok = st.alloc(out->out_tok, n_out ? n_out : 1);
-    if (st.err) return st.err;
-    rc = agn_materialize(ctx, &dl, &dr, &dout, nullptr);
-    if (rc) return rc;
-    AGN_HIP(hipDeviceSynchronize());
-    st.down(out->value, dout.value, Q);
-    st.down(out->hole, dout.hole, Q);
-    st.down(out->lastct, dout.lastct, Q * D);
-    st.down(out->lastct_mask, dout.lastct_mask, Q * W);
-    st.down(out->count, dout.count, Q);
-    st.down(out->flags, dout.flags, Q);
-    st.down(out->err_pos, dout.err_pos, Q);
-    st.down(out->out_n, dout.out_n, Q);
-    st.down(out->out_tag, dout.out_tag, n_out);
-    st.down(out->out_tok, dout.out_tok, n_out);
-    return st.err;
+    Pack p;
+    const size_t l_koff = p.in(log->key_off, K + 1), l_klen = p.in(log->key_len, K),
+                 l_ktype = p.in(log->key_type, K), l_oc = p.in(log->oc, E * D),
+                 l_ocm = p.in(log->oc_mask, E * W), l_id = p.in(log->op_id, E),
+                 l_tx = p.in(log->txid, E), l_eff = p.in(log->eff, E), l_tag = p.in(log->tag, E),
+                 l_add = p.in(log->add_tok, E),
+                 l_roff = p.in(log->rem_off, log->rem_off ? E + 1 : 0),
+                 l_rtok = p.in(log->rem_tok, n_rem), l_id0 = p.in(log->key_id0, K);
+    const size_t q_keys = p.in(req->keys, Q), q_R = p.in(req->R, Q * D),
+                 q_Rm = p.in(req->R_mask, Q * W), q_sct = p.in(req->sct, Q * D),
+                 q_sctm = p.in(req->sct_mask, Q * W), q_sign = p.in(req->sct_ignore, Q),
+                 q_tx = p.in(req->txid, Q), q_bv = p.in(req->base_value, Q),
+                 q_boff = p.in(req->base_off, req->base_off ? Q + 1 : 0),
+                 q_btag = p.in(req->base_tag, n_base), q_btok = p.in(req->base_tok, n_base),
+                 o_off = p.in(out->out_off, out->out_off ? Q + 1 : 0);
+    const size_t o_val = p.out(out->value, Q), o_hole = p.out(out->hole, Q),
+                 o_ct = p.out(out->lastct, Q * D), o_ctm = p.out(out->lastct_mask, Q * W),
+                 o_cnt = p.out(out->count, Q), o_flg = p.out(out->flags, Q),
+                 o_epos = p.out(out->err_pos, Q), o_n = p.out(out->out_n, Q),
+                 o_tag = p.out(out->out_tag, n_out), o_tok = p.out(out->out_tok, n_out);
+    if (p.in_end == 0) p.in_end = p.off;
+    Stager *S = stager_get(ctx);
+    if (!S) return fail(AGN_ENOMEM, "materialize_host: stager");
+    rc = stager_grow(S, p.off);
+    if (rc) {
+        stager_put(ctx, S);
+        return rc;
+    }
+    for (const auto &x : p.ins) std::memcpy(S->h + x.off, x.h, x.bytes);
+    agn_log dl = *log;
+    dl.key_off = at<const uint64_t>(S, l_koff);
+    dl.key_len = at<const uint64_t>(S, l_klen);
+    dl.key_type = at<const uint8_t>(S, l_ktype);
+    dl.oc = at<const uint64_t>(S, l_oc);
+    dl.oc_mask = at<const uint64_t>(S, l_ocm);
+    dl.op_id = at<const uint32_t>(S, l_id);
+    dl.txid = at<const uint64_t>(S, l_tx);
+    dl.eff = at<const int64_t>(S, l_eff);
+    dl.tag = at<const uint32_t>(S, l_tag);
+    dl.add_tok = at<const uint64_t>(S, l_add);
+    dl.rem_off = at<const uint32_t>(S, l_roff);
+    dl.rem_tok = at<const uint64_t>(S, l_rtok);
+    dl.key_id0 = at<const uint32_t>(S, l_id0);
+    agn_read dr = *req;
+    dr.keys = at<const uint64_t>(S, q_keys);
+    dr.R = at<const uint64_t>(S, q_R);
+    dr.R_mask = at<const uint64_t>(S, q_Rm);
+    dr.sct = at<const uint64_t>(S, q_sct);
+    dr.sct_mask = at<const uint64_t>(S, q_sctm);
+    dr.sct_ignore = at<const uint8_t>(S, q_sign);
+    dr.txid = at<const uint64_t>(S, q_tx);
+    dr.base_value = at<const int64_t>(S, q_bv);
+    dr.base_off = at<const uint64_t>(S, q_boff);
+    dr.base_tag = at<const uint32_t>(S, q_btag);
+    dr.base_tok = at<const uint64_t>(S, q_btok);
+    agn_result dout = *out;
+    dout.value = at<int64_t>(S, o_val);
+    dout.hole = at<int64_t>(S, o_hole);
+    dout.lastct = at<uint64_t>(S, o_ct);
+    dout.lastct_mask = at<uint64_t>(S, o_ctm);
+    dout.count = at<uint32_t>(S, o_cnt);
+    dout.flags = at<uint32_t>(S, o_flg);
+    dout.err_pos = at<uint32_t>(S, o_epos);
+    dout.out_off = at<const uint64_t>(S, o_off);
+    dout.out_n = at<uint32_t>(S, o_n);
+    dout.out_tag = at<uint32_t>(S, o_tag);
+    dout.out_tok = at<uint64_t>(S, o_tok);
+    hipError_t e = hipMemcpyAsync(S->d, S->h, p.in_end, hipMemcpyHostToDevice, S->s);
+    if (e == hipSuccess) {
+        rc = agn_materialize(ctx, &dl, &dr, &dout, S->s);
+        if (rc == AGN_OK && p.off > p.in_end)
+            e = hipMemcpyAsync(S->h + p.in_end, S->d + p.in_end, p.off - p.in_end,
+                               hipMemcpyDeviceToHost, S->s);
+    }
+    const hipError_t es = hipStreamSynchronize(S->s);
+    if (e == hipSuccess) e = es;
+    if (rc == AGN_OK && e != hipSuccess)
+        rc = fail(AGN_EHIP, "materialize_host: %s", hipGetErrorString(e));
+    if (rc == AGN_OK)
+        for (const auto &x : p.outs) {
+            // out_tag / out_tok hold n_out elements (at least one slot reserved)
+            const size_t b = (x.h == (void *)out->out_tag) ? n_out * 4
+                           : (x.h == (void *)out->out_tok) ? n_out * 8 : x.bytes;
+            if (b) std::memcpy(x.h, S->h + x.off, b);
+        }
+    stager_put(ctx, S);
+    return rc;
 }
+
+}  // extern "C"
+
+extern "C" {
 
 // ---- base selection / GST ---------------------------------------------------------
 int agn_select_base(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_req, const uint64_t *cache_off,

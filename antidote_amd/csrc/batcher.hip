@@ -94,11 +94,13 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
     std::vector<uint64_t> keys(n);
     std::vector<uint32_t> lens(n);
     for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
+    // flush + exact key lengths + the arena held shared until the batch is done
+    std::shared_lock<std::shared_mutex> hold;
+    int rc = oplog_begin_read(B->log, B->stream, tags ? n : 0, keys.data(), lens.data(), hold);
+    if (rc) return rc;
     uint64_t ncap = 0;
-    if (tags) {
-        oplog_key_lens(B->log, n, keys.data(), lens.data());
+    if (tags)
         for (uint64_t i = 0; i < n; ++i) ncap += (uint64_t)lens[i] + b[i]->rd->n_base;
-    }
     // Layout: in = keys R Rm sct sctm sign txid base_value base_off base_tag base_tok cap_off
     //         out = value hole lastct lastct_mask count flags err_pos out_n out_tag out_tok
     size_t off = 0;
@@ -114,7 +116,7 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
                  o_ctm = slot(sparse ? n * W * 8 : 0), o_cnt = slot(n * 4), o_flg = slot(n * 4),
                  o_epos = slot(n * 4), o_outn = slot(tags ? n * 4 : 0),
                  o_otag = slot(tags ? ncap * 4 : 0), o_otok = slot(tags ? ncap * 8 : 0);
-    int rc = grow(B, off);
+    rc = grow(B, off);
     if (rc) return rc;
     char *h = B->hbuf, *d = B->dbuf;
     std::memset(h, 0, in_bytes);
@@ -190,7 +192,9 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
         res.out_tag = (uint32_t *)(d + o_otag);
         res.out_tok = (uint64_t *)(d + o_otok);
     }
-    rc = agn_oplog_read(B->log, &req, &res, B->stream);
+    agn_log view;
+    oplog_view(B->log, &view);
+    rc = agn_materialize(B->ctx, &view, &req, &res, B->stream);
     if (rc) return rc;
     AGN_HIP(hipMemcpyAsync(h + in_bytes, d + in_bytes, off - in_bytes, hipMemcpyDeviceToHost,
                            B->stream));

@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <shared_mutex>
+
 #include "../../include/antidote_gpu.h"
 
 #define AGN_WAVE 64
@@ -16,6 +18,17 @@ void set_error(const char *fmt, ...);
 int fail(int code, const char *fmt, ...);
 // hipSetDevice(ctx's device); AGN_EINVAL for a null context.
 int use_device(agn_ctx *ctx);
+
+// Stream-ordered scratch and arenas come from the library's own memory pool
+// of the current device (never the device's default pool, which torch and
+// other hipMallocAsync users share): freed blocks stay cached in it (release
+// threshold AGN_POOL_KEEP bytes, default unlimited), agn_pool_trim and
+// agn_close hand them back.
+hipError_t pool_malloc(void **p, size_t bytes, hipStream_t st);
+template <class T>
+inline hipError_t pool_malloc(T **p, size_t bytes, hipStream_t st) {
+    return pool_malloc((void **)p, bytes, st);
+}
 
 #define AGN_HIP(call)                                                              \
     do {                                                                           \
@@ -113,7 +126,9 @@ inline unsigned resident_grid(K kernel, unsigned threads, uint64_t work_blocks) 
 
 // oplog.hip internals used by the read batcher.
 void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, uint64_t *K);
-void oplog_key_lens(const agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t *out);
+int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *keys,
+                     uint32_t *lens, std::shared_lock<std::shared_mutex> &hold);
+void oplog_view(const agn_oplog *L, agn_log *v);
 agn_ctx *oplog_ctx(const agn_oplog *L);
 
 // Launchers (defined in the .hip files).
@@ -147,6 +162,10 @@ int launch_prune_mark(const agn_log &log, const uint8_t *prune, const uint64_t *
 int launch_prune_scatter_seg(const agn_log &log, const agn_log &out, const uint8_t *prune,
                              const uint8_t *keep, const uint64_t *tstart, uint32_t *flags,
                              hipStream_t st);
+int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
+                         uint32_t *key_lcap, const uint8_t *prune, const uint64_t *thr,
+                         const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags,
+                         hipStream_t st);
 int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
                      const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
                      uint64_t *totals, hipStream_t st);

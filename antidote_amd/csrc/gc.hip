@@ -218,7 +218,7 @@ int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *t
     const size_t keep_bytes = (E + 255) / 256 * 256;
     const size_t bytes = tmp_bytes + keep_bytes + 3 * (K + 1) * sizeof(uint64_t) + 256;
     uint8_t *scratch = nullptr;
-    AGN_HIP(hipMallocAsync((void **)&scratch, bytes, st));
+    AGN_HIP(pool_malloc((void **)&scratch, bytes, st));
     void *tmp = scratch;
     uint8_t *keep = scratch + tmp_bytes;
     uint64_t *cnt = (uint64_t *)(keep + keep_bytes);
@@ -257,6 +257,301 @@ int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *t
     const hipError_t ef = hipFreeAsync(scratch, st);
     if (rc == AGN_OK && ef != hipSuccess) rc = fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
     return rc;
+}
+
+// ---- in-place prune of the engine-owned op log (agn_oplog_prune) -----------
+// snapshot_insert_gc -> prune_ops over the segmented arena, in place and in
+// ONE pass: each wave owns a key, runs the VC filter over the key's entries
+// (the mark loop above) and compacts the kept entries toward the segment
+// start while their OpSSCommit slices are still in registers -- every row is
+// read once, every kept row written once, unselected keys cost nothing.
+// Compaction is safe in place: the destination of an entry is never above
+// its source, every load of an iteration precedes its stores in program
+// order (one pointer per array, no __restrict__, so the compiler keeps that
+// order), and an iteration only writes slots below the next iteration's
+// sources.  Removal tokens move the same way; a lane buffers up to PT tokens
+// in registers before any lane stores, and an iteration with a longer list
+// copies its lists one entry at a time in position order instead.
+// Per key it then writes the new key_len, key_id0 (consecutive-id base or
+// AGN_ID0_NONE), the ETS ListLen after the resize policy (:540-558, with
+// prune_ops' NewLength = 1 when nothing survives, :580-583) and
+// meta[4][K] = {len, token len, ListLen, id0} for the host's bookkeeping.
+namespace {
+
+struct InplaceArgs {
+    uint64_t *oc, *mask, *txid, *add, *tok;
+    uint32_t *op_id, *tag, *rem_off;
+    int64_t *eff;
+    const uint64_t *key_off;
+    uint64_t *key_len;
+    uint32_t *key_id0, *key_lcap;
+    uint64_t n_keys;
+    uint32_t D, W;
+};
+
+__device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
+    if ((int64_t)new_len > (int64_t)list_len - AGN_RESIZE_THRESHOLD) return list_len * 2u;
+    const uint32_t half = list_len / 2u;
+    if (half <= AGN_OPS_THRESHOLD) return list_len;
+    return ((int64_t)half - AGN_RESIZE_THRESHOLD > (int64_t)new_len) ? half : list_len;
+}
+
+constexpr int PT = 4;  // removal tokens a lane buffers per entry
+
+template <int DPL, int LPO, bool SPARSE, bool FULL>
+__global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
+                                                       const uint8_t *__restrict__ prune,
+                                                       const uint64_t *__restrict__ thr,
+                                                       const uint64_t *__restrict__ thr_mask,
+                                                       uint32_t *__restrict__ meta,
+                                                       uint32_t *__restrict__ flags) {
+    using S = Shape<DPL, LPO>;
+    const uint64_t k = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (k >= a.n_keys) return;
+    const uint64_t K = a.n_keys;
+    const int lane = lane_id();
+    const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t D = a.D, W = a.W;
+    const bool tags = a.rem_off != nullptr;
+    const uint64_t off = uniform_u64(a.key_off[k]);
+    const uint64_t n = uniform_u64(a.key_len[k]);
+    const bool gc = prune == nullptr || prune[k] != 0;
+    const uint32_t tb = tags ? (uint32_t)uniform_u64(a.rem_off[off]) : 0u;
+    if (!gc) {
+        if (lane == 0) {
+            meta[k] = (uint32_t)n;
+            meta[K + k] = tags ? a.rem_off[off + n] - tb : 0u;
+            meta[2 * K + k] = a.key_lcap[k];
+            meta[3 * K + k] = a.key_id0[k];
+            if (flags) flags[k] = 0u;
+        }
+        return;
+    }
+    uint64_t t[DPL];
+    const uint32_t tbits = chunk_bits<DPL, SPARSE>(thr_mask, k, W, d0, D);
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) t[j] = ((tbits >> j) & 1u) ? thr[k * D + (uint32_t)(d0 + j)] : 0ull;
+    const agn_log rl = [&] {
+        agn_log l;
+        l.oc = a.oc;
+        l.oc_mask = a.mask;
+        return l;
+    }();
+    uint64_t written = 0;
+    uint32_t rwritten = 0, first_id = AGN_ID0_NONE, last_id = 0;
+    bool consec = true;
+    for (uint64_t b = 0; b < n; b += S::OPI) {
+        const uint64_t pos = b + (uint64_t)slot;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);
+        uint64_t o[DPL];
+        uint32_t obits;
+        load_rows<DPL, SPARSE, FULL>(rl, e, d0, D, W, o, obits);
+        if (!valid) obits = 0u;
+        bool le = true;
+#pragma unroll
+        for (int j = 0; j < DPL; ++j)
+            if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
+        if (LPO > 1) {
+            const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
+            le = (ballot(!le) & grp) == 0ull;
+        }
+        const bool kp = valid && !le;  // belongs_to_snapshot_op(Threshold, op)
+        const uint64_t km = ballot(kp && sub == 0);  // one bit per kept op (its sub-0 lane)
+        const uint32_t nk = (uint32_t)__builtin_popcountll(km);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(km & ((1ull << (slot * LPO)) - 1ull) &
+                                                            ~0ull);
+        const uint64_t dst = off + written + rank;
+        // per-entry fields and removal lists: loads of the whole iteration first
+        uint32_t id = 0, tg = 0, r0 = 0, rl_ = 0;
+        uint64_t tx = 0, ad = 0;
+        int64_t ef = 0;
+        uint64_t tk[PT];
+        const bool head = kp && sub == 0;
+        if (head) {
+            id = a.op_id[e];
+            tx = a.txid[e];
+            if (a.eff) ef = a.eff[e];
+            if (a.tag) {
+                tg = a.tag[e];
+                ad = a.add[e];
+            }
+            if (tags) {
+                r0 = a.rem_off[e];
+                rl_ = a.rem_off[e + 1] - r0;
+            }
+        }
+        const bool long_list = tags && ballot(head && rl_ > (uint32_t)PT) != 0ull;
+        if (tags && !long_list && head) {
+#pragma unroll
+            for (int x = 0; x < PT; ++x) tk[x] = (uint32_t)x < rl_ ? a.tok[r0 + x] : 0ull;
+        }
+        // token destinations: exclusive scan of the kept list lengths
+        uint32_t tincl = 0;
+        if (tags) {
+            tincl = rl_;
+#pragma unroll
+            for (int x = 1; x < AGN_WAVE; x <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)tincl, x, AGN_WAVE);
+                if (lane >= x) tincl += v;
+            }
+        }
+        const uint32_t tdst = tb + rwritten + (tincl - rl_);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // stores
+        if (kp) {
+            if constexpr (FULL) {
+                u64x2 *q = reinterpret_cast<u64x2 *>(a.oc + dst * D + (uint32_t)d0);
+#pragma unroll
+                for (int j = 0; j < DPL / 2; ++j) {
+                    u64x2 x;
+                    x.x = o[2 * j];
+                    x.y = o[2 * j + 1];
+                    q[j] = x;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < DPL; ++j)
+                    if ((uint32_t)(d0 + j) < D) a.oc[dst * D + (uint32_t)(d0 + j)] = o[j];
+            }
+        }
+        if (SPARSE && a.mask) {
+            // mask words of the kept entries: lane sub < W of each kept op
+            const uint64_t mw = (kp && (uint32_t)sub < W) ? a.mask[e * W + (uint32_t)sub] : 0ull;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (kp && (uint32_t)sub < W) a.mask[dst * W + (uint32_t)sub] = mw;
+        }
+        if (head) {
+            a.op_id[dst] = id;
+            a.txid[dst] = tx;
+            if (a.eff) a.eff[dst] = ef;
+            if (a.tag) {
+                a.tag[dst] = tg;
+                a.add[dst] = ad;
+            }
+        }
+        if (tags) {
+            if (!long_list) {
+                if (head) {
+#pragma unroll
+                    for (int x = 0; x < PT; ++x)
+                        if ((uint32_t)x < rl_) a.tok[tdst + x] = tk[x];
+                }
+            } else {
+                // position order, one kept entry at a time, 64 tokens per step
+                uint64_t rest = km;
+                while (rest) {
+                    const int src_lane = __builtin_ctzll(rest);
+                    rest &= rest - 1ull;
+                    const uint32_t s0 = (uint32_t)__shfl((int)r0, src_lane, AGN_WAVE);
+                    const uint32_t sl = (uint32_t)__shfl((int)rl_, src_lane, AGN_WAVE);
+                    const uint32_t sd = (uint32_t)__shfl((int)tdst, src_lane, AGN_WAVE);
+                    for (uint32_t c = 0; c < sl; c += AGN_WAVE) {
+                        const bool in = c + (uint32_t)lane < sl;
+                        const uint64_t v = in ? a.tok[s0 + c + (uint32_t)lane] : 0ull;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        if (in) a.tok[sd + c + (uint32_t)lane] = v;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+            }
+            if (head) {
+                a.rem_off[dst] = tdst;
+                a.rem_off[dst + 1] = tdst + rl_;
+            }
+            rwritten += (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
+        }
+        // consecutive-id index over the kept ids, in position order
+        if (nk) {
+            const uint64_t prev_m = km & lt;
+            const int pl = prev_m ? 63 - __builtin_clzll(prev_m) : lane;
+            const uint32_t prev_id = (uint32_t)__shfl((int)id, pl, AGN_WAVE);
+            const bool first_of_iter = head && prev_m == 0ull;
+            bool ok = true;
+            if (head) ok = first_of_iter ? (written == 0 || id == last_id + 1u) : (id == prev_id + 1u);
+            consec = consec && (ballot(head && !ok) == 0ull);
+            const int lo = __builtin_ctzll(km), hi = 63 - __builtin_clzll(km);
+            if (written == 0) first_id = (uint32_t)__shfl((int)id, lo, AGN_WAVE);
+            last_id = (uint32_t)__shfl((int)id, hi, AGN_WAVE);
+        }
+        written += nk;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) {
+        const uint32_t l = (uint32_t)written;
+        const uint32_t id0 = (l && consec && first_id != AGN_ID0_NONE) ? first_id : AGN_ID0_NONE;
+        uint32_t lc = a.key_lcap[k];
+        if (lc) {
+            lc = resize_list_len_dev(l ? l : 1u, lc);  // prune_ops' NewLength (1 if none kept)
+            if (lc < l) lc = l;
+        }
+        a.key_len[k] = written;
+        a.key_id0[k] = id0;
+        a.key_lcap[k] = lc;
+        if (tags && l == 0) a.rem_off[off] = tb;  // an empty segment keeps its token base
+        meta[k] = l;
+        meta[K + k] = rwritten;
+        meta[2 * K + k] = lc;
+        meta[3 * K + k] = id0;
+        if (flags) flags[k] = l == 0 ? AGN_GC_ALL_PRUNED : 0u;
+    }
+}
+
+template <int DPL, int LPO, bool SPARSE>
+int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *thr,
+                  const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags, hipStream_t st) {
+    const unsigned blocks = grid_for(a.n_keys, 4, 0x7fffffffu);
+    const bool full = !a.mask && (DPL % 2 == 0) && a.D == (uint32_t)(DPL * LPO);
+    if (full)
+        hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, (DPL % 2 == 0)>), dim3(blocks),
+                           dim3(256), 0, st, a, prune, thr, thr_mask, meta, flags);
+    else
+        hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, false>), dim3(blocks), dim3(256), 0,
+                           st, a, prune, thr, thr_mask, meta, flags);
+    return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_inplace launch");
+}
+
+template <bool SPARSE>
+int inplace(const InplaceArgs &a, const uint8_t *prune, const uint64_t *thr,
+            const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags, hipStream_t st) {
+#define AGN_L(DPL, LPO) inplace_shape<DPL, LPO, SPARSE>(a, prune, thr, thr_mask, meta, flags, st)
+    AGN_DISPATCH_SHAPES(a.D, AGN_L)
+#undef AGN_L
+}
+
+}  // namespace
+
+int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
+                         uint32_t *key_lcap, const uint8_t *prune, const uint64_t *thr,
+                         const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags,
+                         hipStream_t st) {
+    if (view.n_keys == 0) return AGN_OK;
+    InplaceArgs a;
+    a.oc = (uint64_t *)view.oc;
+    a.mask = (uint64_t *)view.oc_mask;
+    a.txid = (uint64_t *)view.txid;
+    a.add = (uint64_t *)view.add_tok;
+    a.tok = (uint64_t *)view.rem_tok;
+    a.op_id = (uint32_t *)view.op_id;
+    a.tag = (uint32_t *)view.tag;
+    a.rem_off = (uint32_t *)view.rem_off;
+    a.eff = (int64_t *)view.eff;
+    a.key_off = view.key_off;
+    a.key_len = key_len;
+    a.key_id0 = key_id0;
+    a.key_lcap = key_lcap;
+    a.n_keys = view.n_keys;
+    a.D = view.n_dcs;
+    a.W = n_words(view.n_dcs);
+    const bool sparse = view.oc_mask || thr_mask;
+    return sparse ? inplace<true>(a, prune, thr, thr_mask, meta, flags, st)
+                  : inplace<false>(a, prune, thr, thr_mask, meta, flags, st);
 }
 
 // Two-phase prune_ops into a fresh segmented arena (agn_oplog_prune): the

@@ -195,7 +195,7 @@ int launch_log_ingest(const agn_log_records &r, uint32_t D, uint64_t n_keys,
     const size_t words = 2 * T + 4 * n + 2;
     const size_t bytes = tb + words * 8 + (n + 1) * 4 + 512;
     uint8_t *scratch = nullptr;
-    AGN_HIP(hipMallocAsync((void **)&scratch, bytes, st));
+    AGN_HIP(pool_malloc((void **)&scratch, bytes, st));
     void *tmp = scratch;
     uint64_t *hk = (uint64_t *)(scratch + tb);
     uint64_t *hv = hk + T;

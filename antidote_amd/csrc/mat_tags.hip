@@ -499,7 +499,7 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
     // worklist of keys whose live state overflows the fast table: [0] = count
     uint32_t *wl = nullptr;
-    AGN_HIP(hipMallocAsync((void **)&wl, (req.n_req + 1) * sizeof(uint32_t), st));
+    AGN_HIP(pool_malloc((void **)&wl, (req.n_req + 1) * sizeof(uint32_t), st));
     int rc = AGN_OK;
     {
         hipError_t e = hipMemsetAsync(wl, 0, sizeof(uint32_t), st);

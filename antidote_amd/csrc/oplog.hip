@@ -151,7 +151,7 @@ template <class T>
 hipError_t grow_array(T *&p, uint64_t old_n, uint64_t new_n, hipStream_t st) {
     if (!p && old_n) return hipErrorInvalidValue;
     T *q = nullptr;
-    hipError_t e = hipMallocAsync((void **)&q, std::max<uint64_t>(new_n, 1) * sizeof(T), st);
+    hipError_t e = pool_malloc((void **)&q, std::max<uint64_t>(new_n, 1) * sizeof(T), st);
     if (e != hipSuccess) return e;
     if (p && old_n) {
         e = hipMemcpyAsync(q, p, old_n * sizeof(T), hipMemcpyDeviceToDevice, st);
@@ -372,7 +372,7 @@ int do_flush(agn_oplog *L, hipStream_t st) {
         }
     }
     char *d = nullptr;
-    AGN_HIP(hipMallocAsync((void **)&d, off, st));
+    AGN_HIP(pool_malloc((void **)&d, off, st));
     AGN_HIP(hipMemcpyAsync(d, h, off, hipMemcpyHostToDevice, st));
     AGN_HIP(hipEventRecord(L->up_done, st));
     L->up_pending = true;
@@ -616,8 +616,8 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     //    token counts per key.
     uint8_t *keep = nullptr;
     uint64_t *cnts = nullptr;
-    hipError_t e = hipMallocAsync((void **)&keep, NE, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&cnts, 2 * K * 8, st);
+    hipError_t e = pool_malloc((void **)&keep, NE, st);
+    if (e == hipSuccess) e = pool_malloc((void **)&cnts, 2 * K * 8, st);
     auto release = [&]() {
         if (keep) (void)hipFreeAsync(keep, st);
         if (cnts) (void)hipFreeAsync(cnts, st);
@@ -673,16 +673,16 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     Arena b;
     uint64_t *d_start = nullptr;
     const uint64_t U = std::max<uint64_t>(used, 1), TU = std::max<uint64_t>(tused, 1);
-    e = hipMallocAsync((void **)&d_start, 2 * K * 8, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&b.oc, U * D * 8, st);
-    if (e == hipSuccess && L->sparse) e = hipMallocAsync((void **)&b.mask, U * W * 8, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&b.op_id, U * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void **)&b.txid, U * 8, st);
-    if (e == hipSuccess && !L->tags) e = hipMallocAsync((void **)&b.eff, U * 8, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.tag, U * 4, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.add, U * 8, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.rem_off, U * 4, st);
-    if (e == hipSuccess && L->tags) e = hipMallocAsync((void **)&b.tok, TU * 8, st);
+    e = pool_malloc((void **)&d_start, 2 * K * 8, st);
+    if (e == hipSuccess) e = pool_malloc((void **)&b.oc, U * D * 8, st);
+    if (e == hipSuccess && L->sparse) e = pool_malloc((void **)&b.mask, U * W * 8, st);
+    if (e == hipSuccess) e = pool_malloc((void **)&b.op_id, U * 4, st);
+    if (e == hipSuccess) e = pool_malloc((void **)&b.txid, U * 8, st);
+    if (e == hipSuccess && !L->tags) e = pool_malloc((void **)&b.eff, U * 8, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.tag, U * 4, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.add, U * 8, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.rem_off, U * 4, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.tok, TU * 8, st);
     if (e == hipSuccess)
         e = hipMemcpyAsync(d_start, ns, 2 * K * 8, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) {
@@ -742,20 +742,10 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
 
 int agn_oplog_read(agn_oplog *L, const agn_read *req, agn_result *out, void *stream) {
     if (!L) return fail(AGN_EINVAL, "oplog_read: null oplog");
-    int rc = use_device(L->ctx);
-    if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    {
-        // Read-your-writes: update/2 is a sync_command that precedes the read.
-        std::lock_guard<std::mutex> g(L->wmu);
-        if (!L->s_key.empty() || !L->moves.empty() || !L->dirty_keys.empty()) {
-            std::unique_lock<std::shared_mutex> x(L->rw);
-            rc = do_flush(L, st);
-            if (rc) return rc;
-            AGN_HIP(hipStreamSynchronize(st));
-        }
-    }
-    std::shared_lock<std::shared_mutex> r(L->rw);
+    std::shared_lock<std::shared_mutex> hold;
+    int rc = oplog_begin_read(L, st, 0, nullptr, nullptr, hold);
+    if (rc) return rc;
     agn_log view;
     fill_view(L, &view);
     rc = agn_materialize(L->ctx, &view, req, out, stream);
@@ -767,17 +757,33 @@ int agn_oplog_read(agn_oplog *L, const agn_read *req, agn_result *out, void *str
 }  // extern "C"
 
 namespace agn {
+// Start of a read over the resident log: flushes staged appends
+// (read-your-writes: update/2 is a sync_command that precedes the read),
+// then, still under the writer lock, takes the arena shared in `hold` and
+// writes each requested key's length into lens[n] -- so the lengths are
+// exactly those of the device log the read's kernel will see (a concurrent
+// append only stages on the host; its flush waits for `hold`).
+int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *keys,
+                     uint32_t *lens, std::shared_lock<std::shared_mutex> &hold) {
+    int rc = use_device(L->ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(L->wmu);
+    if (!L->s_key.empty() || !L->moves.empty() || !L->dirty_keys.empty()) {
+        std::unique_lock<std::shared_mutex> x(L->rw);
+        rc = do_flush(L, st);
+        if (rc) return rc;
+        AGN_HIP(hipStreamSynchronize(st));
+    }
+    hold = std::shared_lock<std::shared_mutex>(L->rw);
+    for (uint64_t i = 0; i < n; ++i) lens[i] = L->dlen[keys[i]];
+    return AGN_OK;
+}
+void oplog_view(const agn_oplog *L, agn_log *v) { fill_view(L, v); }
 void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, uint64_t *K) {
     *crdt = L->crdt;
     *D = L->D;
     *sparse = L->sparse;
     *K = L->K;
-}
-// Current length (entries, staged included) of each key: an upper bound on
-// its live set/register pairs for the read that follows.
-void oplog_key_lens(const agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t *out) {
-    std::lock_guard<std::mutex> g(L->wmu);
-    for (uint64_t i = 0; i < n; ++i) out[i] = L->len[keys[i]];
 }
 agn_ctx *oplog_ctx(const agn_oplog *L) { return L->ctx; }
 }  // namespace agn

@@ -155,6 +155,14 @@ const char *agn_strerror(int code);
 int agn_open(int device, agn_ctx **out);
 int agn_close(agn_ctx *ctx);
 int agn_device_count(int *out);
+/* Stream-ordered scratch and op-log arenas come from the library's own
+ * memory pool per device (not the device's default pool, so torch and other
+ * hipMallocAsync users in the process are unaffected).  Freed blocks stay
+ * cached in it for the next GC / ingest (environment AGN_POOL_KEEP = bytes to
+ * keep, default unlimited); agn_pool_trim releases all but keep_bytes of the
+ * cached memory back to the device (after synchronizing it), and closing the
+ * last context of a device trims to 0.  Not part of the reference's API. */
+int agn_pool_trim(agn_ctx *ctx, uint64_t keep_bytes);
 
 /* Device memory helpers (for callers without their own allocator). */
 int agn_dev_alloc(agn_ctx *ctx, size_t bytes, void **out);
