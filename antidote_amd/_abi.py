@@ -159,6 +159,7 @@ PROTOTYPES = {
     "agn_batcher_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "agn_oplog_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                   C.POINTER(C.c_uint64)]),
+    "agn_oplog_key_meta": (C.c_int, [P, C.c_uint64, P, P, P, P]),
     "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),
     "agn_comm_unique_id": (C.c_int, [P]),
     "agn_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -96,6 +97,24 @@ hipError_t pool_of(int dev, hipMemPool_t *out) {
 }  // namespace
 
 hipError_t pool_malloc(void **p, size_t bytes, hipStream_t st) {
+    // test hook: AGN_TEST_POOL_FAIL=n makes the n-th allocation from now fail
+    // (tests/test_oplog.py drives the all-or-nothing paths with it)
+    {
+        static std::mutex mu;
+        static std::string armed;
+        static long left = 0;
+        const char *v = getenv("AGN_TEST_POOL_FAIL");
+        std::lock_guard<std::mutex> g(mu);
+        if (!v) {
+            armed.clear();
+        } else {
+            if (armed != v) {
+                armed = v;
+                left = strtol(v, nullptr, 10);
+            }
+            if (left > 0 && --left == 0) return hipErrorOutOfMemory;
+        }
+    }
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     hipMemPool_t pool = nullptr;

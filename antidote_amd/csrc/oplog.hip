@@ -20,11 +20,19 @@
 // move segments, scatter entries, update key_off/key_len.  The arenas grow by
 // doubling with stream-ordered alloc/copy/free.
 //
-// GC.  agn_oplog_prune runs prune_ops (gc.hip) in two passes around one
-// host step: the mark pass (VC filter) gives each key's kept entry and token
-// counts, the host applies the ETS resize policy (snapshot_insert_gc,
-// :540-558) to size the new segments, and the scatter pass copies the kept
-// entries straight from the old arena into their segments of a fresh one.
+// GC.  agn_oplog_prune is one in-place kernel (gc.hip k_prune_inplace): per
+// selected key the VC filter and the compaction of the kept entries toward
+// the segment start, the new key_len / key_id0 and the ETS ListLen after the
+// resize policy (snapshot_insert_gc, :540-558), all on the device; the
+// per-key lengths come back to the host asynchronously (one D2H into the
+// pinned metadata block) and are settled by the next host-side call.  The
+// physical segments stay where they are; ListLen (`lcap`, what op_insert_gc's
+// GC trigger and the resize policy see) is kept apart from the segment's
+// physical capacity (`cap`).  When the arenas hold more than twice the slots
+// the keys want (segments abandoned by growth moves, halved ListLens), the
+// next prune first re-lays the arenas out (relayout: fresh arenas sized
+// max(ListLen, length) per key, one copy kernel), allocating everything
+// before it changes any state.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -135,16 +143,28 @@ __global__ void __launch_bounds__(256) k_scatter_rows(uint64_t *__restrict__ oc,
     oc[dst[i] * D + (j - i * D)] = rows[j];
 }
 
+constexpr int KV = 5;  // k_keys record: key, start, len, id0, ListLen
 __global__ void __launch_bounds__(256) k_keys(uint64_t *__restrict__ key_off,
                                               uint64_t *__restrict__ key_len,
-                                              uint32_t *__restrict__ key_id0, uint64_t n,
+                                              uint32_t *__restrict__ key_id0,
+                                              uint32_t *__restrict__ key_lcap, uint64_t n,
                                               const uint64_t *__restrict__ kv) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint64_t k = kv[4 * i];
-    key_off[k] = kv[4 * i + 1];
-    key_len[k] = kv[4 * i + 2];
-    key_id0[k] = (uint32_t)kv[4 * i + 3];
+    const uint64_t k = kv[KV * i];
+    key_off[k] = kv[KV * i + 1];
+    key_len[k] = kv[KV * i + 2];
+    key_id0[k] = (uint32_t)kv[KV * i + 3];
+    key_lcap[k] = (uint32_t)kv[KV * i + 4];
+}
+
+// relayout: every key's segment from arena a into fresh arena b (one wave per key)
+__global__ void __launch_bounds__(256) k_relayout(Arena a, Arena b, uint32_t D, uint32_t W,
+                                                  const Move *__restrict__ mv, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const Move m = mv[i];
+    copy_segment(a, b, D, W, m.src, m.dst, m.len, m.tsrc, m.tdst, m.tlen, lane_id());
 }
 
 template <class T>
@@ -182,31 +202,38 @@ struct agn_oplog {
     uint64_t K = 0;
 
     // Locking: `wmu` guards the host side (metadata + staging: append),
-    // `rw` the device arenas — shared by readers (agn_oplog_read) for the
-    // whole of their kernel, exclusive for flush / prune, which move and free
-    // segments.  Order: wmu before rw.
+    // `rw` the device arenas -- shared by readers for the whole of their
+    // kernel, exclusive for flush / prune, which move and free segments.
+    // Order: wmu before rw.
     mutable std::mutex wmu;
     std::shared_mutex rw;
 
     // host metadata per key
-    std::vector<uint64_t> start, tstart;
-    std::vector<uint32_t> cap, len, counter, tcap, tlen;
-    std::vector<uint32_t> dlen, dtlen;  // lengths the device already holds
-    std::vector<uint32_t> id0;          // agn_log.key_id0 of each segment (host copy)
+    std::vector<uint64_t> start, tstart;     // physical segments
+    std::vector<uint32_t> cap, tcap, counter;
+    std::vector<uint32_t> s_cnt, s_tcnt;     // staged (not yet flushed) entries / tokens
+    // pinned [4][K]: length (staged included), token length, ListLen, key_id0;
+    // a prune's D2H lands here directly (settled by the next host call)
+    uint32_t *meta = nullptr;
+    uint32_t *len = nullptr, *tlen = nullptr, *lcap = nullptr, *id0 = nullptr;
     std::vector<uint8_t> dirty;
     std::vector<uint64_t> dirty_keys;
     std::vector<int64_t> move_of;  // index into moves, -1 = none pending
     std::vector<Move> moves;
     uint64_t used = 0, tused = 0;  // arena high-water marks (slots)
+    uint64_t live = 0, tlive = 0;  // slots of the current segments
     uint64_t n_entries = 0, n_tokens = 0;
+    bool relayout_wanted = false;
 
     // device
     Arena a;
     uint64_t dcap = 0, tdcap = 0;  // allocated slots
     uint64_t *key_off = nullptr, *key_len = nullptr;
-    uint32_t *key_id0 = nullptr;  // consecutive-id index, kept with key_off / key_len
-    hipEvent_t up_done = nullptr;
-    bool up_pending = false;
+    uint32_t *key_id0 = nullptr;   // consecutive-id index, kept with key_off / key_len
+    uint32_t *key_lcap = nullptr;  // ListLen (the in-place prune applies the resize policy)
+    uint32_t *d_meta = nullptr;    // [4][K] prune output, copied into `meta`
+    hipEvent_t up_done = nullptr, gc_done = nullptr;
+    bool up_pending = false, gc_pending = false;
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
 
@@ -221,19 +248,47 @@ struct agn_oplog {
 
 namespace {
 
+inline uint32_t dlen_of(const agn_oplog *L, uint64_t k) { return L->len[k] - L->s_cnt[k]; }
+inline uint32_t dtlen_of(const agn_oplog *L, uint64_t k) { return L->tlen[k] - L->s_tcnt[k]; }
+
+// The host side of a prune: wait for its kernel and metadata copy, then the
+// totals and the relayout check (arenas holding more than twice the slots
+// the keys want).
+int settle(agn_oplog *L) {
+    if (!L->gc_pending) return AGN_OK;
+    L->gc_pending = false;
+    AGN_HIP(hipEventSynchronize(L->gc_done));
+    uint64_t ne = 0, nt = 0, want = 0;
+    for (uint64_t k = 0; k < L->K; ++k) {
+        ne += L->len[k];
+        nt += L->tlen[k];
+        if (L->cap[k]) want += (uint64_t)std::max(L->lcap[k], L->len[k]) + 1;
+    }
+    L->n_entries = ne;
+    L->n_tokens = nt;
+    L->relayout_wanted = L->used > 2 * want + 1024 || (L->tags && L->tused > 2 * nt + 1024 + 16 * L->K);
+    return AGN_OK;
+}
+
 void oplog_new_segment(agn_oplog *L, uint64_t k, uint32_t need, uint32_t tneed) {
-    // Entry segment.
+    // ListLen: the ETS tuple starts with init_slots (OPS_THRESHOLD) and
+    // doubles while full (the engine grows instead of forcing the GC read)
+    uint32_t lc = L->lcap[k] ? L->lcap[k] : L->init_slots;
+    while (lc < need) lc *= 2;
+    L->lcap[k] = lc;
+    // Physical entry segment: a new one at the arena's end when too small.
     if (need > L->cap[k]) {
-        uint32_t c = L->cap[k] ? L->cap[k] : L->init_slots;
-        while (c < need) c *= 2;
+        const uint32_t c = std::max(lc, need);
         const uint64_t old = L->start[k];
+        L->live += (uint64_t)c + 1 - (L->cap[k] ? (uint64_t)L->cap[k] + 1 : 0);
         L->start[k] = L->used;
         L->used += (uint64_t)c + 1;
         L->cap[k] = c;
-        if (L->dlen[k] || L->dtlen[k] || L->move_of[k] >= 0) {
+        const uint32_t dl = dlen_of(L, k), dt = dtlen_of(L, k);
+        if (dl || dt || L->move_of[k] >= 0) {
             if (L->move_of[k] < 0) {
                 L->move_of[k] = (int64_t)L->moves.size();
-                L->moves.push_back(Move{old, 0, L->tstart[k], 0, L->dlen[k], L->dtlen[k]});
+                L->moves.push_back(Move{old, 0, L->tstart[k], 0, dl, dt});
             }
         }
     }
@@ -241,13 +296,15 @@ void oplog_new_segment(agn_oplog *L, uint64_t k, uint32_t need, uint32_t tneed) 
         uint32_t c = L->tcap[k] ? L->tcap[k] : 16u;
         while (c < tneed) c *= 2;
         const uint64_t old = L->tstart[k];
+        L->tlive += c - L->tcap[k];
         L->tstart[k] = L->tused;
         L->tused += c;
         L->tcap[k] = c;
-        if (L->dlen[k] || L->dtlen[k] || L->move_of[k] >= 0) {
+        const uint32_t dl = dlen_of(L, k), dt = dtlen_of(L, k);
+        if (dl || dt || L->move_of[k] >= 0) {
             if (L->move_of[k] < 0) {
                 L->move_of[k] = (int64_t)L->moves.size();
-                L->moves.push_back(Move{L->start[k], 0, old, 0, L->dlen[k], L->dtlen[k]});
+                L->moves.push_back(Move{L->start[k], 0, old, 0, dl, dt});
             }
         }
     }
@@ -261,6 +318,7 @@ int ensure_pinned(agn_oplog *L, size_t bytes) {
     if (bytes <= L->pinned_bytes) return AGN_OK;
     if (L->pinned) AGN_HIP(hipHostFree(L->pinned));
     L->pinned = nullptr;
+    L->pinned_bytes = 0;
     size_t b = std::max<size_t>(bytes, 2 * L->pinned_bytes);
     AGN_HIP(hipHostMalloc(&L->pinned, b, hipHostMallocDefault));
     L->pinned_bytes = b;
@@ -340,7 +398,7 @@ int do_flush(agn_oplog *L, hipStream_t st) {
                  o_tlen = slot(n * 4), o_opid = slot(n * 4), o_tag = slot(L->tags ? n * 4 : 0),
                  o_eff = slot(L->tags ? 0 : n * 8), o_oc = slot(n * D * 8),
                  o_mask = slot(L->sparse ? n * W * 8 : 0), o_tok = slot(L->s_tok.size() * 8),
-                 o_keys = slot(nk * 32);
+                 o_keys = slot(nk * KV * 8);
     rc = ensure_pinned(L, off);
     if (rc) return rc;
     char *h = (char *)L->pinned;
@@ -365,10 +423,11 @@ int do_flush(agn_oplog *L, hipStream_t st) {
         uint64_t *kv = (uint64_t *)(h + o_keys);
         for (uint64_t j = 0; j < nk; ++j) {
             const uint64_t k = L->dirty_keys[j];
-            kv[4 * j] = k;
-            kv[4 * j + 1] = L->start[k];
-            kv[4 * j + 2] = L->len[k];
-            kv[4 * j + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
+            kv[KV * j] = k;
+            kv[KV * j + 1] = L->start[k];
+            kv[KV * j + 2] = L->len[k];
+            kv[KV * j + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
+            kv[KV * j + 4] = L->lcap[k];
         }
     }
     char *d = nullptr;
@@ -391,12 +450,13 @@ int do_flush(agn_oplog *L, hipStream_t st) {
     }
     if (nk)
         k_keys<<<(unsigned)((nk + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, L->key_id0,
-                                                              nk, (const uint64_t *)(d + o_keys));
+                                                              L->key_lcap, nk,
+                                                              (const uint64_t *)(d + o_keys));
     AGN_HIP(hipGetLastError());
     AGN_HIP(hipFreeAsync(d, st));
     for (uint64_t k : L->dirty_keys) {
-        L->dlen[k] = L->len[k];
-        L->dtlen[k] = L->tlen[k];
+        L->s_cnt[k] = 0;
+        L->s_tcnt[k] = 0;
         L->dirty[k] = 0;
         L->move_of[k] = -1;
     }
@@ -410,12 +470,98 @@ int do_flush(agn_oplog *L, hipStream_t st) {
     return AGN_OK;
 }
 
-// snapshot_insert_gc's NewListLen (src/materializer_vnode.erl:540-558).
-uint32_t resize_list_len(uint32_t new_len, uint32_t list_len) {
-    if ((int64_t)new_len > (int64_t)list_len - AGN_RESIZE_THRESHOLD) return list_len * 2;
-    const uint32_t half = list_len / 2;
-    if (half <= AGN_OPS_THRESHOLD) return list_len;
-    return ((int64_t)half - AGN_RESIZE_THRESHOLD > (int64_t)new_len) ? half : list_len;
+// Fresh arenas sized max(ListLen, length) + 1 per key (token segments
+// max(16, token length)) and one copy kernel.  Every allocation happens
+// before any state changes: on failure the log is left exactly as it was
+// (the caller treats relayout as an optimisation).  Requires a flushed,
+// settled log.
+int relayout(agn_oplog *L, hipStream_t st) {
+    const uint64_t K = L->K;
+    std::vector<uint64_t> ns(K), nts(K);
+    std::vector<uint32_t> nc(K), ntc(K);
+    std::vector<Move> mv;
+    uint64_t used = 0, tused = 0;
+    for (uint64_t k = 0; k < K; ++k) {
+        nc[k] = L->cap[k] ? std::max(L->lcap[k], L->len[k]) : 0u;
+        if (nc[k] == 0 && L->cap[k]) nc[k] = 1;
+        ntc[k] = L->tags && L->tcap[k] ? std::max<uint32_t>(16u, L->tlen[k]) : 0u;
+        ns[k] = nc[k] ? used : 0;
+        nts[k] = tused;
+        if (nc[k]) used += (uint64_t)nc[k] + 1;
+        tused += ntc[k];
+        if (L->cap[k] || L->tcap[k])
+            mv.push_back(Move{L->start[k], ns[k], L->tstart[k], nts[k], L->len[k], L->tlen[k]});
+    }
+    const uint64_t U = std::max<uint64_t>(used, 1), TU = std::max<uint64_t>(tused, 1);
+    Arena b;
+    Move *d_mv = nullptr;
+    uint64_t *d_kv = nullptr;
+    hipError_t e = pool_malloc(&b.oc, U * L->D * 8, st);
+    if (e == hipSuccess && L->sparse) e = pool_malloc(&b.mask, U * L->W * 8, st);
+    if (e == hipSuccess) e = pool_malloc(&b.op_id, U * 4, st);
+    if (e == hipSuccess) e = pool_malloc(&b.txid, U * 8, st);
+    if (e == hipSuccess && !L->tags) e = pool_malloc(&b.eff, U * 8, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc(&b.tag, U * 4, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc(&b.add, U * 8, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc(&b.rem_off, U * 4, st);
+    if (e == hipSuccess && L->tags) e = pool_malloc(&b.tok, TU * 8, st);
+    if (e == hipSuccess) e = pool_malloc(&d_mv, std::max<size_t>(mv.size(), 1) * sizeof(Move), st);
+    if (e == hipSuccess) e = pool_malloc(&d_kv, std::max<uint64_t>(K, 1) * KV * 8, st);
+    int rc = AGN_OK;
+    if (e == hipSuccess) rc = ensure_pinned(L, mv.size() * sizeof(Move) + K * KV * 8);
+    auto drop = [&]() {
+        for (void *p : {(void *)b.oc, (void *)b.mask, (void *)b.op_id, (void *)b.txid,
+                        (void *)b.eff, (void *)b.tag, (void *)b.add, (void *)b.rem_off,
+                        (void *)b.tok, (void *)d_mv, (void *)d_kv})
+            if (p) (void)hipFreeAsync(p, st);
+    };
+    if (e != hipSuccess || rc != AGN_OK) {
+        drop();
+        return fail(AGN_ENOMEM, "oplog relayout: %s", e != hipSuccess ? hipGetErrorString(e) : "staging");
+    }
+    char *h = (char *)L->pinned;
+    std::memcpy(h, mv.data(), mv.size() * sizeof(Move));
+    uint64_t *kv = (uint64_t *)(h + mv.size() * sizeof(Move));
+    for (uint64_t k = 0; k < K; ++k) {
+        kv[KV * k] = k;
+        kv[KV * k + 1] = ns[k];
+        kv[KV * k + 2] = L->len[k];
+        kv[KV * k + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
+        kv[KV * k + 4] = L->lcap[k];
+    }
+    e = hipMemcpyAsync(d_mv, h, mv.size() * sizeof(Move), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_kv, kv, K * KV * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && !mv.empty())
+        k_relayout<<<(unsigned)((mv.size() + 3) / 4), 256, 0, st>>>(L->a, b, L->D, L->W, d_mv,
+                                                                    mv.size());
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) {
+        drop();
+        return fail(AGN_EHIP, "oplog relayout: %s", hipGetErrorString(e));
+    }
+    // commit: the new key_off (the copy above read the old arena first)
+    if (K)
+        k_keys<<<(unsigned)((K + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, L->key_id0,
+                                                             L->key_lcap, K, d_kv);
+    (void)hipEventRecord(L->up_done, st);
+    L->up_pending = true;
+    (void)hipFreeAsync(d_mv, st);
+    (void)hipFreeAsync(d_kv, st);
+    Arena &a = L->a;
+    for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
+                    (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok})
+        if (p) (void)hipFreeAsync(p, st);
+    L->a = b;
+    L->dcap = U;
+    L->tdcap = L->tags ? TU : 0;
+    L->used = L->live = used;
+    L->tused = L->tlive = tused;
+    L->start.swap(ns);
+    L->tstart.swap(nts);
+    L->cap.swap(nc);
+    L->tcap.swap(ntc);
+    L->relayout_wanted = false;
+    return AGN_OK;
 }
 
 }  // namespace
@@ -445,9 +591,7 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
     try {
         L->start.assign(n_keys, 0);
         L->tstart.assign(n_keys, 0);
-        for (auto *v : {&L->cap, &L->len, &L->counter, &L->tcap, &L->tlen, &L->dlen, &L->dtlen})
-            v->assign(n_keys, 0);
-        L->id0.assign(n_keys, AGN_ID0_NONE);
+        for (auto *v : {&L->cap, &L->tcap, &L->counter, &L->s_cnt, &L->s_tcnt}) v->assign(n_keys, 0);
         L->dirty.assign(n_keys, 0);
         L->move_of.assign(n_keys, -1);
     } catch (...) {
@@ -455,13 +599,27 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
         return fail(AGN_ENOMEM, "oplog_create: host metadata for %llu keys",
                     (unsigned long long)n_keys);
     }
-    hipError_t e = hipMalloc((void **)&L->key_off, std::max<uint64_t>(n_keys, 1) * 8);
-    if (e == hipSuccess) e = hipMalloc((void **)&L->key_len, std::max<uint64_t>(n_keys, 1) * 8);
-    if (e == hipSuccess) e = hipMemset(L->key_off, 0, std::max<uint64_t>(n_keys, 1) * 8);
-    if (e == hipSuccess) e = hipMemset(L->key_len, 0, std::max<uint64_t>(n_keys, 1) * 8);
-    if (e == hipSuccess) e = hipMalloc((void **)&L->key_id0, std::max<uint64_t>(n_keys, 1) * 4);
-    if (e == hipSuccess) e = hipMemset(L->key_id0, 0xff, std::max<uint64_t>(n_keys, 1) * 4);
+    const uint64_t K1 = std::max<uint64_t>(n_keys, 1);
+    hipError_t e = hipHostMalloc((void **)&L->meta, 4 * K1 * 4, hipHostMallocDefault);
+    if (e == hipSuccess) {
+        L->len = L->meta;
+        L->tlen = L->meta + K1;
+        L->lcap = L->meta + 2 * K1;
+        L->id0 = L->meta + 3 * K1;
+        std::memset(L->meta, 0, 3 * K1 * 4);
+        for (uint64_t k = 0; k < K1; ++k) L->id0[k] = AGN_ID0_NONE;
+    }
+    if (e == hipSuccess) e = hipMalloc((void **)&L->key_off, K1 * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->key_len, K1 * 8);
+    if (e == hipSuccess) e = hipMemset(L->key_off, 0, K1 * 8);
+    if (e == hipSuccess) e = hipMemset(L->key_len, 0, K1 * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->key_id0, K1 * 4);
+    if (e == hipSuccess) e = hipMemset(L->key_id0, 0xff, K1 * 4);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->key_lcap, K1 * 4);
+    if (e == hipSuccess) e = hipMemset(L->key_lcap, 0, K1 * 4);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->d_meta, 4 * K1 * 4);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L->up_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L->gc_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         agn_oplog_destroy(L);
         return fail(AGN_ENOMEM, "oplog_create: device key arrays");
@@ -477,10 +635,13 @@ int agn_oplog_destroy(agn_oplog *L) {
     Arena &a = L->a;
     for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
                     (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok,
-                    (void *)L->key_off, (void *)L->key_len, (void *)L->key_id0})
+                    (void *)L->key_off, (void *)L->key_len, (void *)L->key_id0,
+                    (void *)L->key_lcap, (void *)L->d_meta})
         if (p) (void)hipFree(p);
     if (L->pinned) (void)hipHostFree(L->pinned);
+    if (L->meta) (void)hipHostFree(L->meta);
     if (L->up_done) (void)hipEventDestroy(L->up_done);
+    if (L->gc_done) (void)hipEventDestroy(L->gc_done);
     delete L;
     return AGN_OK;
 }
@@ -500,6 +661,8 @@ int agn_oplog_append(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint8
     if (!L) return fail(AGN_EINVAL, "oplog_append: null oplog");
     if (n == 0) return AGN_OK;
     std::lock_guard<std::mutex> g(L->wmu);
+    int rc = settle(L);
+    if (rc) return rc;
     try {
         return oplog_append_locked(L, n, keys, same_op, oc, oc_mask, txid, eff, tag, add_tok,
                                    rem_off, rem_tok, out_op_id, out_gc_due);
@@ -537,7 +700,7 @@ static int oplog_append_locked(agn_oplog *L, uint64_t n, const uint64_t *keys,
         if (out_op_id) out_op_id[i] = id;
         if (out_gc_due)
             out_gc_due[i] = !(same_op && same_op[i]) &&
-                            (L->len[k] >= std::max(L->cap[k], L->init_slots) ||
+                            (L->len[k] >= std::max(L->lcap[k], L->init_slots) ||
                              id % AGN_OPS_THRESHOLD == 0);
         const uint32_t tl = L->tags ? rem_off[i + 1] - rem_off[i] : 0u;
         oplog_new_segment(L, k, L->len[k] + 1, L->tlen[k] + tl);
@@ -568,7 +731,9 @@ static int oplog_append_locked(agn_oplog *L, uint64_t n, const uint64_t *keys,
             L->id0[k] = AGN_ID0_NONE;
         if (id == AGN_ID0_NONE) L->id0[k] = AGN_ID0_NONE;
         ++L->len[k];
+        ++L->s_cnt[k];
         L->tlen[k] += tl;
+        L->s_tcnt[k] += tl;
         if (!L->dirty[k]) {
             L->dirty[k] = 1;
             L->dirty_keys.push_back(k);
@@ -585,7 +750,13 @@ int agn_oplog_flush(agn_oplog *L, agn_log *view, void *stream) {
     if (rc) return rc;
     std::lock_guard<std::mutex> g(L->wmu);
     std::unique_lock<std::shared_mutex> x(L->rw);
-    rc = do_flush(L, (hipStream_t)stream);
+    rc = settle(L);
+    if (rc) return rc;
+    try {
+        rc = do_flush(L, (hipStream_t)stream);
+    } catch (const std::bad_alloc &) {
+        rc = fail(AGN_ENOMEM, "oplog_flush: host staging");
+    }
     if (rc) return rc;
     // Readers on other streams must see the scattered entries.
     AGN_HIP(hipStreamSynchronize((hipStream_t)stream));
@@ -603,140 +774,31 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     std::lock_guard<std::mutex> g(L->wmu);
     std::unique_lock<std::shared_mutex> x(L->rw);
     hipStream_t st = (hipStream_t)stream;
-    rc = do_flush(L, st);
+    rc = settle(L);
+    if (rc) return rc;
+    try {
+        rc = do_flush(L, st);
+        if (rc == AGN_OK && L->relayout_wanted) {
+            // an optimisation: on failure the log stays as it is (fragmented)
+            const int r2 = relayout(L, st);
+            (void)r2;
+        }
+    } catch (const std::bad_alloc &) {
+        rc = fail(AGN_ENOMEM, "oplog_prune: host staging");
+    }
     if (rc) return rc;
     if (L->K == 0) return AGN_OK;
-    // keep bytes are indexed by arena position: the view's n_entries = used
-    const uint64_t K = L->K, NE = std::max<uint64_t>(L->used, 1);
-    const uint32_t D = L->D, W = L->W;
-    if (L->used > 0x7fffffffull) return fail(AGN_ENOTSUP, "oplog_prune: log too large for one pass");
+    if (L->used > 0xffffffffull) return fail(AGN_ENOTSUP, "oplog_prune: arena beyond 2^32 slots");
     agn_log view;
     fill_view(L, &view);
-    // 1. mark pass (prune_ops' VC filter): keep byte per entry, kept entry and
-    //    token counts per key.
-    uint8_t *keep = nullptr;
-    uint64_t *cnts = nullptr;
-    hipError_t e = pool_malloc((void **)&keep, NE, st);
-    if (e == hipSuccess) e = pool_malloc((void **)&cnts, 2 * K * 8, st);
-    auto release = [&]() {
-        if (keep) (void)hipFreeAsync(keep, st);
-        if (cnts) (void)hipFreeAsync(cnts, st);
-    };
-    if (e != hipSuccess) {
-        release();
-        return fail(AGN_ENOMEM, "oplog_prune: scratch");
-    }
-    rc = launch_prune_mark(view, prune, threshold, threshold_mask, keep, cnts, cnts + K, st);
-    if (rc) {
-        release();
-        return rc;
-    }
-    // 2. read back the counts and which keys were collected.  Host staging
-    //    in the log's pinned buffer: counts | new starts | new key_off, len.
-    rc = ensure_pinned(L, 6 * K * 8);
-    if (rc) {
-        release();
-        return rc;
-    }
-    uint64_t *nlen = (uint64_t *)L->pinned, *ns = nlen + 2 * K, *kv = ns + 2 * K;
-    std::vector<uint8_t> pr(prune ? K : 0);
-    e = hipMemcpyAsync(nlen, cnts, 2 * K * 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess && prune) e = hipMemcpyAsync(pr.data(), prune, K, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) {
-        release();
-        return fail(AGN_EHIP, "oplog_prune: read back: %s", hipGetErrorString(e));
-    }
-    if (!L->tags)
-        for (uint64_t k = 0; k < K; ++k) nlen[K + k] = 0;
-    // 3. new segments (resize policy on the collected keys), fresh arena.
-    uint64_t used = 0, tused = 0, ne = 0, nt = 0;
-    for (uint64_t k = 0; k < K; ++k) {
-        const uint32_t l = (uint32_t)nlen[k], tl = (uint32_t)nlen[K + k];
-        if ((!prune || pr[k]) && L->cap[k]) L->cap[k] = resize_list_len(l, L->cap[k]);
-        if (L->tags && (!prune || pr[k]) && L->tcap[k])
-            L->tcap[k] = std::max<uint32_t>(16u, std::max(tl, std::min(L->tcap[k], 2 * tl)));
-        if (L->cap[k] && L->cap[k] < l) L->cap[k] = l;  // never below the kept length
-        ns[k] = L->cap[k] ? used : ~0ull;
-        ns[K + k] = L->tcap[k] ? tused : 0;
-        kv[k] = L->cap[k] ? used : 0ull;
-        kv[K + k] = L->cap[k] ? l : 0u;
-        if (L->cap[k]) used += (uint64_t)L->cap[k] + 1;
-        tused += L->tcap[k];
-        L->len[k] = L->dlen[k] = l;
-        L->tlen[k] = L->dtlen[k] = tl;
-        ne += l;
-        nt += tl;
-    }
-    for (uint64_t k = 0; k < K; ++k) L->start[k] = L->cap[k] ? ns[k] : 0;
-    L->tstart.assign(ns + K, ns + 2 * K);
-    Arena b;
-    uint64_t *d_start = nullptr;
-    const uint64_t U = std::max<uint64_t>(used, 1), TU = std::max<uint64_t>(tused, 1);
-    e = pool_malloc((void **)&d_start, 2 * K * 8, st);
-    if (e == hipSuccess) e = pool_malloc((void **)&b.oc, U * D * 8, st);
-    if (e == hipSuccess && L->sparse) e = pool_malloc((void **)&b.mask, U * W * 8, st);
-    if (e == hipSuccess) e = pool_malloc((void **)&b.op_id, U * 4, st);
-    if (e == hipSuccess) e = pool_malloc((void **)&b.txid, U * 8, st);
-    if (e == hipSuccess && !L->tags) e = pool_malloc((void **)&b.eff, U * 8, st);
-    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.tag, U * 4, st);
-    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.add, U * 8, st);
-    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.rem_off, U * 4, st);
-    if (e == hipSuccess && L->tags) e = pool_malloc((void **)&b.tok, TU * 8, st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d_start, ns, 2 * K * 8, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) {
-        release();
-        return fail(AGN_ENOMEM, "oplog_prune: new arena");
-    }
-    // 4. scatter the kept entries straight into their new segments, then the
-    //    new key_off / key_len (the old view is read by the scatter first).
-    agn_log out;
-    std::memset(&out, 0, sizeof out);
-    out.key_off = d_start;
-    out.oc = b.oc;
-    out.oc_mask = b.mask;
-    out.op_id = b.op_id;
-    out.txid = b.txid;
-    out.eff = b.eff;
-    out.tag = b.tag;
-    out.add_tok = b.add;
-    out.rem_off = b.rem_off;
-    out.rem_tok = b.tok;
-    rc = launch_prune_scatter_seg(view, out, prune, keep, d_start + K, out_flags, st);
-    if (rc) e = hipErrorLaunchFailure;
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(L->key_off, kv, K * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(L->key_len, kv + K, K * 8, hipMemcpyHostToDevice, st);
-    // pruning leaves id gaps: rebuild the consecutive-id index of every key
-    if (e == hipSuccess) {
-        agn_log nv;
-        std::memset(&nv, 0, sizeof nv);
-        nv.n_keys = K;
-        nv.key_off = L->key_off;
-        nv.key_len = L->key_len;
-        nv.op_id = b.op_id;
-        if (launch_index_ids(nv, L->key_id0, st) != AGN_OK) e = hipErrorLaunchFailure;
-    }
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(L->id0.data(), L->key_id0, K * 4, hipMemcpyDeviceToHost, st);
-    // the pinned staging (ns, kv) must not be reused before the copies land
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFreeAsync(d_start, st);
-    release();
-    Arena &a = L->a;
-    for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
-                    (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok})
-        if (p) (void)hipFreeAsync(p, st);
-    L->a = b;
-    L->dcap = U;
-    L->tdcap = L->tags ? TU : 0;
-    L->used = used;
-    L->tused = tused;
-    L->n_entries = ne;
-    L->n_tokens = nt;
-    if (e != hipSuccess) return fail(AGN_EHIP, "oplog_prune: %s", hipGetErrorString(e));
+    rc = launch_prune_inplace(view, L->key_len, L->key_id0, L->key_lcap, prune, threshold,
+                              threshold_mask, L->d_meta, out_flags, st);
+    if (rc) return rc;
+    // the host's copy of {len, token len, ListLen, id0}: settled by the next call
+    AGN_HIP(hipMemcpyAsync(L->meta, L->d_meta, 4 * std::max<uint64_t>(L->K, 1) * 4,
+                           hipMemcpyDeviceToHost, st));
+    AGN_HIP(hipEventRecord(L->gc_done, st));
+    L->gc_pending = true;
     return AGN_OK;
 }
 
@@ -754,6 +816,37 @@ int agn_oplog_read(agn_oplog *L, const agn_read *req, agn_result *out, void *str
     return AGN_OK;
 }
 
+int agn_oplog_stats(const agn_oplog *Lc, uint64_t *entries, uint64_t *slots, uint64_t *tokens) {
+    if (!Lc) return fail(AGN_EINVAL, "oplog_stats: null oplog");
+    agn_oplog *L = const_cast<agn_oplog *>(Lc);
+    std::lock_guard<std::mutex> g(L->wmu);
+    int rc = settle(L);
+    if (rc) return rc;
+    if (entries) *entries = L->n_entries;
+    if (slots) *slots = L->used;
+    if (tokens) *tokens = L->n_tokens;
+    return AGN_OK;
+}
+
+int agn_oplog_key_meta(agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t *out_len,
+                       uint32_t *out_list_len, uint32_t *out_counter) {
+    if (!L) return fail(AGN_EINVAL, "oplog_key_meta: null oplog");
+    if (n && !keys) return fail(AGN_EINVAL, "oplog_key_meta: null keys");
+    std::lock_guard<std::mutex> g(L->wmu);
+    int rc = settle(L);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (keys[i] >= L->K)
+            return fail(AGN_EINVAL, "oplog_key_meta: key %llu >= n_keys", (unsigned long long)keys[i]);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t k = keys[i];
+        if (out_len) out_len[i] = L->len[k];
+        if (out_list_len) out_list_len[i] = L->lcap[k];
+        if (out_counter) out_counter[i] = L->counter[k];
+    }
+    return AGN_OK;
+}
+
 }  // extern "C"
 
 namespace agn {
@@ -768,14 +861,20 @@ int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *k
     int rc = use_device(L->ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(L->wmu);
+    rc = settle(L);  // a prune's kernel precedes every later read
+    if (rc) return rc;
     if (!L->s_key.empty() || !L->moves.empty() || !L->dirty_keys.empty()) {
         std::unique_lock<std::shared_mutex> x(L->rw);
-        rc = do_flush(L, st);
+        try {
+            rc = do_flush(L, st);
+        } catch (const std::bad_alloc &) {
+            rc = fail(AGN_ENOMEM, "oplog read: host staging");
+        }
         if (rc) return rc;
         AGN_HIP(hipStreamSynchronize(st));
     }
     hold = std::shared_lock<std::shared_mutex>(L->rw);
-    for (uint64_t i = 0; i < n; ++i) lens[i] = L->dlen[keys[i]];
+    for (uint64_t i = 0; i < n; ++i) lens[i] = dlen_of(L, keys[i]);
     return AGN_OK;
 }
 void oplog_view(const agn_oplog *L, agn_log *v) { fill_view(L, v); }
@@ -787,16 +886,3 @@ void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, u
 }
 agn_ctx *oplog_ctx(const agn_oplog *L) { return L->ctx; }
 }  // namespace agn
-
-extern "C" {
-
-int agn_oplog_stats(const agn_oplog *L, uint64_t *entries, uint64_t *slots, uint64_t *tokens) {
-    if (!L) return fail(AGN_EINVAL, "oplog_stats: null oplog");
-    std::lock_guard<std::mutex> g(L->wmu);
-    if (entries) *entries = L->n_entries;
-    if (slots) *slots = L->used;
-    if (tokens) *tokens = L->n_tokens;
-    return AGN_OK;
-}
-
-}  // extern "C"

@@ -352,6 +352,16 @@ class OpLog:
         check(self.eng.lib.agn_oplog_stats(self.h, C.byref(e), C.byref(s), C.byref(t)))
         return {"entries": e.value, "slots": s.value, "tokens": t.value}
 
+    def key_meta(self, keys=None):
+        """Per key: (Length, ListLen, op counter) of the ETS tuple it mirrors."""
+        keys = np.arange(self.n_keys, dtype=np.uint64) if keys is None else \
+            np.ascontiguousarray(keys, np.uint64)
+        n = len(keys)
+        ln, ll, ct = (np.zeros(n, np.uint32) for _ in range(3))
+        check(self.eng.lib.agn_oplog_key_meta(self.h, n, _ptr(keys), _ptr(ln), _ptr(ll), _ptr(ct)),
+              "agn_oplog_key_meta")
+        return ln, ll, ct
+
 
 class Batcher:
     """agn_batcher: per-key materializer_vnode:read/6 calls from many threads

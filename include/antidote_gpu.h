@@ -261,13 +261,25 @@ int agn_oplog_flush(agn_oplog *log, agn_log *view, void *stream);
 /* GC of the resident log: snapshot_insert_gc's prune_ops for every key with
  * prune[k] != 0 (device arrays, e.g. from agn_ss_store), then the ETS resize
  * policy (:540-560: ListLen doubles when fewer than RESIZE_THRESHOLD slots
- * stay free, halves when that leaves room and stays above OPS_THRESHOLD).
- * Flushes first and synchronises `stream` (the new lengths are read back).
- * out_flags (device, may be NULL) as agn_prune_ops. */
+ * stay free, halves when that leaves room and stays above OPS_THRESHOLD;
+ * prune_ops' NewLength counts 1 when nothing survives, :580-583).  One
+ * in-place kernel on `stream` (unselected keys cost nothing); flushes first,
+ * does not block: the new per-key lengths reach the host asynchronously and
+ * every later call on this log (append, flush, read, stats) waits for them,
+ * so reads on any stream see the pruned log.  When the arenas hold more than
+ * twice the slots the keys want, the call first re-lays them out into fresh
+ * arenas (allocating everything before changing anything; skipped if memory
+ * is short).  out_flags (device, may be NULL) as agn_prune_ops. */
 int agn_oplog_prune(agn_oplog *log, const uint8_t *prune, const uint64_t *threshold,
                     const uint64_t *threshold_mask, uint32_t *out_flags, void *stream);
 /* Host-side accounting: entries in use, allocated slots, removal tokens. */
 int agn_oplog_stats(const agn_oplog *log, uint64_t *entries, uint64_t *slots, uint64_t *tokens);
+/* Per key (host arrays, each may be NULL): its entries (staged included) =
+ * the ETS tuple's Length, its ListLen (0 = never written; what op_insert_gc's
+ * GC trigger and the resize policy see) and its op counter (element 3,
+ * :630) -- the {Length, ListLen} / OpId of deconstruct_opscache_entry (:614). */
+int agn_oplog_key_meta(agn_oplog *log, uint64_t n, const uint64_t *keys, uint32_t *out_len,
+                       uint32_t *out_list_len, uint32_t *out_counter);
 /* Batched materialize/4 over the oplog's current contents (req / out as
  * agn_materialize, device pointers, req->keys indexing the oplog's keys).
  * Staged appends are flushed first (read-your-writes: update/2 is a

@@ -320,3 +320,146 @@ def test_oplog_gc_due_and_errors(eng):
         assert ids.tolist() == [1, 1, 121]
         view = ol.flush()
         assert dl(eng, view.key_len, np.uint64, 4).tolist() == [121, 2, 0, 0]
+
+
+def new_list_len(new_length, list_len):
+    """snapshot_insert_gc's NewListLen (src/materializer_vnode.erl:540-558)."""
+    if new_length > list_len - _abi.RESIZE_THRESHOLD:
+        return list_len * 2
+    half = list_len // 2
+    if half <= _abi.OPS_THRESHOLD:
+        return list_len
+    return half if half - _abi.RESIZE_THRESHOLD > new_length else list_len
+
+
+def expected_meta(before, prune, kept):
+    """Per key {Length, ListLen, OpId} after a prune: selected keys get the
+    kept length and the resized ListLen (prune_ops' NewLength is 1 when no op
+    survives, :580-583), the others and every op counter are unchanged."""
+    ln, ll, ct = (x.copy() for x in before)
+    for k in range(len(ln)):
+        if prune[k]:
+            ln[k] = kept[k]
+            if ll[k]:
+                ll[k] = max(new_list_len(max(int(kept[k]), 1), int(ll[k])), int(kept[k]))
+    return ln, ll, ct
+
+
+def check_segments(eng, view, want, K, D, W, tags, sparse):
+    segs = segments(eng, view, K, D, W, tags, sparse)
+    for k in range(K):
+        w = csr_key(want, k, tags)
+        for name, v in w.items():
+            g = segs[k][name]
+            if name == "rems":
+                assert g == v, (k, name)
+            else:
+                assert np.array_equal(np.asarray(g), np.asarray(v)), (k, name)
+
+
+@pytest.mark.parametrize("crdt,D,sparse", [(_abi.COUNTER_PN, 8, False), (_abi.SET_AW, 12, True),
+                                           (_abi.REGISTER_MV, 3, False)])
+def test_oplog_resize_policy_and_relayout(eng, oracle_lib, monkeypatch, crdt, D, sparse):
+    """The ETS resize policy after a prune (ListLen doubles / halves / stays,
+    per key, against the reference's NewListLen), then the relayout of the
+    fragmented arenas: refused once by a forced allocation failure (the log
+    must come through unchanged and correct), done on the next prune; the
+    log stays bit-exact and appendable throughout."""
+    rng = np.random.default_rng(77 + D + crdt)
+    tags = crdt != _abi.COUNTER_PN
+    W = (D + 63) // 64
+    K = 120
+    log, req, _ = random_case(31 * D + crdt, crdt, K, D, 260, sparse=sparse,
+                              multi=0.2 if crdt == _abi.SET_AW else 0.0, empty=0.05)
+    with OpLog(eng, crdt, D, K, sparse=sparse, init_slots=1) as ol:
+        got = append_ops(ol, log, interleave(rng, ops_of(log)), rng, flush_p=0.2)
+        log2 = renumbered(log, got)
+        before = ol.key_meta()
+        prune, thr, tm = thresholds(3 * D + crdt, log2, sparse)
+        want, wflags, n_out = oracle_prune(oracle_lib, log2, prune, thr, tm)
+        kept = np.diff(want["key_off"]).astype(np.int64)
+        bp, bt = eng.upload(prune), eng.upload(thr)
+        btm = eng.upload(tm) if tm is not None else None
+        fl = eng.empty(4 * K)
+        ol.prune(bp.ptr, bt.ptr, btm.ptr if btm else None, fl.ptr)
+        after = ol.key_meta()
+        exp = expected_meta(before, prune, kept)
+        for name, g, w in zip(("Length", "ListLen", "OpId"), after, exp):
+            assert np.array_equal(g, w), (name, np.flatnonzero(g != w)[:5])
+        assert (after[1] != before[1]).any()
+        assert np.array_equal(eng.download(fl, np.uint32, (K,)), wflags)
+        slots0 = ol.stats()["slots"]
+        # a prune selecting nothing: the relayout is wanted, its first
+        # allocation fails -> skipped, the log is untouched
+        none = eng.upload(np.zeros(K, np.uint8))
+        monkeypatch.setenv("AGN_TEST_POOL_FAIL", "1")
+        ol.prune(none.ptr, bt.ptr, btm.ptr if btm else None)
+        monkeypatch.delenv("AGN_TEST_POOL_FAIL")
+        assert ol.stats()["slots"] == slots0
+        view = ol.flush()
+        check_segments(eng, view, want, K, D, W, tags, sparse)
+        # the next prune re-lays the arenas out
+        ol.prune(none.ptr, bt.ptr, btm.ptr if btm else None)
+        assert ol.stats()["slots"] < slots0 // 2 + 1, (ol.stats()["slots"], slots0)
+        assert all(np.array_equal(a, b) for a, b in zip(ol.key_meta(), after))
+        view = ol.flush()
+        check_id_index(eng, view, K)
+        check_segments(eng, view, want, K, D, W, tags, sparse)
+        # appends past the shrunk ListLens, then a full materialize
+        more, req2, _ = random_case(17 * D + crdt, crdt, K, D, 80, sparse=sparse,
+                                    multi=0.2 if crdt == _abi.SET_AW else 0.0, empty=0.2)
+        got2 = append_ops(ol, more, interleave(rng, ops_of(more)), rng)
+        pruned = EncodedLog(crdt_type=crdt, n_dcs=D, key_off=want["key_off"],
+                            key_type=np.full(K, crdt, np.uint8), oc=want["oc"][:n_out],
+                            oc_mask=None if tm is None else want["oc_mask"][:n_out],
+                            op_id=want["op_id"][:n_out], txid=want["txid"][:n_out])
+        if tags:
+            nr = int(want["rem_off"][n_out])
+            pruned.tag, pruned.add_tok = want["tag"][:n_out], want["add_tok"][:n_out]
+            pruned.rem_off = want["rem_off"][:n_out + 1]
+            pruned.rem_tok = want["rem_tok"][:max(nr, 1)]
+        else:
+            pruned.eff = want["eff"][:n_out]
+        both = concat(pruned, renumbered(more, got2))
+        view = ol.flush()
+        check_id_index(eng, view, K)
+        assert not materialize_view(eng, oracle_lib, view, both, req2, sparse)
+        for b in (bp, bt, btm, fl, none):
+            if b is not None:
+                b.free()
+
+
+def test_oplog_resize_policy_directions(eng):
+    """Deterministic NewListLen cases (OPS_THRESHOLD = 50 slots at first):
+    key 0: 48 ops, nothing pruned -> 48 > 50 - 5: ListLen doubles to 100;
+    key 1: 200 ops (ListLen 50 -> 100 -> 200), 10 kept -> halves to 100;
+    key 2: 60 ops (ListLen 100), 30 kept -> half = 50 <= OPS_THRESHOLD: stays;
+    key 3: 3 ops, all pruned -> NewLength 1: 50 stays (and AGN_GC_ALL_PRUNED);
+    key 4: never written -> ListLen 0 stays 0."""
+    D, K = 2, 5
+    lens = [48, 200, 60, 3, 0]
+    kept = [48, 10, 30, 0, 0]
+    with OpLog(eng, _abi.COUNTER_PN, D, K) as ol:
+        keys = np.concatenate([np.full(n, k, np.uint64) for k, n in enumerate(lens)])
+        pos = np.concatenate([np.arange(n) for n in lens]).astype(np.uint64)
+        oc = np.stack([pos + 1, pos + 1], axis=1).astype(np.uint64)   # op i: clock i+1
+        ol.append(keys, oc, eff=np.ones(len(keys), np.int64))
+        ln, ll, ct = ol.key_meta()
+        assert ln.tolist() == lens and ll.tolist() == [50, 200, 100, 50, 0]
+        # threshold t covers ops with clock <= t: keep the newest kept[k] ops
+        thr = np.array([[n - m, n - m] for n, m in zip(lens, kept)], np.uint64)
+        bt, bp, fl = eng.upload(thr), eng.upload(np.ones(K, np.uint8)), eng.empty(4 * K)
+        ol.prune(bp.ptr, bt.ptr, None, fl.ptr)
+        ln, ll, ct2 = ol.key_meta()
+        assert ln.tolist() == kept
+        assert ll.tolist() == [100, 100, 100, 50, 0]
+        assert ct2.tolist() == ct.tolist()
+        assert eng.download(fl, np.uint32, (K,)).tolist() == [0, 0, 0, _abi.GC_ALL_PRUNED,
+                                                              _abi.GC_ALL_PRUNED]
+        # op_insert_gc's trigger now counts against the new ListLen (:635)
+        _, due = ol.append(np.array([1] * 91, np.uint64), np.full((91, D), 10 ** 6, np.uint64),
+                           eff=np.ones(91, np.int64))
+        # ids 201..291: id 250 (NewId rem 50 == 0) and the 91st (Length 100 >= ListLen 100)
+        assert np.flatnonzero(due).tolist() == [49, 90]
+        for b in (bt, bp, fl):
+            b.free()
