@@ -76,7 +76,7 @@ class AgnKeyRead(C.Structure):
     _fields_ = [
         ("key", C.c_uint64), ("R", P), ("R_mask", P), ("sct", P), ("sct_mask", P),
         ("txid", C.c_uint64), ("base_value", C.c_int64), ("n_base", C.c_uint32),
-        ("_pad", C.c_uint32), ("base_tag", P), ("base_tok", P),
+        ("flags", C.c_uint32), ("base_tag", P), ("base_tok", P),
     ]
 
 
@@ -84,7 +84,7 @@ class AgnKeyResult(C.Structure):
     _fields_ = [
         ("value", C.c_int64), ("hole", C.c_int64), ("lastct", P), ("lastct_mask", P),
         ("count", C.c_uint32), ("flags", C.c_uint32), ("err_pos", C.c_uint32),
-        ("out_cap", C.c_uint32), ("out_n", C.c_uint32), ("_pad", C.c_uint32),
+        ("out_cap", C.c_uint32), ("out_n", C.c_uint32), ("status", C.c_uint32),
         ("out_tag", P), ("out_tok", P),
     ]
 
@@ -100,6 +100,7 @@ class AgnLogRecords(C.Structure):
 REC_OTHER, REC_UPDATE, REC_COMMIT = 0, 1, 2
 SNAPSHOT_THRESHOLD, SNAPSHOT_MIN, MIN_OP_STORE_SS = 10, 3, 5
 SS_HIT, SS_NEW, SS_LOG = 0, 1, 2
+READ_GC = 0x1
 
 
 class AgnGenCfg(C.Structure):
@@ -157,9 +158,16 @@ PROTOTYPES = {
     "agn_batcher_destroy": (C.c_int, [P]),
     "agn_batcher_read": (C.c_int, [P, C.POINTER(AgnKeyRead), C.POINTER(AgnKeyResult)]),
     "agn_batcher_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "agn_batcher_create_cached": (C.c_int, [P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(P)]),
     "agn_oplog_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                   C.POINTER(C.c_uint64)]),
     "agn_oplog_key_meta": (C.c_int, [P, C.c_uint64, P, P, P, P]),
+    "agn_interner_create": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(P)]),
+    "agn_interner_destroy": (C.c_int, [P]),
+    "agn_intern": (C.c_int, [P, P, C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
+    "agn_intern_find": (C.c_int, [P, P, C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
+    "agn_intern_bytes": (C.c_int, [P, C.c_uint64, C.POINTER(P), C.POINTER(C.c_size_t)]),
+    "agn_interner_size": (C.c_int, [P, C.POINTER(C.c_uint64)]),
     "agn_dep_check": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, C.c_uint64, P, P, P, P]),
     "agn_comm_unique_id": (C.c_int, [P]),
     "agn_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),

@@ -11,6 +11,17 @@
 // materialize kernel over the resident log, held shared) and one D2H copy,
 // then wakes the callers.  Requests that arrive while a batch runs form the
 // next batch, so the batch size adapts to the offered load.
+//
+// Cached mode (agn_batcher_create_cached, counter_pn) runs every batch as the
+// whole of materializer_vnode:read/6 on the device: the batcher owns the
+// partition's snapshot cache (agn_ss_cache), and a batch is
+// get_from_snapshot_cache (agn_ss_lookup: the base snapshot <= R) ->
+// materialize/4 from that base -> internal_store_ss / snapshot_insert_gc's
+// policy (agn_ss_store) -> prune_ops of the keys the policy selected
+// (agn_oplog_prune, in place, enqueued after the batch's results are out).
+// One batch holds distinct keys only (the cache's per-key state is
+// read-modify-write); a second read of a key waits for the next batch, so
+// reads of one key are applied in arrival order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,6 +32,7 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "common.hpp"
@@ -62,6 +74,13 @@ struct agn_batcher {
     char *dbuf = nullptr, *hbuf = nullptr;  // device / pinned [in | out]
     size_t cap = 0;
     std::atomic<uint64_t> n_batches{0}, n_reads{0};
+
+    // cached mode: the partition's device snapshot cache + GC scratch
+    bool cached = false;
+    agn_ss_cache ss{};
+    uint8_t *prune = nullptr;   // [K] agn_ss_store's prune flags
+    uint64_t *thr = nullptr;    // [K][D] prune thresholds
+    uint64_t *thrm = nullptr;   // [K][W] (sparse logs)
 };
 
 namespace {
@@ -77,6 +96,120 @@ int grow(agn_batcher *B, size_t bytes) {
     AGN_HIP(hipHostMalloc((void **)&B->hbuf, c, hipHostMallocDefault));
     B->cap = c;
     return AGN_OK;
+}
+
+__global__ void __launch_bounds__(256) k_gather_u8(const uint8_t *__restrict__ src,
+                                                   const uint64_t *__restrict__ idx, uint64_t n,
+                                                   uint8_t *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = src[idx[i]];
+}
+
+// Cached mode: read/6 for a batch of distinct keys (see the file comment).
+int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
+    const uint64_t n = b.size();
+    const uint32_t D = B->D, W = B->W;
+    bool sparse = B->sparse_log != 0;
+    for (Pending *p : b) sparse = sparse || p->rd->R_mask;
+    std::vector<uint64_t> keys(n);
+    for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
+    int rc;
+    {
+        std::shared_lock<std::shared_mutex> hold;
+        rc = oplog_begin_read(B->log, B->stream, 0, nullptr, nullptr, hold);
+        if (rc) return rc;
+        // in = keys R Rm txid gc | scratch = sct sctm ign base first
+        // out = value hole lastct lastct_mask count flags err_pos status prune
+        size_t off = 0;
+        auto slot = [&](size_t bytes) { size_t o = off; off = al(off + bytes); return o; };
+        const size_t o_keys = slot(n * 8), o_R = slot(n * D * 8), o_Rm = slot(sparse ? n * W * 8 : 0),
+                     o_txid = slot(n * 8), o_gc = slot(n);
+        const size_t in_bytes = off;
+        const size_t o_sct = slot(n * D * 8), o_sctm = slot(sparse ? n * W * 8 : 0),
+                     o_ign = slot(n), o_base = slot(n * 8), o_first = slot(n);
+        const size_t out_start = off;
+        const size_t o_val = slot(n * 8), o_hole = slot(n * 8), o_ct = slot(n * D * 8),
+                     o_ctm = slot(sparse ? n * W * 8 : 0), o_cnt = slot(n * 4), o_flg = slot(n * 4),
+                     o_epos = slot(n * 4), o_st = slot(n), o_pr = slot(n);
+        rc = grow(B, off);
+        if (rc) return rc;
+        char *h = B->hbuf, *d = B->dbuf;
+        auto H = [&](size_t o) { return h + o; };
+        uint64_t full[4] = {0, 0, 0, 0};
+        for (uint32_t x = 0; x < D; ++x) full[x >> 6] |= 1ull << (x & 63);
+        for (uint64_t i = 0; i < n; ++i) {
+            const agn_key_read *r = b[i]->rd;
+            ((uint64_t *)H(o_keys))[i] = r->key;
+            std::memcpy(H(o_R) + i * D * 8, r->R, D * 8);
+            if (sparse) std::memcpy(H(o_Rm) + i * W * 8, r->R_mask ? r->R_mask : full, W * 8);
+            ((uint64_t *)H(o_txid))[i] = r->txid;
+            ((uint8_t *)H(o_gc))[i] = (r->flags & AGN_READ_GC) ? 1 : 0;
+        }
+        AGN_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, B->stream));
+        agn_log view;
+        oplog_view(B->log, &view);
+        const uint64_t *dkeys = (const uint64_t *)(d + o_keys);
+        rc = agn_ss_lookup(B->ctx, &B->ss, n, dkeys, (const uint64_t *)(d + o_R),
+                           sparse ? (const uint64_t *)(d + o_Rm) : nullptr, (uint64_t *)(d + o_sct),
+                           sparse ? (uint64_t *)(d + o_sctm) : nullptr, (uint8_t *)(d + o_ign),
+                           (int64_t *)(d + o_base), (uint8_t *)(d + o_first),
+                           (uint8_t *)(d + o_st), B->stream);
+        if (rc) return rc;
+        agn_read req;
+        std::memset(&req, 0, sizeof req);
+        req.n_req = n;
+        req.keys = dkeys;
+        req.R = (const uint64_t *)(d + o_R);
+        req.R_mask = sparse ? (const uint64_t *)(d + o_Rm) : nullptr;
+        req.sct = (const uint64_t *)(d + o_sct);
+        req.sct_mask = sparse ? (const uint64_t *)(d + o_sctm) : nullptr;
+        req.sct_ignore = (const uint8_t *)(d + o_ign);
+        req.txid = (const uint64_t *)(d + o_txid);
+        req.req_type = B->crdt;
+        req.base_value = (const int64_t *)(d + o_base);
+        agn_result res;
+        std::memset(&res, 0, sizeof res);
+        res.value = (int64_t *)(d + o_val);
+        res.hole = (int64_t *)(d + o_hole);
+        res.lastct = (uint64_t *)(d + o_ct);
+        res.lastct_mask = sparse ? (uint64_t *)(d + o_ctm) : nullptr;
+        res.count = (uint32_t *)(d + o_cnt);
+        res.flags = (uint32_t *)(d + o_flg);
+        res.err_pos = (uint32_t *)(d + o_epos);
+        // a key whose cache has no snapshot <= R (AGN_SS_LOG) still runs
+        // through the kernel from the empty base; its result is discarded
+        rc = agn_materialize(B->ctx, &view, &req, &res, B->stream);
+        if (rc) return rc;
+        rc = agn_ss_store(B->ctx, &B->ss, &view, n, dkeys, (const uint8_t *)(d + o_first),
+                          (const uint8_t *)(d + o_st), (const uint8_t *)(d + o_gc), &res, nullptr,
+                          B->prune, B->thr, B->thrm, B->stream);
+        if (rc) return rc;
+        k_gather_u8<<<(unsigned)((n + 255) / 256), 256, 0, B->stream>>>(B->prune, dkeys, n,
+                                                                        (uint8_t *)(d + o_pr));
+        AGN_HIP(hipGetLastError());
+        AGN_HIP(hipMemcpyAsync(h + out_start, d + out_start, off - out_start, hipMemcpyDeviceToHost,
+                               B->stream));
+        AGN_HIP(hipStreamSynchronize(B->stream));
+        bool any_prune = false;
+        for (uint64_t i = 0; i < n; ++i) {
+            agn_key_result *o = b[i]->out;
+            o->status = ((const uint8_t *)H(o_st))[i];
+            o->value = ((const int64_t *)H(o_val))[i];
+            o->hole = ((const int64_t *)H(o_hole))[i];
+            std::memcpy(o->lastct, H(o_ct) + i * D * 8, D * 8);
+            if (o->lastct_mask)
+                std::memcpy(o->lastct_mask, sparse ? H(o_ctm) + i * W * 8 : (char *)full, W * 8);
+            o->count = ((const uint32_t *)H(o_cnt))[i];
+            o->flags = ((const uint32_t *)H(o_flg))[i];
+            o->err_pos = ((const uint32_t *)H(o_epos))[i];
+            o->out_n = 0;
+            any_prune = any_prune || ((const uint8_t *)H(o_pr))[i] != 0;
+        }
+        if (!any_prune) return AGN_OK;
+    }  // the shared hold ends: the GC takes the log exclusively
+    // prune_ops of the collected keys (in place, asynchronous: the next
+    // read of the log waits for it)
+    return agn_oplog_prune(B->log, B->prune, B->thr, B->thrm, nullptr, B->stream);
 }
 
 // One batch: pack, copy in, materialize over the resident log, copy out, unpack.
@@ -208,10 +341,12 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
         o->count = ((const uint32_t *)H(o_cnt))[i];
         o->flags = ((const uint32_t *)H(o_flg))[i];
         o->err_pos = ((const uint32_t *)H(o_epos))[i];
+        o->status = 0;
         if (tags) {
             const uint32_t m = ((const uint32_t *)H(o_outn))[i];
             const uint64_t s = ((const uint64_t *)H(o_cap))[i];
             o->out_n = m;
+            o->status = 0;
             if (m > o->out_cap) {
                 b[i]->rc = AGN_ECAPACITY;
                 std::snprintf(b[i]->err, sizeof b[i]->err, "batcher_read: %u pairs, out_cap %u", m,
@@ -236,11 +371,26 @@ void worker_main(agn_batcher *B) {
         const auto deadline = B->q.front()->t + std::chrono::microseconds(B->max_wait_us);
         while (!B->stop && B->q.size() < B->max_batch && Clock::now() < deadline)
             B->cv_work.wait_until(lk, deadline);
-        const size_t n = std::min<size_t>(B->q.size(), B->max_batch);
-        std::vector<Pending *> batch(B->q.begin(), B->q.begin() + n);
-        B->q.erase(B->q.begin(), B->q.begin() + n);
+        std::vector<Pending *> batch;
+        if (!B->cached) {
+            const size_t n = std::min<size_t>(B->q.size(), B->max_batch);
+            batch.assign(B->q.begin(), B->q.begin() + n);
+            B->q.erase(B->q.begin(), B->q.begin() + n);
+        } else {
+            // distinct keys, in arrival order; a repeated key waits for the next batch
+            std::unordered_set<uint64_t> in;
+            std::deque<Pending *> rest;
+            for (Pending *p : B->q) {
+                if (batch.size() < B->max_batch && in.insert(p->rd->key).second)
+                    batch.push_back(p);
+                else
+                    rest.push_back(p);
+            }
+            B->q.swap(rest);
+        }
+        const size_t n = batch.size();
         lk.unlock();
-        int rc = run_batch(B, batch);
+        int rc = B->cached ? run_batch_cached(B, batch) : run_batch(B, batch);
         if (rc)
             for (Pending *p : batch) {
                 p->rc = rc;
@@ -298,10 +448,66 @@ int agn_batcher_destroy(agn_batcher *B) {
     B->cv_work.notify_all();
     if (B->worker.joinable()) B->worker.join();
     (void)use_device(B->ctx);
+    if (B->stream) (void)hipStreamSynchronize(B->stream);
     if (B->dbuf) (void)hipFree(B->dbuf);
     if (B->hbuf) (void)hipHostFree(B->hbuf);
+    for (void *p : {(void *)B->ss.n, (void *)B->ss.clock, (void *)B->ss.clock_mask,
+                    (void *)B->ss.last_op, (void *)B->ss.value, (void *)B->prune, (void *)B->thr,
+                    (void *)B->thrm})
+        if (p) (void)hipFree(p);
     if (B->stream) (void)hipStreamDestroy(B->stream);
     delete B;
+    return AGN_OK;
+}
+
+int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch,
+                              uint32_t max_wait_us, agn_batcher **out) {
+    if (!out || !log) return fail(AGN_EINVAL, "batcher_create_cached: null argument");
+    *out = nullptr;
+    uint32_t crdt, D;
+    int sparse;
+    uint64_t K;
+    oplog_shape(log, &crdt, &D, &sparse, &K);
+    if (crdt != AGN_COUNTER_PN)
+        return fail(AGN_ENOTSUP, "batcher_create_cached: counter_pn only (set/register states "
+                                 "are cached by the caller)");
+    if (slots == 0) slots = AGN_SNAPSHOT_THRESHOLD;
+    if (slots < AGN_SNAPSHOT_THRESHOLD - 1)
+        return fail(AGN_EINVAL, "batcher_create_cached: slots %u < %d", slots,
+                    AGN_SNAPSHOT_THRESHOLD - 1);
+    int rc = use_device(oplog_ctx(log));
+    if (rc) return rc;
+    const uint32_t W = n_words(D);
+    const uint64_t K1 = std::max<uint64_t>(K, 1);
+    agn_ss_cache c{};
+    c.n_dcs = D;
+    c.slots = slots;
+    c.n_keys = K;
+    uint8_t *prune = nullptr;
+    uint64_t *thr = nullptr, *thrm = nullptr;
+    hipError_t e = hipMalloc((void **)&c.n, K1 * 4);
+    if (e == hipSuccess) e = hipMemset(c.n, 0, K1 * 4);
+    if (e == hipSuccess) e = hipMalloc((void **)&c.clock, K1 * slots * D * 8);
+    if (e == hipSuccess && sparse) e = hipMalloc((void **)&c.clock_mask, K1 * slots * W * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&c.last_op, K1 * slots * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&c.value, K1 * slots * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&prune, K1);
+    if (e == hipSuccess) e = hipMalloc((void **)&thr, K1 * D * 8);
+    if (e == hipSuccess && sparse) e = hipMalloc((void **)&thrm, K1 * W * 8);
+    if (e == hipSuccess) rc = agn_batcher_create(log, max_batch, max_wait_us, out);
+    if (e != hipSuccess || rc != AGN_OK) {
+        for (void *p : {(void *)c.n, (void *)c.clock, (void *)c.clock_mask, (void *)c.last_op,
+                        (void *)c.value, (void *)prune, (void *)thr, (void *)thrm})
+            if (p) (void)hipFree(p);
+        return e != hipSuccess ? fail(AGN_ENOMEM, "batcher_create_cached: snapshot cache") : rc;
+    }
+    // the worker only looks at `cached` under the queue lock, after a read arrives
+    std::lock_guard<std::mutex> g((*out)->mu);
+    (*out)->cached = true;
+    (*out)->ss = c;
+    (*out)->prune = prune;
+    (*out)->thr = thr;
+    (*out)->thrm = thrm;
     return AGN_OK;
 }
 
@@ -310,6 +516,7 @@ int agn_batcher_read(agn_batcher *B, const agn_key_read *rd, agn_key_result *out
     if (rd->key >= B->K) return fail(AGN_EINVAL, "batcher_read: key %llu >= n_keys",
                                      (unsigned long long)rd->key);
     if (!rd->R || !out->lastct) return fail(AGN_EINVAL, "batcher_read: R / lastct required");
+    if (rd->flags & ~(uint32_t)AGN_READ_GC) return fail(AGN_EINVAL, "batcher_read: unknown flags");
     if (B->crdt != AGN_COUNTER_PN) {
         if (rd->n_base && (!rd->base_tag || !rd->base_tok))
             return fail(AGN_EINVAL, "batcher_read: base pairs missing");

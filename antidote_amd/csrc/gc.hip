@@ -345,9 +345,17 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
         const uint64_t pos = b + (uint64_t)slot;
         const bool valid = pos < n;
         const uint64_t e = off + (valid ? pos : 0ull);
+        // the raw row (absent DCs included: a kept row moves bit for bit)
         uint64_t o[DPL];
         uint32_t obits;
-        load_rows<DPL, SPARSE, FULL>(rl, e, d0, D, W, o, obits);
+        if constexpr (FULL) {
+            load_rows<DPL, SPARSE, FULL>(rl, e, d0, D, W, o, obits);
+        } else {
+            obits = chunk_bits<DPL, SPARSE>(a.mask, e, W, d0, D);
+#pragma unroll
+            for (int j = 0; j < DPL; ++j)
+                o[j] = ((uint32_t)(d0 + j) < D) ? a.oc[e * D + (uint32_t)(d0 + j)] : 0ull;
+        }
         if (!valid) obits = 0u;
         bool le = true;
 #pragma unroll

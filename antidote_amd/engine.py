@@ -368,11 +368,18 @@ class Batcher:
     coalesced into batched kernels.  `read` blocks the calling thread (ctypes
     releases the GIL for the duration)."""
 
-    def __init__(self, oplog: OpLog, max_batch: int = 1024, max_wait_us: int = 0):
+    def __init__(self, oplog: OpLog, max_batch: int = 1024, max_wait_us: int = 0,
+                 cached: bool = False, slots: int = 0):
+        """cached=True: agn_batcher_create_cached -- each batch is the whole
+        read/6 over the batcher's device snapshot cache (counter_pn)."""
         self.oplog, self.lib = oplog, oplog.eng.lib
         self.h = C.c_void_p()
-        check(self.lib.agn_batcher_create(oplog.h, max_batch, max_wait_us, C.byref(self.h)),
-              "agn_batcher_create")
+        if cached:
+            check(self.lib.agn_batcher_create_cached(oplog.h, slots, max_batch, max_wait_us,
+                                                     C.byref(self.h)), "agn_batcher_create_cached")
+        else:
+            check(self.lib.agn_batcher_create(oplog.h, max_batch, max_wait_us, C.byref(self.h)),
+                  "agn_batcher_create")
 
     def close(self):
         if self.h:
@@ -386,7 +393,7 @@ class Batcher:
         self.close()
 
     def read(self, key, R, R_mask=None, sct=None, sct_mask=None, txid=0, base_value=0,
-             base_tag=None, base_tok=None, out_cap=0):
+             base_tag=None, base_tok=None, out_cap=0, gc=False):
         """One read/6; returns a dict of the key's result."""
         D = self.oplog.n_dcs
         W = n_words(D)
@@ -396,6 +403,7 @@ class Batcher:
         rd.key, rd.R, rd.R_mask, rd.sct, rd.sct_mask = key, _ptr(R), _ptr(R_mask), _ptr(sct), \
             _ptr(sct_mask)
         rd.txid, rd.base_value = txid, base_value
+        rd.flags = _abi.READ_GC if gc else 0
         if base_tag is not None:
             base_tag = np.ascontiguousarray(base_tag, np.uint32)
             base_tok = np.ascontiguousarray(base_tok, np.uint64)
@@ -408,6 +416,7 @@ class Batcher:
         check(self.lib.agn_batcher_read(self.h, C.byref(rd), C.byref(o)), "agn_batcher_read")
         return {"value": o.value, "hole": o.hole, "lastct": ct, "lastct_mask": ctm,
                 "count": o.count, "flags": o.flags, "err_pos": o.err_pos, "out_n": o.out_n,
+                "status": o.status,
                 "out_tag": otag[:o.out_n], "out_tok": otok[:o.out_n]}
 
     def stats(self):
@@ -433,3 +442,47 @@ def host_view(ptr, dtype, n):
         return np.zeros(0, dtype)
     ct = np.ctypeslib.as_ctypes_type(np.dtype(dtype))
     return np.ctypeslib.as_array((ct * int(n)).from_address(ptr))
+
+
+class Interner:
+    """agn_interner: exact byte-string <-> dense id map (the NIF's term tables:
+    keys, DC ids, TxIds, set elements / register values, tokens).  Host-only."""
+
+    def __init__(self, first_id: int = 1, max_ids: int = 1 << 40):
+        self.lib = load()
+        self.h = C.c_void_p()
+        check(self.lib.agn_interner_create(first_id, max_ids, C.byref(self.h)),
+              "agn_interner_create")
+
+    def close(self):
+        if self.h:
+            self.lib.agn_interner_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def intern(self, b: bytes):
+        """-> (id, is_new)"""
+        i, new = C.c_uint64(), C.c_int()
+        check(self.lib.agn_intern(self.h, b, len(b), C.byref(i), C.byref(new)), "agn_intern")
+        return i.value, bool(new.value)
+
+    def find(self, b: bytes):
+        i, f = C.c_uint64(), C.c_int()
+        check(self.lib.agn_intern_find(self.h, b, len(b), C.byref(i), C.byref(f)),
+              "agn_intern_find")
+        return i.value if f.value else None
+
+    def bytes_of(self, i: int) -> bytes:
+        p, n = C.c_void_p(), C.c_size_t()
+        check(self.lib.agn_intern_bytes(self.h, i, C.byref(p), C.byref(n)), "agn_intern_bytes")
+        return C.string_at(p.value, n.value) if n.value else b""
+
+    def __len__(self):
+        n = C.c_uint64()
+        check(self.lib.agn_interner_size(self.h, C.byref(n)))
+        return n.value

@@ -304,10 +304,12 @@ typedef struct agn_key_read { /* one read/6 (host pointers) */
     uint64_t txid;              /* 0 = ignore */
     int64_t base_value;         /* counter_pn base */
     uint32_t n_base;            /* set/register base pairs */
-    uint32_t _pad;
+    uint32_t flags;             /* AGN_READ_GC: op_insert_gc's GC read (ShouldGc = true,
+                                   src/materializer_vnode.erl:640; cached mode) */
     const uint32_t *base_tag;
     const uint64_t *base_tok;
 } agn_key_read;
+#define AGN_READ_GC 0x1u
 typedef struct agn_key_result { /* caller-owned host memory */
     int64_t value, hole;
     uint64_t *lastct;           /* [D] */
@@ -315,7 +317,9 @@ typedef struct agn_key_result { /* caller-owned host memory */
     uint32_t count, flags, err_pos;
     uint32_t out_cap;           /* set/register: room in out_tag / out_tok */
     uint32_t out_n;             /* live pairs (> out_cap => AGN_ECAPACITY) */
-    uint32_t _pad;
+    uint32_t status;            /* cached mode: AGN_SS_HIT / AGN_SS_NEW, or AGN_SS_LOG (no
+                                   cached snapshot <= R: the caller reads the log,
+                                   get_from_snapshot_log :416-419; the result is void) */
     uint32_t *out_tag;
     uint64_t *out_tok;
 } agn_key_result;
@@ -324,6 +328,36 @@ int agn_batcher_create(agn_oplog *log, uint32_t max_batch, uint32_t max_wait_us,
 int agn_batcher_destroy(agn_batcher *b);
 int agn_batcher_read(agn_batcher *b, const agn_key_read *rd, agn_key_result *out);
 int agn_batcher_stats(agn_batcher *b, uint64_t *batches, uint64_t *reads);
+/* Cached mode (counter_pn): the batcher also owns the partition's device
+ * snapshot cache (an agn_ss_cache of n_keys x slots, 0 = SNAPSHOT_THRESHOLD)
+ * and serves each batch as the whole of materializer_vnode:read/6
+ * (:96-102, 371-509): get_from_snapshot_cache (agn_ss_lookup) -> materialize/4
+ * from the cached base -> internal_store_ss / snapshot_insert_gc
+ * (agn_ss_store; AGN_READ_GC in agn_key_read.flags forces the GC as
+ * op_insert_gc's GC read does) -> prune_ops of the selected keys
+ * (agn_oplog_prune, in place).  agn_key_read.sct / base_value are ignored
+ * (the base comes from the cache); agn_key_result.status tells HIT / NEW /
+ * LOG.  Reads of one key are applied in arrival order. */
+int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch,
+                              uint32_t max_wait_us, agn_batcher **out);
+
+/* ---- exact term interning (the Erlang binding's term <-> integer maps) ----
+ * Host-only.  The device log holds DC ids, keys, TxIds, set elements /
+ * register values and tokens as integers; the NIF maps a term through its
+ * external term format (enif_term_to_binary) with an interner: equal byte
+ * strings <=> equal id (full comparison, no hash shortcut -- exact, as
+ * is_op_in_snapshot's TxId == Op#clocksi_payload.txid,
+ * src/clocksi_materializer.erl:220, requires), ids dense from first_id, at
+ * most max_ids (AGN_ECAPACITY beyond).  agn_intern_bytes returns the stored
+ * bytes of an id for decoding (valid until destroy).  Thread-safe. */
+typedef struct agn_interner agn_interner;
+int agn_interner_create(uint64_t first_id, uint64_t max_ids, agn_interner **out);
+int agn_interner_destroy(agn_interner *t);
+int agn_intern(agn_interner *t, const void *bytes, size_t n, uint64_t *id, int *is_new);
+int agn_intern_find(const agn_interner *t, const void *bytes, size_t n, uint64_t *id,
+                    int *found);
+int agn_intern_bytes(const agn_interner *t, uint64_t id, const void **bytes, size_t *n);
+int agn_interner_size(const agn_interner *t, uint64_t *n);
 
 /* ---- base-snapshot selection: vector_orddict:get_smaller/2 --------------
  * (src/vector_orddict.erl:74-87, called from

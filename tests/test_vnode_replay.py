@@ -1,0 +1,186 @@
+"""The drop-in's call sequence (what the NIF does for materializer_vnode,
+SURVEY.md §8(b) Ownership / Threading) replayed through the C ABI:
+
+  update/2  -> agn_oplog_append (op ids, op_insert_gc's GC trigger) and, when
+               due, the GC read (agn_batcher_read with AGN_READ_GC);
+  read/6    -> agn_batcher_read on a cached batcher: agn_ss_lookup ->
+               agn_materialize -> agn_ss_store -> agn_oplog_prune (in place).
+
+Sequentially, every read must equal the reference's transcription
+(oracle/py_oracle.MaterializerVnode: ETS ops tuple, snapshot cache, GC,
+resize), including whether the snapshot cache can serve it at all.  With a
+writer thread and 8 reader threads, every served read must equal the value
+of the key's ops at R (whatever the cache held and whatever GC ran)."""
+import threading
+
+import numpy as np
+import pytest
+
+from antidote_amd import _abi
+from antidote_amd.engine import Batcher, OpLog
+from oracle import py_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+D = 3
+BIG = 10 ** 15
+
+
+def vc(row):
+    return {d: int(row[d]) for d in range(D)}
+
+
+class Workload:
+    """Per-DC clocks that only grow; an op commits at DC c after the others'
+    current times (its snapshot), so op clocks are causal and reads at any
+    R <= the current clocks see exactly the ops already appended."""
+
+    def __init__(self, seed, K):
+        self.rng = np.random.default_rng(seed)
+        self.K = K
+        self.clk = np.full(D, 1000, np.int64)
+        self.ops = [[] for _ in range(K)]   # per key: (oc row, eff)
+
+    def op(self, key):
+        c = int(self.rng.integers(0, D))
+        ss = self.clk - self.rng.integers(0, 40, D)
+        ss = np.maximum(ss, 0)
+        self.clk[c] += int(self.rng.integers(1, 30))
+        ct = int(self.clk[c])
+        oc = ss.copy()
+        oc[c] = ct
+        eff = int(self.rng.integers(-50, 51))
+        return c, ss, ct, oc, eff
+
+    def read_clock(self, lag=400):
+        return np.maximum(self.clk - self.rng.integers(0, lag, D), 0)
+
+
+def has_placeholder(vn, key):
+    """The reference's all-pruned quirk: prune_ops keeps element(?FIRST_OP+Len),
+    an empty slot (0), as the only op (src/materializer_vnode.erl:580-583); the
+    engine keeps zero entries instead (AGN_GC_ALL_PRUNED)."""
+    tup = vn.ops_cache.get(key)
+    if tup is None:
+        return False
+    length = tup[1][0]
+    return any(tup[po.FIRST_OP - 1 + i] == 0 for i in range(length))
+
+
+def engine_update(ol, bt, key, ss, oc, eff, txid):
+    ids, due = ol.append(np.array([key], np.uint64), oc.reshape(1, D).astype(np.uint64),
+                         eff=np.array([eff], np.int64), txid=np.array([txid], np.uint64))
+    if due[0]:
+        # op_insert_gc's GC read at the op's snapshot time (:640)
+        bt.read(key, R=ss.astype(np.uint64), gc=True)
+    return int(ids[0])
+
+
+def test_vnode_replay_sequential_vs_reference(eng):
+    K, steps = 24, 4000
+    w = Workload(11, K)
+    vn = po.MaterializerVnode()
+    quirk = set()   # keys where the reference hit the all-pruned placeholder (:580-583)
+    served = log_reads = 0
+    with OpLog(eng, _abi.COUNTER_PN, D, K) as ol, \
+            Batcher(ol, max_batch=8, cached=True) as bt:
+        for s in range(steps):
+            key = int(w.rng.integers(0, K))
+            if w.rng.random() < 0.7:
+                c, ss, ct, oc, eff = w.op(key)
+                pay = po.Payload(key, po.COUNTER_PN, eff, vc(ss), (c, ct), s + 1)
+                try:
+                    vn.update(key, pay)
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                engine_update(ol, bt, key, ss, oc, eff, s + 1)
+                w.ops[key].append((oc, eff))
+                if has_placeholder(vn, key):
+                    quirk.add(key)
+            else:
+                R = w.read_clock()
+                g = bt.read(key, R=R.astype(np.uint64))
+                if key in quirk:
+                    continue
+                try:
+                    want = vn.read(key, po.COUNTER_PN, vc(R), po.IGNORE)
+                except NotImplementedError:      # get_from_snapshot_log
+                    assert g["status"] == _abi.SS_LOG, (s, key)
+                    log_reads += 1
+                    continue
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                    continue
+                assert g["status"] in (_abi.SS_HIT, _abi.SS_NEW), (s, key, g["status"])
+                assert want == ("ok", g["value"]), (s, key, want, g["value"])
+                served += 1
+                if has_placeholder(vn, key):
+                    quirk.add(key)
+        ln, ll, ct = ol.key_meta()
+    assert served > 1000 and log_reads > 0
+    assert len(quirk) < K // 2
+    for k in range(K):
+        if k in quirk or k not in vn.ops_cache:
+            continue
+        length, list_len = vn.ops_cache[k][1]
+        assert (int(ln[k]), int(ll[k]), int(ct[k])) == (length, list_len, vn.ops_cache[k][2]), k
+
+
+def test_vnode_replay_threads_values(eng):
+    """1 writer (the vnode: update/2 + GC reads) and 8 read servers."""
+    K = 16
+    w = Workload(5, K)
+    lock = threading.Lock()
+    errs, stats = [], {"served": 0, "log": 0}
+    with OpLog(eng, _abi.COUNTER_PN, D, K, init_slots=8) as ol, \
+            Batcher(ol, max_batch=16, max_wait_us=100, cached=True) as bt:
+        stop = threading.Event()
+
+        def writer():
+            try:
+                for s in range(3000):
+                    key = s % K if s < K else int(w.rng.integers(0, K))
+                    # the clocks a reader may pick advance only with the append
+                    with lock:
+                        c, ss, ct, oc, eff = w.op(key)
+                        engine_update(ol, bt, key, ss, oc, eff, s + 1)
+                        w.ops[key].append((oc, eff))
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+            finally:
+                stop.set()
+
+        def reader(t):
+            rng = np.random.default_rng(100 + t)
+            try:
+                while not stop.is_set():
+                    key = int(rng.integers(0, K))
+                    with lock:
+                        # ops at or below the published clocks are all appended
+                        R = np.maximum(w.clk - rng.integers(0, 300, D), 0)
+                    g = bt.read(key, R=R.astype(np.uint64))
+                    with lock:
+                        ops = list(w.ops[key])
+                    if g["status"] == _abi.SS_LOG:
+                        stats["log"] += 1
+                        continue
+                    want = sum(e for oc, e in ops if (oc <= R).all())
+                    assert g["value"] == want, (key, g["value"], want)
+                    stats["served"] += 1
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=writer)] + \
+            [threading.Thread(target=reader, args=(t,)) for t in range(8)]
+        for x in ts:
+            x.start()
+        for x in ts:
+            x.join()
+        assert not errs, errs[0]
+        # after the storm: every key read at the current clocks, served
+        for key in range(K):
+            g = bt.read(key, R=w.clk.astype(np.uint64))
+            assert g["status"] in (_abi.SS_HIT, _abi.SS_NEW)
+            assert g["value"] == sum(e for _, e in w.ops[key])
+        st = ol.stats()
+    assert stats["served"] > 200, stats
+    assert st["entries"] < sum(len(x) for x in w.ops)   # the GC ran
