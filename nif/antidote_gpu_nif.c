@@ -10,6 +10,28 @@
  *
  * Exports (antidote_gpu_nif):
  *   open(Device) -> {ok, Ctx} | {error, Reason}
+ *
+ *   Engine-owned partition (the materializer_vnode ETS ops cache in HBM,
+ *   one per vnode; the resource's destructor frees it):
+ *   part_open(Ctx, Type, NDcs, NKeys, Cached) -> {ok, Part}
+ *   part_update(Part, Key, OcPairs, TxId, Effect) -> {ok, OpId, GcDue}
+ *       update/2 -> op_insert_gc/3 (agn_oplog_append): OcPairs =
+ *       [{Dc, Time}] of the op's OpSSCommit, TxId a term or ignore, Effect the
+ *       #clocksi_payload.op_param (counter_pn integer, set_aw
+ *       [{Elem, AddToks, RemToks}], register_mv {V, Tok, Ovr} | {reset, Ovr})
+ *   part_read(Part, Key, RPairs, TxId, Gc) -> {ok, Value, NewLastOp, LastOpCt,
+ *       IsNewSS, Count} | {error, no_snapshot} | {error, Reason}
+ *       cached partition: the whole read/6 (device snapshot cache + GC);
+ *       Gc = true is op_insert_gc's GC read
+ *   part_materialize(Part, Key, RPairs, SctPairs | ignore, TxId, Base) ->
+ *       same result: materialize/4 of the resident ops from a caller base
+ *       (the reference's own ETS snapshot cache stays in Erlang)
+ *   part_gc(Part, Key, ThresholdPairs) -> ok
+ *       snapshot_insert_gc's prune_ops + resize for one key (agn_oplog_prune)
+ *   part_stats(Part) -> {Entries, Slots, Tokens}
+ *   part_key_meta(Part, Key) -> {Length, ListLen, OpId}
+ *   Keys, DC ids, TxIds, elements / values and tokens are interned exactly
+ *   (agn_interner over enif_term_to_binary), never hashed.
  *   materialize(Ctx, Type, NDcs, Log, Read, CapOff) ->
  *       {ok, {Value, Hole, LastCt, LastCtMask, Count, Flags, ErrPos, OutN, OutTag, OutTok}}
  *     Log  = {KeyOff, KeyType, Oc, OcMask, OpId, TxId, Eff, Tag, AddTok, RemOff, RemTok}
@@ -23,7 +45,11 @@
 
 #include "../include/antidote_gpu.h"
 
+#include <pthread.h>
+#include <stdlib.h>
+
 static ErlNifResourceType *CTX_RES;
+static ErlNifResourceType *PART_RES;
 
 typedef struct {
     agn_ctx *ctx;
@@ -52,11 +78,46 @@ static void ctx_dtor(ErlNifEnv *env, void *obj) {
     r->ctx = NULL;
 }
 
+/* ---- partition resource ------------------------------------------------ */
+typedef struct {
+    ctx_res *ctx;           /* kept alive while the partition lives */
+    agn_oplog *log;
+    agn_batcher *bt;
+    agn_interner *keys, *dcs, *txids, *tags, *toks;
+    uint32_t type, D, W;
+    uint64_t K;
+    int cached;
+    /* part_gc scratch (device): prune flags [K], threshold row [K][D] (+ mask) */
+    pthread_mutex_t gc_mu;
+    uint8_t *d_prune;
+    uint64_t *d_thr, *d_thrm;
+} part_res;
+
+static void part_dtor(ErlNifEnv *env, void *obj) {
+    (void)env;
+    part_res *p = (part_res *)obj;
+    if (p->bt) agn_batcher_destroy(p->bt);
+    if (p->log) agn_oplog_destroy(p->log);
+    if (p->ctx) {
+        agn_dev_free(p->ctx->ctx, p->d_prune);
+        agn_dev_free(p->ctx->ctx, p->d_thr);
+        agn_dev_free(p->ctx->ctx, p->d_thrm);
+    }
+    agn_interner_destroy(p->keys);
+    agn_interner_destroy(p->dcs);
+    agn_interner_destroy(p->txids);
+    agn_interner_destroy(p->tags);
+    agn_interner_destroy(p->toks);
+    pthread_mutex_destroy(&p->gc_mu);
+    if (p->ctx) enif_release_resource(p->ctx);
+}
+
 static int load(ErlNifEnv *env, void **priv, ERL_NIF_TERM info) {
     (void)priv;
     (void)info;
     CTX_RES = enif_open_resource_type(env, NULL, "agn_ctx", ctx_dtor, ERL_NIF_RT_CREATE, NULL);
-    return CTX_RES == NULL;
+    PART_RES = enif_open_resource_type(env, NULL, "agn_part", part_dtor, ERL_NIF_RT_CREATE, NULL);
+    return CTX_RES == NULL || PART_RES == NULL;
 }
 
 static int get_ctx(ErlNifEnv *env, ERL_NIF_TERM t, agn_ctx **out) {
@@ -246,8 +307,465 @@ static ERL_NIF_TERM nif_select_base(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     return enif_make_tuple2(env, atom(env, "ok"), enif_make_tuple2(env, ti, tf));
 }
 
+/* ---- partition functions -------------------------------------------------- */
+static int get_part(ErlNifEnv *env, ERL_NIF_TERM t, part_res **out) {
+    return enif_get_resource(env, t, PART_RES, (void **)out) && (*out)->log != NULL;
+}
+
+/* exact id of a term: its external format through an interner */
+static int term_id(ErlNifEnv *env, agn_interner *t, ERL_NIF_TERM term, uint64_t *id) {
+    ErlNifBinary b;
+    if (!enif_term_to_binary(env, term, &b)) return AGN_ENOMEM;
+    int rc = agn_intern(t, b.data, b.size, id, NULL);
+    enif_release_binary(&b);
+    return rc;
+}
+
+static ERL_NIF_TERM id_term(ErlNifEnv *env, agn_interner *t, uint64_t id) {
+    const void *data;
+    size_t n;
+    ERL_NIF_TERM out;
+    if (agn_intern_bytes(t, id, &data, &n) != AGN_OK ||
+        enif_binary_to_term(env, (const unsigned char *)data, n, &out, 0) == 0)
+        return atom(env, "undefined");
+    return out;
+}
+
+/* [{Dc, Time}] -> dense row + presence mask; columns from the DC interner */
+static int clock_row(ErlNifEnv *env, part_res *p, ERL_NIF_TERM pairs, uint64_t *row,
+                     uint64_t *mask) {
+    memset(row, 0, p->D * 8);
+    memset(mask, 0, p->W * 8);
+    ERL_NIF_TERM head, tail = pairs;
+    while (enif_get_list_cell(env, tail, &head, &tail)) {
+        int ar;
+        const ERL_NIF_TERM *kv;
+        ErlNifUInt64 t;
+        uint64_t col;
+        if (!enif_get_tuple(env, head, &ar, &kv) || ar != 2 || !enif_get_uint64(env, kv[1], &t))
+            return AGN_EINVAL;
+        int rc = term_id(env, p->dcs, kv[0], &col);
+        if (rc) return rc;
+        col -= 1;
+        row[col] = t;
+        mask[col >> 6] |= 1ull << (col & 63);
+    }
+    return enif_is_empty_list(env, tail) ? AGN_OK : AGN_EINVAL;
+}
+
+static ERL_NIF_TERM clock_pairs(ErlNifEnv *env, part_res *p, const uint64_t *row,
+                                const uint64_t *mask) {
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    for (uint32_t d = p->D; d-- > 0;)
+        if ((mask[d >> 6] >> (d & 63)) & 1ull)
+            l = enif_make_list_cell(env, enif_make_tuple2(env, id_term(env, p->dcs, d + 1),
+                                                         enif_make_uint64(env, row[d])), l);
+    return l;
+}
+
+static int key_index(ErlNifEnv *env, part_res *p, ERL_NIF_TERM key, uint64_t *k) {
+    uint64_t id;
+    int rc = term_id(env, p->keys, key, &id);
+    if (rc) return rc;
+    *k = id - 1;
+    return AGN_OK;
+}
+
+static int txid_of(ErlNifEnv *env, part_res *p, ERL_NIF_TERM t, uint64_t *id) {
+    if (enif_is_identical(t, atom(env, "ignore"))) {
+        *id = 0;
+        return AGN_OK;
+    }
+    return term_id(env, p->txids, t, id);
+}
+
+static ERL_NIF_TERM nif_part_open(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    ctx_res *c;
+    unsigned type, D;
+    ErlNifUInt64 K;
+    if (argc != 5 || !enif_get_resource(env, argv[0], CTX_RES, (void **)&c) || !c->ctx ||
+        !enif_get_uint(env, argv[1], &type) || !enif_get_uint(env, argv[2], &D) || D == 0 ||
+        D > 256 || !enif_get_uint64(env, argv[3], &K) || K == 0)
+        return enif_make_badarg(env);
+    const int cached = enif_is_identical(argv[4], atom(env, "true"));
+    part_res *p = enif_alloc_resource(PART_RES, sizeof *p);
+    memset(p, 0, sizeof *p);
+    pthread_mutex_init(&p->gc_mu, NULL);
+    p->type = type;
+    p->D = D;
+    p->W = (D + 63) / 64;
+    p->K = K;
+    p->cached = cached;
+    int rc = agn_oplog_create(c->ctx, type, D, K, 1, 0, &p->log);
+    if (!rc) rc = cached ? agn_batcher_create_cached(p->log, 0, 1024, 50, &p->bt)
+                         : agn_batcher_create(p->log, 1024, 50, &p->bt);
+    if (!rc) rc = agn_interner_create(1, K, &p->keys);
+    if (!rc) rc = agn_interner_create(1, D, &p->dcs);
+    if (!rc) rc = agn_interner_create(1, UINT64_MAX / 2, &p->txids);
+    if (!rc) rc = agn_interner_create(0, 0xFFFFFFFEull, &p->tags);
+    if (!rc) rc = agn_interner_create(1, UINT64_MAX / 2, &p->toks);
+    if (!rc) rc = agn_dev_alloc(c->ctx, K, (void **)&p->d_prune);
+    if (!rc) rc = agn_dev_alloc(c->ctx, K * D * 8, (void **)&p->d_thr);
+    if (!rc) rc = agn_dev_alloc(c->ctx, K * p->W * 8, (void **)&p->d_thrm);
+    p->ctx = c;
+    enif_keep_resource(c);
+    if (rc) {
+        ERL_NIF_TERM e = error_tuple(env, rc);
+        enif_release_resource(p);  /* the destructor frees what was created */
+        return e;
+    }
+    ERL_NIF_TERM t = enif_make_resource(env, p);
+    enif_release_resource(p);
+    return enif_make_tuple2(env, atom(env, "ok"), t);
+}
+
+/* Entries of one effect (set_aw: one per {Elem, Add, Rem} part and per extra
+ * add token; register_mv: one) into the arrays; returns the entry count or -1
+ * when the effect cannot be represented (-> an invalid entry). */
+#define MAXE 256
+#define MAXT 4096
+typedef struct {
+    uint32_t n, nrem;
+    uint32_t tag[MAXE];
+    uint64_t add[MAXE];
+    uint32_t rem_off[MAXE + 1];
+    uint64_t rem[MAXT];
+} entries;
+
+static int push_rems(ErlNifEnv *env, part_res *p, ERL_NIF_TERM list, entries *E) {
+    ERL_NIF_TERM h, t = list;
+    while (enif_get_list_cell(env, t, &h, &t)) {
+        uint64_t id;
+        if (E->nrem >= MAXT || term_id(env, p->toks, h, &id)) return -1;
+        E->rem[E->nrem++] = id;
+    }
+    return enif_is_empty_list(env, t) ? 0 : -1;
+}
+
+/* one entry {tag, add token, removal tokens of `rems` (or none)} */
+static int push_entry(ErlNifEnv *env, part_res *p, entries *E, uint64_t tag, uint64_t add,
+                      const ERL_NIF_TERM *rems) {
+    if (E->n >= MAXE) return -1;
+    E->rem_off[E->n] = E->nrem;
+    E->tag[E->n] = (uint32_t)tag;
+    E->add[E->n] = add;
+    if (rems && push_rems(env, p, *rems, E)) return -1;
+    E->n++;
+    E->rem_off[E->n] = E->nrem;
+    return 0;
+}
+
+static int effect_entries(ErlNifEnv *env, part_res *p, ERL_NIF_TERM eff, entries *E) {
+    E->n = E->nrem = 0;
+    E->rem_off[0] = 0;
+    int ar;
+    const ERL_NIF_TERM *tp;
+    if (p->type == AGN_REGISTER_MV) {
+        uint64_t tag = 0, tok = 0;
+        if (!enif_get_tuple(env, eff, &ar, &tp)) return -1;
+        if (ar == 2 && enif_is_identical(tp[0], atom(env, "reset")))
+            return push_entry(env, p, E, 0, 0, &tp[1]) ? -1 : 1;   /* {reset, Overridden} */
+        if (ar != 3 || term_id(env, p->tags, tp[0], &tag) || term_id(env, p->toks, tp[1], &tok))
+            return -1;
+        return push_entry(env, p, E, tag, tok, &tp[2]) ? -1 : 1;    /* {Value, Token, Overridden} */
+    }
+    /* set_aw: [{Elem, AddTokens, RemoveTokens}], one part per element (add_all /
+     * remove_all have several); a part with several add tokens becomes several
+     * entries, the removals riding on the first, as the Python encoder does */
+    ERL_NIF_TERM h, t = eff;
+    while (enif_get_list_cell(env, t, &h, &t)) {
+        uint64_t tag;
+        if (!enif_get_tuple(env, h, &ar, &tp) || ar != 3 || term_id(env, p->tags, tp[0], &tag))
+            return -1;
+        if (enif_is_empty_list(env, tp[1])) {
+            if (push_entry(env, p, E, tag, 0, &tp[2])) return -1;
+            continue;
+        }
+        ERL_NIF_TERM ah, at = tp[1];
+        int first = 1;
+        while (enif_get_list_cell(env, at, &ah, &at)) {
+            uint64_t tok;
+            if (term_id(env, p->toks, ah, &tok) ||
+                push_entry(env, p, E, tag, tok, first ? &tp[2] : NULL))
+                return -1;
+            first = 0;
+        }
+        if (!enif_is_empty_list(env, at)) return -1;
+    }
+    return enif_is_empty_list(env, t) ? (int)E->n : -1;
+}
+
+static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    if (argc != 5 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    uint64_t k, tx, row[256], mask[4];
+    int rc = key_index(env, p, argv[1], &k);
+    if (!rc) rc = clock_row(env, p, argv[2], row, mask);
+    if (!rc) rc = txid_of(env, p, argv[3], &tx);
+    if (rc == AGN_EINVAL) return enif_make_badarg(env);
+    if (rc) return error_tuple(env, rc);
+    const uint32_t D = p->D, W = p->W;
+    uint64_t keys[MAXE], txids[MAXE];
+    uint8_t same[MAXE];
+    int64_t eff[MAXE];
+    entries *E = enif_alloc(sizeof *E);
+    uint64_t *oc = enif_alloc((size_t)MAXE * D * 8), *ocm = enif_alloc((size_t)MAXE * W * 8);
+    if (!E || !oc || !ocm) {
+        enif_free(E);
+        enif_free(oc);
+        enif_free(ocm);
+        return error_tuple(env, AGN_ENOMEM);
+    }
+    uint32_t n = 1;
+    int invalid = 0;
+    if (p->type == AGN_COUNTER_PN) {
+        ErlNifSInt64 v;
+        invalid = !enif_get_int64(env, argv[4], &v) || v == AGN_EFFECT_INVALID;
+        eff[0] = invalid ? AGN_EFFECT_INVALID : (int64_t)v;
+        E->n = 0;
+    } else {
+        const int ne = effect_entries(env, p, argv[4], E);
+        if (ne < 0) {  /* not representable: one invalid entry (update/2 raises at read) */
+            E->n = 1;
+            E->nrem = 0;
+            E->tag[0] = AGN_TAG_INVALID;
+            E->add[0] = 0;
+            E->rem_off[0] = E->rem_off[1] = 0;
+            invalid = 1;
+        }
+        n = E->n;
+    }
+    uint32_t ids[MAXE];
+    uint8_t due[MAXE];
+    if (n == 0) {  /* an effect with no parts (add_all of []) changes nothing */
+        enif_free(E);
+        enif_free(oc);
+        enif_free(ocm);
+        return enif_make_tuple3(env, atom(env, "ok"), enif_make_uint(env, 0), atom(env, "false"));
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        keys[i] = k;
+        txids[i] = tx;
+        same[i] = i > 0;
+        memcpy(oc + (size_t)i * D, row, D * 8);
+        memcpy(ocm + (size_t)i * W, mask, W * 8);
+    }
+    rc = agn_oplog_append(p->log, n, keys, same, oc, ocm, txids,
+                          p->type == AGN_COUNTER_PN ? eff : NULL,
+                          p->type == AGN_COUNTER_PN ? NULL : E->tag,
+                          p->type == AGN_COUNTER_PN ? NULL : E->add,
+                          p->type == AGN_COUNTER_PN ? NULL : E->rem_off,
+                          p->type == AGN_COUNTER_PN ? NULL : E->rem, ids, due);
+    enif_free(E);
+    enif_free(oc);
+    enif_free(ocm);
+    (void)invalid;
+    if (rc) return error_tuple(env, rc);
+    return enif_make_tuple3(env, atom(env, "ok"), enif_make_uint(env, ids[0]),
+                            atom(env, due[0] ? "true" : "false"));
+}
+
+/* the state pairs of a set/register result -> orddict [{Elem, [Tok]}] /
+ * sorted [{Value, Token}] (decoded through the interners) */
+static ERL_NIF_TERM state_term(ErlNifEnv *env, part_res *p, uint32_t n, const uint32_t *tag,
+                               const uint64_t *tok) {
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    if (p->type == AGN_REGISTER_MV) {
+        for (uint32_t i = n; i-- > 0;)
+            l = enif_make_list_cell(env, enif_make_tuple2(env, id_term(env, p->tags, tag[i]),
+                                                         id_term(env, p->toks, tok[i])), l);
+        return l;
+    }
+    /* pairs come grouped by element (sorted), tokens in fold order */
+    uint32_t i = n;
+    while (i > 0) {
+        uint32_t j = i;
+        while (j > 0 && tag[j - 1] == tag[i - 1]) --j;
+        ERL_NIF_TERM toks = enif_make_list(env, 0);
+        for (uint32_t x = i; x-- > j;) toks = enif_make_list_cell(env, id_term(env, p->toks, tok[x]), toks);
+        l = enif_make_list_cell(env, enif_make_tuple2(env, id_term(env, p->tags, tag[i - 1]), toks), l);
+        i = j;
+    }
+    return l;
+}
+
+static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, const agn_key_result *o,
+                                const uint64_t *ct, const uint64_t *ctm) {
+    if (o->flags & AGN_F_ERR_CORRUPTED) return enif_make_tuple2(env, atom(env, "error"), atom(env, "corrupted_ops_cache"));
+    if (o->flags & AGN_F_ERR_UNEXPECTED)
+        return enif_make_tuple2(env, atom(env, "error"),
+                                enif_make_tuple3(env, atom(env, "unexpected_operation"),
+                                                 atom(env, "invalid_effect"),
+                                                 enif_make_uint(env, p->type)));
+    ERL_NIF_TERM v = p->type == AGN_COUNTER_PN ? enif_make_int64(env, o->value)
+                                               : state_term(env, p, o->out_n, o->out_tag, o->out_tok);
+    ERL_NIF_TERM lct = (o->flags & AGN_F_CT_IGNORE) ? atom(env, "ignore") : clock_pairs(env, p, ct, ctm);
+    ERL_NIF_TERM res[6] = {atom(env, "ok"), v, enif_make_int64(env, o->hole), lct,
+                           atom(env, (o->flags & AGN_F_NEWSS) ? "true" : "false"),
+                           enif_make_uint(env, o->count)};
+    return enif_make_tuple_from_array(env, res, 6);
+}
+
+/* one read through the partition's batcher */
+static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM key,
+                                     ERL_NIF_TERM rpairs, ERL_NIF_TERM sct, ERL_NIF_TERM txid,
+                                     ERL_NIF_TERM base, int gc) {
+    uint64_t k, tx, R[256], Rm[4], S[256], Sm[4], ct[256], ctm[4];
+    int rc = key_index(env, p, key, &k);
+    if (!rc) rc = clock_row(env, p, rpairs, R, Rm);
+    if (!rc) rc = txid_of(env, p, txid, &tx);
+    const int has_sct = !enif_is_identical(sct, atom(env, "ignore"));
+    if (!rc && has_sct) rc = clock_row(env, p, sct, S, Sm);
+    if (rc == AGN_EINVAL) return enif_make_badarg(env);
+    if (rc) return error_tuple(env, rc);
+    agn_key_read rd;
+    agn_key_result o;
+    memset(&rd, 0, sizeof rd);
+    memset(&o, 0, sizeof o);
+    rd.key = k;
+    rd.R = R;
+    rd.R_mask = Rm;
+    rd.sct = has_sct ? S : NULL;
+    rd.sct_mask = has_sct ? Sm : NULL;
+    rd.txid = tx;
+    rd.flags = gc ? AGN_READ_GC : 0;
+    o.lastct = ct;
+    o.lastct_mask = ctm;
+    uint32_t len = 0, nb = 0;
+    uint32_t *btag = NULL, *otag = NULL;
+    uint64_t *btok = NULL, *otok = NULL;
+    if (p->type == AGN_COUNTER_PN) {
+        ErlNifSInt64 v = 0;
+        if (!enif_is_identical(base, atom(env, "undefined")) && !enif_get_int64(env, base, &v))
+            return enif_make_badarg(env);
+        rd.base_value = v;
+    } else {
+        /* base state pairs: set_aw orddict [{Elem, [Tok]}], register_mv [{V, Tok}] */
+        unsigned nl = 0;
+        if (!enif_get_list_length(env, base, &nl)) return enif_make_badarg(env);
+        ERL_NIF_TERM h, t = base;
+        uint32_t cap = 0;
+        while (enif_get_list_cell(env, t, &h, &t)) {
+            int ar;
+            const ERL_NIF_TERM *tp;
+            unsigned m = 1;
+            if (!enif_get_tuple(env, h, &ar, &tp) || ar != 2) return enif_make_badarg(env);
+            if (p->type == AGN_SET_AW && !enif_get_list_length(env, tp[1], &m)) return enif_make_badarg(env);
+            cap += m;
+        }
+        btag = enif_alloc(4 * (cap + 1));
+        btok = enif_alloc(8 * (cap + 1));
+        for (t = base; enif_get_list_cell(env, t, &h, &t);) {
+            int ar;
+            const ERL_NIF_TERM *tp;
+            uint64_t tg, tk;
+            enif_get_tuple(env, h, &ar, &tp);
+            if (term_id(env, p->tags, tp[0], &tg)) goto oom;
+            if (p->type == AGN_REGISTER_MV) {
+                if (term_id(env, p->toks, tp[1], &tk)) goto oom;
+                btag[nb] = (uint32_t)tg;
+                btok[nb++] = tk;
+            } else {
+                ERL_NIF_TERM th, tt = tp[1];
+                while (enif_get_list_cell(env, tt, &th, &tt)) {
+                    if (term_id(env, p->toks, th, &tk)) goto oom;
+                    btag[nb] = (uint32_t)tg;
+                    btok[nb++] = tk;
+                }
+            }
+        }
+        rd.n_base = nb;
+        rd.base_tag = btag;
+        rd.base_tok = btok;
+        if (agn_oplog_key_meta(p->log, 1, &k, &len, NULL, NULL)) goto oom;
+        o.out_cap = len + nb;
+        otag = enif_alloc(4 * (o.out_cap + 1));
+        otok = enif_alloc(8 * (o.out_cap + 1));
+        o.out_tag = otag;
+        o.out_tok = otok;
+    }
+    rc = agn_batcher_read(p->bt, &rd, &o);
+    ERL_NIF_TERM r;
+    if (rc) r = error_tuple(env, rc);
+    else if (p->cached && o.status == AGN_SS_LOG)
+        r = enif_make_tuple2(env, atom(env, "error"), atom(env, "no_snapshot"));
+    else r = read_result(env, p, &o, ct, ctm);
+    enif_free(btag);
+    enif_free(btok);
+    enif_free(otag);
+    enif_free(otok);
+    return r;
+oom:
+    enif_free(btag);
+    enif_free(btok);
+    return error_tuple(env, AGN_ENOMEM);
+}
+
+static ERL_NIF_TERM nif_part_read(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    if (argc != 5 || !get_part(env, argv[0], &p) || !p->cached) return enif_make_badarg(env);
+    return part_read_common(env, p, argv[1], argv[2], atom(env, "ignore"), argv[3],
+                            atom(env, "undefined"), enif_is_identical(argv[4], atom(env, "true")));
+}
+
+static ERL_NIF_TERM nif_part_materialize(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    if (argc != 6 || !get_part(env, argv[0], &p) || p->cached) return enif_make_badarg(env);
+    return part_read_common(env, p, argv[1], argv[2], argv[3], argv[4], argv[5], 0);
+}
+
+static ERL_NIF_TERM nif_part_gc(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    if (argc != 3 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    uint64_t k, row[256], mask[4];
+    int rc = key_index(env, p, argv[1], &k);
+    if (!rc) rc = clock_row(env, p, argv[2], row, mask);
+    if (rc == AGN_EINVAL) return enif_make_badarg(env);
+    if (rc) return error_tuple(env, rc);
+    agn_ctx *c = p->ctx->ctx;
+    const uint8_t one = 1;
+    pthread_mutex_lock(&p->gc_mu);
+    rc = agn_memset_d(c, p->d_prune, 0, p->K, NULL);
+    if (!rc) rc = agn_memcpy_h2d(c, p->d_prune + k, &one, 1, NULL);
+    if (!rc) rc = agn_memcpy_h2d(c, p->d_thr + k * p->D, row, p->D * 8, NULL);
+    if (!rc) rc = agn_memcpy_h2d(c, p->d_thrm + k * p->W, mask, p->W * 8, NULL);
+    if (!rc) rc = agn_stream_sync(c, NULL);
+    if (!rc) rc = agn_oplog_prune(p->log, p->d_prune, p->d_thr, p->d_thrm, NULL, NULL);
+    pthread_mutex_unlock(&p->gc_mu);
+    return rc ? error_tuple(env, rc) : atom(env, "ok");
+}
+
+static ERL_NIF_TERM nif_part_stats(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    uint64_t e, s, t;
+    if (argc != 1 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    int rc = agn_oplog_stats(p->log, &e, &s, &t);
+    if (rc) return error_tuple(env, rc);
+    return enif_make_tuple3(env, enif_make_uint64(env, e), enif_make_uint64(env, s),
+                            enif_make_uint64(env, t));
+}
+
+static ERL_NIF_TERM nif_part_key_meta(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    uint64_t k;
+    uint32_t len = 0, ll = 0, ct = 0;
+    if (argc != 2 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    int rc = key_index(env, p, argv[1], &k);
+    if (!rc) rc = agn_oplog_key_meta(p->log, 1, &k, &len, &ll, &ct);
+    if (rc) return error_tuple(env, rc);
+    return enif_make_tuple3(env, enif_make_uint(env, len), enif_make_uint(env, ll),
+                            enif_make_uint(env, ct));
+}
+
 static ErlNifFunc funcs[] = {
     {"open", 1, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_open", 5, nif_part_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_update", 5, nif_part_update, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_read", 5, nif_part_read, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_materialize", 6, nif_part_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_gc", 3, nif_part_gc, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_stats", 1, nif_part_stats, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_key_meta", 2, nif_part_key_meta, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"materialize", 6, nif_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"gst_min", 5, nif_gst_min, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"select_base", 7, nif_select_base, ERL_NIF_DIRTY_JOB_IO_BOUND},

@@ -1,15 +1,22 @@
 %% antidote_gpu_nif — Erlang side of the MI355X materialization engine.
 %%
 %% Drop-in for the hot path of clocksi_materializer:materialize/4
-%% (src/clocksi_materializer.erl:82-101) and stable_time_functions:get_min_time/1
-%% (src/stable_time_functions.erl:51-85).  Terms are encoded here into the SoA
-%% binaries of include/antidote_gpu.h; the NIF (antidote_gpu_nif.c) runs the HIP
+%% (src/clocksi_materializer.erl:82-101), materializer_vnode update/2 and
+%% read/6 (src/materializer_vnode.erl:96-110) over an engine-owned partition
+%% log, and stable_time_functions:get_min_time/1
+%% (src/stable_time_functions.erl:51-85).  Terms are encoded here (per-call
+%% path) or in the NIF (partition path, exact interning) into the SoA arrays
+%% of include/antidote_gpu.h; the NIF (antidote_gpu_nif.c) runs the HIP
 %% kernels on a dirty scheduler.  Built only where erl_nif.h exists; see
-%% INTEGRATION.md for the two-line patches that route the reference through it.
+%% INTEGRATION.md for the patches that route the reference through it.
 -module(antidote_gpu_nif).
 
 -export([open/1, materialize/6, gst_min/5, select_base/7]).
 -export([materialize/4, get_min_time/1]).
+%% engine-owned partition (one per materializer_vnode)
+-export([part_open/5, part_update/5, part_read/5, part_materialize/6, part_gc/3,
+         part_stats/1, part_key_meta/2]).
+-export([new_partition/3, update/3, read/4, read_from/6, gc/3]).
 
 -on_load(init/0).
 
@@ -36,6 +43,13 @@ open(_Device) -> erlang:nif_error(not_loaded).
 materialize(_Ctx, _Type, _NDcs, _Log, _Read, _CapOff) -> erlang:nif_error(not_loaded).
 gst_min(_Ctx, _NDcs, _NParts, _Clocks, _Defined) -> erlang:nif_error(not_loaded).
 select_base(_Ctx, _NDcs, _CacheOff, _Clocks, _ClockMask, _R, _RMask) -> erlang:nif_error(not_loaded).
+part_open(_Ctx, _Type, _NDcs, _NKeys, _Cached) -> erlang:nif_error(not_loaded).
+part_update(_Part, _Key, _OcPairs, _TxId, _Effect) -> erlang:nif_error(not_loaded).
+part_read(_Part, _Key, _RPairs, _TxId, _Gc) -> erlang:nif_error(not_loaded).
+part_materialize(_Part, _Key, _RPairs, _Sct, _TxId, _Base) -> erlang:nif_error(not_loaded).
+part_gc(_Part, _Key, _ThresholdPairs) -> erlang:nif_error(not_loaded).
+part_stats(_Part) -> erlang:nif_error(not_loaded).
+part_key_meta(_Part, _Key) -> erlang:nif_error(not_loaded).
 
 ctx() ->
     case persistent_term:get({?MODULE, ctx}, undefined) of
@@ -60,8 +74,11 @@ materialize(Type, TxId, MinSnapshotTime,
     Dcs = dc_table([MinSnapshotTime, SCT | [clock_of(Op) || {_, Op} <- OpList]]),
     D = max(1, length(Dcs)),
     Idx = maps:from_list(lists:zip(Dcs, lists:seq(0, length(Dcs) - 1))),
-    {Log, Terms, Tags, Toks} = encode_log(Type, TypeId, OpList, Idx, D),
-    {Read, CapOff} = encode_read(TypeId, Idx, D, MinSnapshotTime, SCT, TxId, Base, Log, Tags, Toks),
+    TxCodes = txid_codes(TxId, OpList),
+    {Log, Terms, Tags0, Toks0} = encode_log(Type, TypeId, OpList, Idx, D, TxCodes),
+    {BaseOff, BaseTag, BaseTok, Tags, Toks} = encode_base(TypeId, Base, Tags0, Toks0),
+    {Read, CapOff} = encode_read(TypeId, Idx, D, MinSnapshotTime, SCT, txid_code(TxId, TxCodes),
+                                 Base, {BaseOff, BaseTag, BaseTok}, Log),
     {ok, R} = materialize(ctx(), TypeId, D, Log, Read, CapOff),
     decode(Type, TypeId, Dcs, D, R, Terms, Tags, Toks).
 
@@ -83,19 +100,33 @@ row(Clock, Idx, D) ->
     W = (D + 63) div 64,
     {<< <<V:64/native>> || V <- tuple_to_list(Vals) >>, <<Mask:(64 * W)/little>>}.
 
-encode_log(Type, TypeId, OpList, Idx, D) ->
-    N = length(OpList),
+%% TxIds are interned exactly per call (a map keyed by the term itself, =:=
+%% semantics; a #tx_id{} holds integers and a pid, where == and =:= agree):
+%% is_op_in_snapshot compares TxId == Op#clocksi_payload.txid
+%% (src/clocksi_materializer.erl:220), so no two distinct TxIds may share a code.
+txid_codes(TxId, OpList) ->
+    All = [TxId | [Op#clocksi_payload.txid || {_, Op} <- OpList]],
+    {Map, _} = lists:foldl(fun(ignore, Acc) -> Acc;
+                              (T, {M, N}) -> case maps:is_key(T, M) of
+                                                 true -> {M, N};
+                                                 false -> {maps:put(T, N, M), N + 1}
+                                             end
+                           end, {#{}, 1}, All),
+    Map.
+
+encode_log(Type, TypeId, OpList, Idx, D, TxCodes) ->
     KeyType = case lists:all(fun({_, #clocksi_payload{type = T}}) -> T =:= Type end, OpList) of
                   true -> TypeId;
                   false -> 16#FF
               end,
-    {Rows, Masks} = lists:unzip([row(clock_of(Op), Idx, D) || {_, Op} <- OpList]),
-    Ids = << <<Id:32/native>> || {Id, _} <- OpList >>,
-    TxIds = << <<(erlang:phash2(Op#clocksi_payload.txid, 16#7FFFFFFF) + 1):64/native>> || {_, Op} <- OpList >>,
-    Base = {<<0:64/native, N:64/native>>, <<KeyType:8>>, iolist_to_binary(Rows),
-            iolist_to_binary(Masks), Ids, TxIds},
     case TypeId of
         ?COUNTER ->
+            N = length(OpList),
+            {Rows, Masks} = lists:unzip([row(clock_of(Op), Idx, D) || {_, Op} <- OpList]),
+            Ids = << <<Id:32/native>> || {Id, _} <- OpList >>,
+            TxIds = << <<(txid_code(Op#clocksi_payload.txid, TxCodes)):64/native>> || {_, Op} <- OpList >>,
+            Base = {<<0:64/native, N:64/native>>, <<KeyType:8>>, iolist_to_binary(Rows),
+                    iolist_to_binary(Masks), Ids, TxIds},
             {Effs, Terms} = lists:foldl(
                 fun({_, #clocksi_payload{op_param = E}}, {Acc, T}) when is_integer(E),
                                                                         E > ?INVALID_EFFECT,
@@ -109,39 +140,83 @@ encode_log(Type, TypeId, OpList, Idx, D) ->
                      iolist_to_binary(lists:reverse(Effs))), <<>>), <<>>), <<>>), <<>>),
              maps:from_list(Terms), #{}, #{}};
         _ ->
-            %% one entry per op (add_all / multi-part effects are split by the
-            %% Python reference encoder; this shim keeps one part per op)
-            encode_tag_log(Base, OpList, TypeId)
+            %% one entry per {Elem, Add, Rem} part (add_all / remove_all) and
+            %% per extra add token, all under the op's id
+            encode_tag_log(KeyType, OpList, TypeId, Idx, D, TxCodes)
     end.
 
-encode_tag_log(Base, OpList, TypeId) ->
-    {Tags, Toks, Tag, Add, RemOff, Rem, Terms, _} = lists:foldl(
-        fun({_, #clocksi_payload{op_param = E}}, {Tg, Tk, TagA, AddA, OffA, RemA, Tm, I}) ->
-                case part(TypeId, E) of
-                    {ok, TagTerm, AddTok, Rems} ->
-                        {Tg1, TagId} = intern(TagTerm, Tg),
-                        {Tk1, AddId} = case AddTok of none -> {Tk, 0}; _ -> intern(AddTok, Tk) end,
-                        {Tk2, RemIds} = lists:foldl(fun(X, {T, L}) -> {T2, Id} = intern(X, T), {T2, [Id | L]} end,
-                                                    {Tk1, []}, Rems),
-                        Off = hd(OffA) + length(RemIds),
-                        {Tg1, Tk2, [<<TagId:32/native>> | TagA], [<<AddId:64/native>> | AddA],
-                         [Off | OffA], [[<<R:64/native>> || R <- lists:reverse(RemIds)] | RemA], Tm, I + 1};
-                    error ->
-                        {Tg, Tk, [<<16#FFFFFFFF:32/native>> | TagA], [<<0:64>> | AddA],
-                         [hd(OffA) | OffA], RemA, maps:put(I, E, Tm), I + 1}
-                end
-        end, {#{}, #{}, [], [], [0], [], #{}, 0}, OpList),
-    Log = list_to_tuple(tuple_to_list(Base) ++
-                        [<<>>, iolist_to_binary(lists:reverse(Tag)), iolist_to_binary(lists:reverse(Add)),
-                         << <<O:32/native>> || O <- lists:reverse(RemOff) >>,
-                         iolist_to_binary(lists:reverse(Rem))]),
+txid_code(ignore, _) -> 0;
+txid_code(T, Codes) -> maps:get(T, Codes).
+
+encode_tag_log(KeyType, OpList, TypeId, Idx, D, TxCodes) ->
+    %% entries: {OpId, Op, TagTerm | invalid, AddTok | none, Rems}
+    Entries = lists:append([op_entries(TypeId, Id, Op) || {Id, Op} <- OpList]),
+    N = length(Entries),
+    {Rows, Masks} = lists:unzip([row(clock_of(Op), Idx, D) || {_, Op, _, _, _} <- Entries]),
+    Ids = << <<Id:32/native>> || {Id, _, _, _, _} <- Entries >>,
+    TxIds = << <<(txid_code(Op#clocksi_payload.txid, TxCodes)):64/native>> || {_, Op, _, _, _} <- Entries >>,
+    {Tags, Toks, TagA, AddA, OffA, RemA, Terms, _} = lists:foldl(
+        fun({_, Op, invalid, _, _}, {Tg, Tk, TagA0, AddA0, OffA0, RemA0, Tm, I}) ->
+                {Tg, Tk, [<<16#FFFFFFFF:32/native>> | TagA0], [<<0:64>> | AddA0],
+                 [hd(OffA0) | OffA0], RemA0, maps:put(I, Op#clocksi_payload.op_param, Tm), I + 1};
+           ({_, _, TagTerm, AddTok, Rems}, {Tg, Tk, TagA0, AddA0, OffA0, RemA0, Tm, I}) ->
+                {Tg1, TagId} = intern(TagTerm, Tg),
+                {Tk1, AddId} = case AddTok of none -> {Tk, 0}; _ -> intern(AddTok, Tk) end,
+                {Tk2, RemIds} = lists:foldl(fun(X, {T, L}) -> {T2, Id} = intern(X, T), {T2, [Id | L]} end,
+                                            {Tk1, []}, Rems),
+                Off = hd(OffA0) + length(RemIds),
+                {Tg1, Tk2, [<<TagId:32/native>> | TagA0], [<<AddId:64/native>> | AddA0],
+                 [Off | OffA0], [[<<R:64/native>> || R <- lists:reverse(RemIds)] | RemA0], Tm, I + 1}
+        end, {#{}, #{}, [], [], [0], [], #{}, 0}, Entries),
+    Log = {<<0:64/native, N:64/native>>, <<KeyType:8>>, iolist_to_binary(Rows),
+           iolist_to_binary(Masks), Ids, TxIds, <<>>,
+           iolist_to_binary(lists:reverse(TagA)), iolist_to_binary(lists:reverse(AddA)),
+           << <<O:32/native>> || O <- lists:reverse(OffA) >>,
+           iolist_to_binary(lists:reverse(RemA))},
     {Log, Terms, Tags, Toks}.
 
-part(?SET_AW, [{Elem, Adds, Rems}]) when length(Adds) =< 1 ->
-    {ok, Elem, case Adds of [A] -> A; [] -> none end, Rems};
-part(?REGISTER_MV, {reset, Ovr}) -> {ok, reset, none, Ovr};
-part(?REGISTER_MV, {Value, Token, Ovr}) -> {ok, Value, Token, Ovr};
-part(_, _) -> error.
+%% the entries of one op: set_aw parts {Elem, Adds, Rems} (several for
+%% add_all / remove_all; a part with n add tokens gives n entries, the removals
+%% riding on the first), register_mv {V, Tok, Ovr} / {reset, Ovr}; an effect the
+%% CRDT could not apply stays one invalid entry (update/2 raises at read)
+op_entries(TypeId, Id, Op = #clocksi_payload{op_param = E}) ->
+    case parts(TypeId, E) of
+        {ok, Parts} -> [{Id, Op, Tag, Add, Rems} || {Tag, Add, Rems} <- Parts];
+        error -> [{Id, Op, invalid, none, []}]
+    end.
+
+parts(?SET_AW, Parts) when is_list(Parts) ->
+    try {ok, lists:append([set_part(P) || P <- Parts])}
+    catch _:_ -> error
+    end;
+parts(?REGISTER_MV, {reset, Ovr}) when is_list(Ovr) -> {ok, [{reset, none, Ovr}]};
+parts(?REGISTER_MV, {Value, Token, Ovr}) when is_list(Ovr) -> {ok, [{Value, Token, Ovr}]};
+parts(_, _) -> error.
+
+set_part({Elem, [], Rems}) when is_list(Rems) -> [{Elem, none, Rems}];
+set_part({Elem, [A | More], Rems}) when is_list(Rems), is_list(More) ->
+    [{Elem, A, Rems} | [{Elem, X, []} || X <- More]].
+
+%% #materialized_snapshot.value of a set_aw ([{Elem, [Tok]}]) or register_mv
+%% ([{Value, Token}]) base, as (elem/value, token) pairs through the same
+%% intern maps as the log
+encode_base(?SET_AW, State, Tags, Toks) ->
+    base_pairs([{E, T} || {E, Ts} <- State, T <- Ts], Tags, Toks);
+encode_base(?REGISTER_MV, State, Tags, Toks) ->
+    base_pairs(State, Tags, Toks);
+encode_base(_, _, Tags, Toks) ->
+    {<<>>, <<>>, <<>>, Tags, Toks}.
+
+base_pairs(Pairs, Tags, Toks) ->
+    {TagB, TokB, Tags1, Toks1} = lists:foldl(
+        fun({E, T}, {TgA, TkA, Tg, Tk}) ->
+                {Tg1, TagId} = intern(E, Tg),
+                {Tk1, TokId} = intern(T, Tk),
+                {[<<TagId:32/native>> | TgA], [<<TokId:64/native>> | TkA], Tg1, Tk1}
+        end, {[], [], Tags, Toks}, Pairs),
+    N = length(Pairs),
+    {<<0:64/native, N:64/native>>, iolist_to_binary(lists:reverse(TagB)),
+     iolist_to_binary(lists:reverse(TokB)), Tags1, Toks1}.
 
 intern(Term, Map) ->
     case maps:find(Term, Map) of
@@ -149,18 +224,20 @@ intern(Term, Map) ->
         error -> Id = maps:size(Map) + 1, {maps:put(Term, Id, Map), Id}
     end.
 
-encode_read(TypeId, Idx, D, R, SCT, TxId, Base, Log, _Tags, _Toks) ->
+encode_read(TypeId, Idx, D, R, SCT, TxCode, Base, {BaseOff, BaseTag, BaseTok}, Log) ->
     {RRow, RMask} = row(R, Idx, D),
     {SRow, SMask, SIgn} = case SCT of
                               ignore -> {<<>>, <<>>, <<1:8>>};
                               _ -> {Sr, Sm} = row(SCT, Idx, D), {Sr, Sm, <<0:8>>}
                           end,
-    Tx = case TxId of ignore -> <<0:64>>; _ -> <<(erlang:phash2(TxId, 16#7FFFFFFF) + 1):64/native>> end,
+    Tx = <<TxCode:64/native>>,
     BaseValue = case TypeId of ?COUNTER -> <<Base:64/signed-native>>; _ -> <<>> end,
-    Read = {<<0:64/native>>, RRow, RMask, SRow, SMask, SIgn, Tx, BaseValue, <<>>, <<>>, <<>>},
+    Read = {<<0:64/native>>, RRow, RMask, SRow, SMask, SIgn, Tx, BaseValue, BaseOff, BaseTag,
+            BaseTok},
     Cap = case TypeId of
               ?COUNTER -> <<>>;
-              _ -> N = byte_size(element(8, Log)) div 8, <<0:64/native, N:64/native>>
+              _ -> N = byte_size(element(9, Log)) div 8 + byte_size(BaseTok) div 8,
+                   <<0:64/native, N:64/native>>
           end,
     {Read, Cap}.
 
@@ -222,3 +299,45 @@ get_min_time(Dict) ->
     Words = [W || <<W:64/native>> <= Vec],
     dict:from_list([{Dc, T} || {Dc, T} <- lists:zip(Dcs, lists:sublist(Words, length(Dcs))),
                                T =/= ?U64_MAX]).
+
+%% ---------------------------------------------------------------------------
+%% The engine-owned partition: materializer_vnode's ops cache in HBM.
+%% Cached = true: the snapshot cache lives on the device too (counter_pn),
+%% read/4 is the whole read/6; Cached = false: the reference's own ETS
+%% snapshot cache stays, and read_from/6 is materialize/4 over the resident ops.
+new_partition(Type, NKeys, Cached) ->
+    {ok, Ps} = application:get_env(antidote, gpu_dcs),   % DC slots per clock (<= 256)
+    part_open(ctx(), type_id(Type), Ps, NKeys, Cached).
+
+%% update/2 -> op_insert_gc/3: the op's OpSSCommit is its snapshot_time with
+%% the commit DC set to the commit time (src/clocksi_materializer.erl:224).
+%% Returns {ok, OpId, GcDue}; GcDue = true is op_insert_gc's GC trigger
+%% (:635), for which the caller runs the GC read (read/4 with gc, or the
+%% reference's internal_read(..., true) + gc/3).
+update(Part, Key, #clocksi_payload{snapshot_time = SS, commit_time = {Dc, Ct},
+                                   txid = TxId, op_param = Effect}) ->
+    part_update(Part, Key, dict:to_list(dict:store(Dc, Ct, SS)), TxId, Effect).
+
+%% read/6 on a cached partition: {ok, Value} | {error, no_snapshot} (the
+%% caller reads the log: get_from_snapshot_log, :416-419) | {error, Reason}.
+read(Part, Key, MinSnapshotTime, TxId) ->
+    case part_read(Part, Key, dict:to_list(MinSnapshotTime), TxId, false) of
+        {ok, Value, _NewLastOp, _LastOpCt, _IsNewSS, _Count} -> {ok, Value};
+        Other -> Other
+    end.
+
+%% materialize/4 over the partition's resident ops from a base snapshot the
+%% caller's ETS snapshot cache selected: same result as
+%% clocksi_materializer:materialize/4 ({ok, V, NewLastOp, LastOpCt, IsNewSS, Count}).
+read_from(Part, Key, MinSnapshotTime, SCT, TxId, BaseValue) ->
+    Sct = case SCT of ignore -> ignore; _ -> dict:to_list(SCT) end,
+    case part_materialize(Part, Key, dict:to_list(MinSnapshotTime), Sct, TxId, BaseValue) of
+        {ok, V, H, Ct, NewSS, C} ->
+            {ok, V, H, case Ct of ignore -> ignore; _ -> dict:from_list(Ct) end, NewSS, C};
+        Other -> Other
+    end.
+
+%% snapshot_insert_gc's prune_ops + resize for one key (threshold = the
+%% vectorclock:min of the kept snapshots, :523-527).
+gc(Part, Key, Threshold) ->
+    part_gc(Part, Key, dict:to_list(Threshold)).
