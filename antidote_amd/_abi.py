@@ -173,6 +173,7 @@ PROTOTYPES = {
     "agn_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
     "agn_comm_destroy": (C.c_int, [P]),
     "agn_gst_allreduce": (C.c_int, [P, P, C.c_uint64, P]),
+    "agn_gst_merge": (C.c_int, [C.c_uint32, C.c_uint64, P, P]),
     "agn_gen_host": (C.c_int, [C.POINTER(AgnGenCfg), C.POINTER(AgnLog), C.POINTER(AgnRead)]),
     "agn_gen_free_host": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead)]),
     "agn_gen_dev": (C.c_int, [P, C.POINTER(AgnGenCfg), C.POINTER(AgnLog),

@@ -716,6 +716,20 @@ int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *nw, int *c
     return AGN_OK;
 }
 
+int agn_gst_merge(uint32_t n_dcs, uint64_t n_vecs, const uint64_t *vecs, uint64_t *out) {
+    if (!out || (n_vecs && !vecs)) return fail(AGN_EINVAL, "gst_merge: null buffer");
+    if (n_dcs == 0) return fail(AGN_EINVAL, "gst_merge: n_dcs = 0");
+    const uint64_t W = (uint64_t)n_dcs + 1;
+    for (uint64_t j = 0; j < W; ++j) out[j] = UINT64_MAX;
+    out[n_dcs] = 1;  // no vector: nothing undefined
+    for (uint64_t v = 0; v < n_vecs; ++v)
+        for (uint64_t j = 0; j < W; ++j) out[j] = std::min(out[j], vecs[v * W + j]);
+    if (out[n_dcs] == 0)  // some partition undefined: every present DC -> 0 (:78-84)
+        for (uint32_t d = 0; d < n_dcs; ++d)
+            if (out[d] != UINT64_MAX) out[d] = 0;
+    return AGN_OK;
+}
+
 // ---- RCCL ------------------------------------------------------------------------
 int agn_comm_unique_id(uint8_t *out_id) {
     static_assert(sizeof(ncclUniqueId) <= AGN_UNIQUE_ID_BYTES, "unique id size");

@@ -563,6 +563,12 @@ int agn_comm_unique_id(uint8_t *out_id /* [AGN_UNIQUE_ID_BYTES] */);
 int agn_comm_init(agn_ctx *ctx, int nranks, int rank, const uint8_t *id);
 int agn_comm_destroy(agn_ctx *ctx);
 int agn_gst_allreduce(agn_ctx *ctx, uint64_t *dev_vec, uint64_t n_words, void *stream);
+/* The same exchange over any other transport (disterl casts, a gloo /
+ * host all-gather): the [n_vecs][D+1] vectors agn_gst_min produced on the
+ * nodes (host pointers) -> out[D+1] = their element-wise min followed by
+ * agn_gst_finalize's rule -- get_min_time over {local_merged, remote...}
+ * (src/meta_data_sender.erl:244).  Host-only. */
+int agn_gst_merge(uint32_t n_dcs, uint64_t n_vecs, const uint64_t *vecs, uint64_t *out);
 
 /* ---- synthetic op logs (BASELINE.md §3 / SURVEY.md §8(d) generator) -----
  * Deterministic SplitMix64 streams, one per key (global key index

@@ -1,8 +1,12 @@
 """World-size-2 CPU tests (torch.distributed gloo on 127.0.0.1) of the N>1
 paths: vnode-partition sharding of the materialize batch and the GST
 local-min -> MIN-allreduce -> finalize exchange.  The kernels are replaced by
-the C oracle (CPU); what is tested is the placement and the exchange algebra
-the GPU ranks use (bench.py, stable_time_functions.GstExchange)."""
+the C oracle (CPU); what is tested is the placement and the exchange: each
+rank's local vector (oracle_gst_min = agn_gst_min's contract) crosses ranks
+through torch.distributed and is merged by the product's host exchange
+agn_gst_merge (the all-gather + min of meta_data_sender, the transport-
+agnostic twin of agn_gst_allreduce's RCCL min), with undefined partitions on
+one rank so the flag word crosses ranks."""
 import ctypes as C
 import os
 import socket
@@ -60,19 +64,31 @@ def _worker(rank, world, port, q):
         dist.all_gather(gathered, vals)
         # ---- GST: each rank owns partitions p with p % world == rank
         D, P = 6, 64
-        rng = np.random.default_rng(11)
-        clocks = (1_000_000 + rng.integers(0, 10 ** 6, (P, D))).astype(np.uint64)
-        clocks[rng.random((P, D)) < 0.1] = np.uint64(sharding.U64_MAX)
-        defined = np.ones(P, np.uint8)  # all defined: the per-DC min survives the merge
-        mine = [p for p in range(P) if sharding.gpu_of(p, world) == rank]
-        local = sharding.local_gst_vector(clocks[mine], defined[mine])
-        # transport: u64 -> i64 with U64_MAX -> I64_MAX (clock values < 2^63)
-        t = torch.tensor(np.where(local == np.uint64(sharding.U64_MAX), np.iinfo(np.int64).max,
-                                  local.astype(np.int64)))
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        merged = t.numpy().astype(np.uint64)
-        merged[t.numpy() == np.iinfo(np.int64).max] = np.uint64(sharding.U64_MAX)
-        q.put((rank, [g.numpy() for g in gathered], sharding.finalize(merged), clocks, defined))
+        lib = _abi.bind(C.CDLL(os.path.join(ROOT, "antidote_amd", "libantidote_gpu.so")),
+                        _abi.PROTOTYPES)
+        gsts = []
+        for case, p_undef in enumerate((0.0, 0.05)):
+            rng = np.random.default_rng(11 + case)
+            clocks = (1_000_000 + rng.integers(0, 10 ** 6, (P, D))).astype(np.uint64)
+            clocks[rng.random((P, D)) < 0.1] = np.uint64(sharding.U64_MAX)
+            defined = (rng.random(P) >= p_undef).astype(np.uint8)
+            if p_undef:   # undefined partitions on rank 1's side only
+                defined[[p for p in range(P) if sharding.gpu_of(p, world) == 0]] = 1
+                defined[1] = 0
+            mine = [p for p in range(P) if sharding.gpu_of(p, world) == rank]
+            local = np.zeros(D + 1, np.uint64)
+            cm, dm = np.ascontiguousarray(clocks[mine]), np.ascontiguousarray(defined[mine])
+            _oracle().oracle_gst_min(D, len(mine), 1, cm.ctypes.data, dm.ctypes.data,
+                                     local.ctypes.data, 0)
+            # the local vector is agn_gst_min's (before finalize): check it
+            assert np.array_equal(local, sharding.local_gst_vector(cm, dm))
+            vecs = [torch.zeros(D + 1, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(vecs, torch.from_numpy(local.view(np.int64).copy()))
+            allv = np.ascontiguousarray(np.stack([v.numpy() for v in vecs]).view(np.uint64))
+            out = np.zeros(D + 1, np.uint64)
+            assert lib.agn_gst_merge(D, world, allv.ctypes.data, out.ctypes.data) == 0
+            gsts.append((out, clocks, defined))
+        q.put((rank, [g.numpy() for g in gathered], gsts))
     finally:
         dist.destroy_process_group()
 
@@ -100,9 +116,10 @@ def test_world2_sharding_and_gst():
     for r in range(world):
         assert np.array_equal(gathered[r], full.value[r::world])
     # GST after the exchange == get_min_time over every partition (oracle)
-    _, _, gst, clocks, defined = outs[0]
-    assert np.array_equal(outs[1][2], gst)
-    want = np.zeros(clocks.shape[1] + 1, np.uint64)
-    _oracle().oracle_gst_min(clocks.shape[1], clocks.shape[0], 1, clocks.ctypes.data,
-                             defined.ctypes.data, want.ctypes.data, 1)
-    assert np.array_equal(gst, want)
+    for case, (gst, clocks, defined) in enumerate(outs[0][2]):
+        assert np.array_equal(outs[1][2][case][0], gst)
+        want = np.zeros(clocks.shape[1] + 1, np.uint64)
+        _oracle().oracle_gst_min(clocks.shape[1], clocks.shape[0], 1, clocks.ctypes.data,
+                                 defined.ctypes.data, want.ctypes.data, 1)
+        assert np.array_equal(gst, want)
+        assert bool(want[-1] == 0) == bool((defined == 0).any())
