@@ -117,7 +117,8 @@ class MaterializerVnode:
             t = OpsTuple(key, 0, 0)
         new_ops = self.prune_ops(t, commit_time)
         self.snapshot_cache[key] = pruned
-        list_len, new_length = t.list_len, len(new_ops)
+        # prune_ops' NewLength is 1 when nothing survives (:580-583)
+        list_len, new_length = t.list_len, max(len(new_ops), 1)
         if new_length > list_len - RESIZE_THRESHOLD:
             new_list_len = list_len * 2
         else:
@@ -135,12 +136,13 @@ class MaterializerVnode:
         one device launch for the whole tuple)."""
         keep = belongs_to_snapshot_ops(
             [(threshold, p.commit_time, p.snapshot_time) for _i, p in t.ops], self.device)
-        kept = [op for op, k in zip(t.ops, keep) if k]
-        if not kept:
-            # reference quirk (:580-583): with no survivor it stores the slot
-            # after the last op, which is an empty slot of the tuple
-            raise LogFallbackRequired(("all ops pruned", t.key))
-        return kept
+        # With no survivor the reference stores element(?FIRST_OP+Len), an empty
+        # slot of the tuple (0), as the only op (:580-583) -- the next
+        # materialize of the key then fails on `{_, Op} = 0`.  The engine
+        # (agn_oplog_prune / agn_prune_ops: AGN_GC_ALL_PRUNED) and this mirror
+        # keep zero ops instead, and count NewLength as 1 for the resize policy
+        # like the reference (intentional deviation, DESIGN.md §8).
+        return [op for op, k in zip(t.ops, keep) if k]
 
     # ------------------------------------------------------------------ writes
     def op_insert_gc(self, key, op):

@@ -148,3 +148,24 @@ def test_system_seq_kat(c):
         assert cm.value(typ, r[1]) == want
         if "expect_state_tokens_per_elem" in c:
             assert all(len(toks) == 1 for _, toks in r[1])
+
+
+def test_vnode_all_pruned_keeps_zero_ops():
+    """prune_ops with every op covered: the reference stores an empty tuple
+    slot as the only op (:580-583), which its next materialize cannot read;
+    the mirror (like the device GC, AGN_GC_ALL_PRUNED) keeps zero ops, sizes
+    the list with NewLength = 1, and the key stays readable from its snapshot."""
+    typ = "antidote_crdt_counter_pn"
+    vn = MaterializerVnode()
+    for i in range(1, 6):
+        vn.update("k", ClocksiPayload("k", typ, i, {"dc1": 10 * i - 5}, ("dc1", 10 * i), i))
+    assert vn.read("k", typ, {"dc1": 100}) == ("ok", 15)
+    snaps = VectorOrddict()
+    for t, v in ((60, 15), (70, 15), (80, 15)):
+        snaps = snaps.insert_bigger({"dc1": t}, MaterializedSnapshot(5, v))
+    vn.snapshot_insert_gc("k", snaps, True)
+    t = vn.ops_cache["k"]
+    assert t.length == 0 and t.list_len == 50 and t.op_counter == 5
+    assert vn.read("k", typ, {"dc1": 100}) == ("ok", 15)
+    vn.update("k", ClocksiPayload("k", typ, 7, {"dc1": 95}, ("dc1", 110), 6))
+    assert vn.read("k", typ, {"dc1": 200}) == ("ok", 22)
