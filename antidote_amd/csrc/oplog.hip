@@ -847,6 +847,23 @@ int agn_oplog_key_meta(agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t 
     return AGN_OK;
 }
 
+int agn_oplog_gc_due(agn_oplog *L, uint64_t n, const uint64_t *keys, uint8_t *out_due) {
+    if (!L) return fail(AGN_EINVAL, "oplog_gc_due: null oplog");
+    if (n && (!keys || !out_due)) return fail(AGN_EINVAL, "oplog_gc_due: null argument");
+    std::lock_guard<std::mutex> g(L->wmu);
+    int rc = settle(L);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (keys[i] >= L->K)
+            return fail(AGN_EINVAL, "oplog_gc_due: key %llu >= n_keys", (unsigned long long)keys[i]);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t k = keys[i];
+        out_due[i] = L->len[k] >= std::max(L->lcap[k], L->init_slots) ||
+                     (L->counter[k] + 1u) % AGN_OPS_THRESHOLD == 0;
+    }
+    return AGN_OK;
+}
+
 }  // extern "C"
 
 namespace agn {

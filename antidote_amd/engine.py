@@ -352,6 +352,14 @@ class OpLog:
         check(self.eng.lib.agn_oplog_stats(self.h, C.byref(e), C.byref(s), C.byref(t)))
         return {"entries": e.value, "slots": s.value, "tokens": t.value}
 
+    def gc_due(self, keys):
+        """op_insert_gc's GC trigger for the next op of each key (before it is appended)."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), np.uint64)
+        out = np.zeros(len(keys), np.uint8)
+        check(self.eng.lib.agn_oplog_gc_due(self.h, len(keys), _ptr(keys), _ptr(out)),
+              "agn_oplog_gc_due")
+        return out.astype(bool)
+
     def key_meta(self, keys=None):
         """Per key: (Length, ListLen, op counter) of the ETS tuple it mirrors."""
         keys = np.arange(self.n_keys, dtype=np.uint64) if keys is None else \

@@ -280,6 +280,14 @@ int agn_oplog_stats(const agn_oplog *log, uint64_t *entries, uint64_t *slots, ui
  * :630) -- the {Length, ListLen} / OpId of deconstruct_opscache_entry (:614). */
 int agn_oplog_key_meta(agn_oplog *log, uint64_t n, const uint64_t *keys, uint32_t *out_len,
                        uint32_t *out_list_len, uint32_t *out_counter);
+/* op_insert_gc's trigger for the NEXT op of each key (:635: Length >= ListLen
+ * or NewId rem OPS_THRESHOLD == 0), before it is appended: the reference runs
+ * the GC read first and inserts after it, so a caller that wants the ETS
+ * list sizes to the slot calls this, runs the GC read (agn_batcher_read with
+ * AGN_READ_GC, or agn_oplog_prune) when due, then agn_oplog_append.
+ * (agn_oplog_append's out_gc_due reports the same condition, but the entry is
+ * then already in the log.) */
+int agn_oplog_gc_due(agn_oplog *log, uint64_t n, const uint64_t *keys, uint8_t *out_due);
 /* Batched materialize/4 over the oplog's current contents (req / out as
  * agn_materialize, device pointers, req->keys indexing the oplog's keys).
  * Staged appends are flushed first (read-your-writes: update/2 is a

@@ -26,6 +26,9 @@
  *   part_materialize(Part, Key, RPairs, SctPairs | ignore, TxId, Base) ->
  *       same result: materialize/4 of the resident ops from a caller base
  *       (the reference's own ETS snapshot cache stays in Erlang)
+ *   part_gc_due(Part, Key) -> boolean()
+ *       op_insert_gc's GC trigger for the key's next op (:635), checked
+ *       before the insert as the reference does
  *   part_gc(Part, Key, ThresholdPairs) -> ok
  *       snapshot_insert_gc's prune_ops + resize for one key (agn_oplog_prune)
  *   part_stats(Part) -> {Entries, Slots, Tokens}
@@ -735,6 +738,17 @@ static ERL_NIF_TERM nif_part_gc(ErlNifEnv *env, int argc, const ERL_NIF_TERM arg
     return rc ? error_tuple(env, rc) : atom(env, "ok");
 }
 
+static ERL_NIF_TERM nif_part_gc_due(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    uint64_t k;
+    uint8_t due = 0;
+    if (argc != 2 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    int rc = key_index(env, p, argv[1], &k);
+    if (!rc) rc = agn_oplog_gc_due(p->log, 1, &k, &due);
+    if (rc) return error_tuple(env, rc);
+    return atom(env, due ? "true" : "false");
+}
+
 static ERL_NIF_TERM nif_part_stats(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
     uint64_t e, s, t;
@@ -764,6 +778,7 @@ static ErlNifFunc funcs[] = {
     {"part_read", 5, nif_part_read, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_materialize", 6, nif_part_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_gc", 3, nif_part_gc, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_gc_due", 2, nif_part_gc_due, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_stats", 1, nif_part_stats, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_key_meta", 2, nif_part_key_meta, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"materialize", 6, nif_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},

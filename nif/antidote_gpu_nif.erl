@@ -15,7 +15,7 @@
 -export([materialize/4, get_min_time/1]).
 %% engine-owned partition (one per materializer_vnode)
 -export([part_open/5, part_update/5, part_read/5, part_materialize/6, part_gc/3,
-         part_stats/1, part_key_meta/2]).
+         part_gc_due/2, part_stats/1, part_key_meta/2]).
 -export([new_partition/3, update/3, read/4, read_from/6, gc/3]).
 
 -on_load(init/0).
@@ -48,6 +48,7 @@ part_update(_Part, _Key, _OcPairs, _TxId, _Effect) -> erlang:nif_error(not_loade
 part_read(_Part, _Key, _RPairs, _TxId, _Gc) -> erlang:nif_error(not_loaded).
 part_materialize(_Part, _Key, _RPairs, _Sct, _TxId, _Base) -> erlang:nif_error(not_loaded).
 part_gc(_Part, _Key, _ThresholdPairs) -> erlang:nif_error(not_loaded).
+part_gc_due(_Part, _Key) -> erlang:nif_error(not_loaded).
 part_stats(_Part) -> erlang:nif_error(not_loaded).
 part_key_meta(_Part, _Key) -> erlang:nif_error(not_loaded).
 
@@ -309,14 +310,24 @@ new_partition(Type, NKeys, Cached) ->
     {ok, Ps} = application:get_env(antidote, gpu_dcs),   % DC slots per clock (<= 256)
     part_open(ctx(), type_id(Type), Ps, NKeys, Cached).
 
-%% update/2 -> op_insert_gc/3: the op's OpSSCommit is its snapshot_time with
-%% the commit DC set to the commit time (src/clocksi_materializer.erl:224).
-%% Returns {ok, OpId, GcDue}; GcDue = true is op_insert_gc's GC trigger
-%% (:635), for which the caller runs the GC read (read/4 with gc, or the
-%% reference's internal_read(..., true) + gc/3).
+%% update/2 -> op_insert_gc/3 (:621-647) on a cached partition, in the
+%% reference's order: when the trigger of :635 holds, the GC read at the op's
+%% snapshot time (:640) runs first, then the op is inserted.  Its OpSSCommit is
+%% the snapshot_time with the commit DC set to the commit time
+%% (src/clocksi_materializer.erl:224).  Returns {ok, OpId, GcRan}.  (With the
+%% reference's ETS snapshot cache, the vnode checks part_gc_due/2 itself, runs
+%% its own internal_read(..., true) -- whose snapshot_insert_gc calls gc/3 --
+%% and then part_update/5.)
 update(Part, Key, #clocksi_payload{snapshot_time = SS, commit_time = {Dc, Ct},
                                    txid = TxId, op_param = Effect}) ->
-    part_update(Part, Key, dict:to_list(dict:store(Dc, Ct, SS)), TxId, Effect).
+    GcRan = case part_gc_due(Part, Key) of
+                true -> _ = part_read(Part, Key, dict:to_list(SS), ignore, true), true;
+                false -> false
+            end,
+    case part_update(Part, Key, dict:to_list(dict:store(Dc, Ct, SS)), TxId, Effect) of
+        {ok, OpId, _} -> {ok, OpId, GcRan};
+        Error -> Error
+    end.
 
 %% read/6 on a cached partition: {ok, Value} | {error, no_snapshot} (the
 %% caller reads the log: get_from_snapshot_log, :416-419) | {error, Reason}.

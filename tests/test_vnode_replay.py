@@ -68,11 +68,12 @@ def has_placeholder(vn, key):
 
 
 def engine_update(ol, bt, key, ss, oc, eff, txid):
-    ids, due = ol.append(np.array([key], np.uint64), oc.reshape(1, D).astype(np.uint64),
-                         eff=np.array([eff], np.int64), txid=np.array([txid], np.uint64))
-    if due[0]:
-        # op_insert_gc's GC read at the op's snapshot time (:640)
+    """op_insert_gc/3 (:621-647) in the reference's order: the GC read at the
+    op's snapshot time (:640) when due, then the insert."""
+    if ol.gc_due(key)[0]:
         bt.read(key, R=ss.astype(np.uint64), gc=True)
+    ids, _ = ol.append(np.array([key], np.uint64), oc.reshape(1, D).astype(np.uint64),
+                       eff=np.array([eff], np.int64), txid=np.array([txid], np.uint64))
     return int(ids[0])
 
 
@@ -98,7 +99,9 @@ def test_vnode_replay_sequential_vs_reference(eng):
                 if has_placeholder(vn, key):
                     quirk.add(key)
             else:
-                R = w.read_clock()
+                # mostly recent reads; some far in the past (older than every
+                # cached snapshot once GC has run: the log fallback)
+                R = w.read_clock(lag=400 if w.rng.random() < 0.85 else 20000)
                 g = bt.read(key, R=R.astype(np.uint64))
                 if key in quirk:
                     continue
