@@ -675,9 +675,17 @@ int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
     out->n_dcs = log->n_dcs;
     out->n_keys = log->n_keys;
     out->key_type = log->key_type;
+    hipStream_t st = (hipStream_t)stream;
+    if (out->key_len) {
+        // segmented output: one pass, each key at its input segment start
+        out->n_entries = log->n_entries;
+        rc = launch_prune_segmented(*log, prune, threshold, threshold_mask, *out, out_flags, st);
+        if (rc == AGN_OK && out_totals) rc = launch_seg_totals(*out, out_totals, st);
+        return rc;
+    }
     out->key_id0 = nullptr;  // pruning leaves id gaps: rebuild with agn_log_index_ids
     return launch_prune_ops(*log, prune, threshold, threshold_mask, *out, out_flags, out_totals,
-                            (hipStream_t)stream);
+                            st);
 }
 
 int agn_gst_scalar(agn_ctx *ctx, uint32_t n_dcs, uint64_t n_epochs, uint64_t *vec,

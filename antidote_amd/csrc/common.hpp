@@ -166,6 +166,10 @@ int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_i
                          uint32_t *key_lcap, const uint8_t *prune, const uint64_t *thr,
                          const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags,
                          hipStream_t st);
+int launch_prune_segmented(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+                           const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
+                           hipStream_t st);
+int launch_seg_totals(const agn_log &out, uint64_t *totals, hipStream_t st);
 int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
                      const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
                      uint64_t *totals, hipStream_t st);

@@ -276,17 +276,29 @@ int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *t
 // AGN_ID0_NONE), the ETS ListLen after the resize policy (:540-558, with
 // prune_ops' NewLength = 1 when nothing survives, :580-583) and
 // meta[4][K] = {len, token len, ListLen, id0} for the host's bookkeeping.
+//
+// The same kernel runs out of place into segmented output (agn_prune_ops
+// with out.key_len): every key keeps its input segment start in the output
+// arrays and only its length changes -- no prefix scan over the keys, one pass,
+// rows still read once and kept rows written once; unselected keys are copied.
 namespace {
 
 struct InplaceArgs {
-    uint64_t *oc, *mask, *txid, *add, *tok;
-    uint32_t *op_id, *tag, *rem_off;
-    int64_t *eff;
+    // source arrays, and the destination arrays (the same pointers in place)
+    const uint64_t *oc, *mask, *txid, *add, *tok;
+    const uint32_t *op_id, *tag, *rem_off;
+    const int64_t *eff;
+    uint64_t *d_oc, *d_mask, *d_txid, *d_add, *d_tok;
+    uint32_t *d_op_id, *d_tag, *d_rem_off;
+    int64_t *d_eff;
     const uint64_t *key_off;
-    uint64_t *key_len;
-    uint32_t *key_id0, *key_lcap;
+    const uint64_t *key_len;   // input lengths, NULL = CSR (key_off[k+1] - key_off[k])
+    uint64_t *d_key_len;       // output lengths
+    uint64_t *d_key_off;       // out of place: the output segment starts (= input), or NULL
+    uint32_t *key_id0, *key_lcap;  // may be NULL (no index / no ListLen)
     uint64_t n_keys;
     uint32_t D, W;
+    int copy_unselected;       // out of place: keys with prune[k] == 0 are copied whole
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -315,15 +327,18 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
     const uint32_t D = a.D, W = a.W;
     constexpr bool tags = TAGS;
     const uint64_t off = uniform_u64(a.key_off[k]);
-    const uint64_t n = uniform_u64(a.key_len[k]);
+    const uint64_t n = uniform_u64(key_n(a.key_off, a.key_len, k));
     const bool gc = prune == nullptr || prune[k] != 0;
     const uint32_t tb = tags ? (uint32_t)uniform_u64(a.rem_off[off]) : 0u;
-    if (!gc) {
+    if (lane == 0 && a.d_key_off) a.d_key_off[k] = off;
+    if (!gc && !a.copy_unselected) {
         if (lane == 0) {
-            meta[k] = (uint32_t)n;
-            meta[K + k] = tags ? a.rem_off[off + n] - tb : 0u;
-            meta[2 * K + k] = a.key_lcap[k];
-            meta[3 * K + k] = a.key_id0[k];
+            if (meta) {
+                meta[k] = (uint32_t)n;
+                meta[K + k] = tags ? a.rem_off[off + n] - tb : 0u;
+                meta[2 * K + k] = a.key_lcap ? a.key_lcap[k] : 0u;
+                meta[3 * K + k] = a.key_id0 ? a.key_id0[k] : AGN_ID0_NONE;
+            }
             if (flags) flags[k] = 0u;
         }
         return;
@@ -365,7 +380,7 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
         int64_t ef = 0;
         if (valid && sub == 0) {
             id = a.op_id[e];
-            tx = a.txid[e];
+            tx = a.txid ? a.txid[e] : 0ull;
             if constexpr (TAGS) {
                 tg = a.tag[e];
                 ad = a.add[e];
@@ -383,7 +398,7 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
             const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
             le = (ballot(!le) & grp) == 0ull;
         }
-        const bool kp = valid && !le;  // belongs_to_snapshot_op(Threshold, op)
+        const bool kp = valid && (!gc || !le);  // belongs_to_snapshot_op(Threshold, op)
         const uint64_t km = ballot(kp && sub == 0);  // one bit per kept op (its sub-0 lane)
         const uint32_t nk = (uint32_t)__builtin_popcountll(km);
         const uint32_t rank = (uint32_t)__builtin_popcountll(km & ((1ull << (slot * LPO)) - 1ull) &
@@ -414,7 +429,7 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
         // stores
         if (kp) {
             if constexpr (FULL) {
-                u64x2 *q = reinterpret_cast<u64x2 *>(a.oc + dst * D + (uint32_t)d0);
+                u64x2 *q = reinterpret_cast<u64x2 *>(a.d_oc + dst * D + (uint32_t)d0);
 #pragma unroll
                 for (int j = 0; j < DPL / 2; ++j) {
                     u64x2 x;
@@ -425,7 +440,7 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
             } else {
 #pragma unroll
                 for (int j = 0; j < DPL; ++j)
-                    if ((uint32_t)(d0 + j) < D) a.oc[dst * D + (uint32_t)(d0 + j)] = o[j];
+                    if ((uint32_t)(d0 + j) < D) a.d_oc[dst * D + (uint32_t)(d0 + j)] = o[j];
             }
         }
         if (SPARSE && a.mask) {
@@ -433,16 +448,16 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
             const uint64_t mw = (kp && (uint32_t)sub < W) ? a.mask[e * W + (uint32_t)sub] : 0ull;
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (kp && (uint32_t)sub < W) a.mask[dst * W + (uint32_t)sub] = mw;
+            if (kp && (uint32_t)sub < W) a.d_mask[dst * W + (uint32_t)sub] = mw;
         }
         if (head) {
-            a.op_id[dst] = id;
-            a.txid[dst] = tx;
+            a.d_op_id[dst] = id;
+            if (a.d_txid) a.d_txid[dst] = tx;
             if constexpr (TAGS) {
-                a.tag[dst] = tg;
-                a.add[dst] = ad;
+                a.d_tag[dst] = tg;
+                a.d_add[dst] = ad;
             } else {
-                a.eff[dst] = ef;
+                a.d_eff[dst] = ef;
             }
         }
         if (tags) {
@@ -450,7 +465,7 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
                 if (head) {
 #pragma unroll
                     for (int x = 0; x < PT; ++x)
-                        if ((uint32_t)x < rl_) a.tok[tdst + x] = tk[x];
+                        if ((uint32_t)x < rl_) a.d_tok[tdst + x] = tk[x];
                 }
             } else {
                 // position order, one kept entry at a time, 64 tokens per step
@@ -466,15 +481,15 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
                         const uint64_t v = in ? a.tok[s0 + c + (uint32_t)lane] : 0ull;
                         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                         __builtin_amdgcn_wave_barrier();
-                        if (in) a.tok[sd + c + (uint32_t)lane] = v;
+                        if (in) a.d_tok[sd + c + (uint32_t)lane] = v;
                         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
                         __builtin_amdgcn_wave_barrier();
                     }
                 }
             }
             if (head) {
-                a.rem_off[dst] = tdst;
-                a.rem_off[dst + 1] = tdst + rl_;
+                a.d_rem_off[dst] = tdst;
+                a.d_rem_off[dst + 1] = tdst + rl_;
             }
             rwritten += (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
         }
@@ -498,20 +513,22 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
     if (lane == 0) {
         const uint32_t l = (uint32_t)written;
         const uint32_t id0 = (l && consec && first_id != AGN_ID0_NONE) ? first_id : AGN_ID0_NONE;
-        uint32_t lc = a.key_lcap[k];
-        if (lc) {
+        uint32_t lc = a.key_lcap ? a.key_lcap[k] : 0u;
+        if (lc && gc) {
             lc = resize_list_len_dev(l ? l : 1u, lc);  // prune_ops' NewLength (1 if none kept)
             if (lc < l) lc = l;
         }
-        a.key_len[k] = written;
-        a.key_id0[k] = id0;
-        a.key_lcap[k] = lc;
-        if (tags && l == 0) a.rem_off[off] = tb;  // an empty segment keeps its token base
-        meta[k] = l;
-        meta[K + k] = rwritten;
-        meta[2 * K + k] = lc;
-        meta[3 * K + k] = id0;
-        if (flags) flags[k] = l == 0 ? AGN_GC_ALL_PRUNED : 0u;
+        a.d_key_len[k] = written;
+        if (a.key_id0) a.key_id0[k] = id0;
+        if (a.key_lcap) a.key_lcap[k] = lc;
+        if (tags && l == 0) a.d_rem_off[off] = tb;  // an empty segment keeps its token base
+        if (meta) {
+            meta[k] = l;
+            meta[K + k] = rwritten;
+            meta[2 * K + k] = lc;
+            meta[3 * K + k] = id0;
+        }
+        if (flags) flags[k] = (gc && l == 0) ? AGN_GC_ALL_PRUNED : 0u;
     }
 }
 
@@ -543,6 +560,39 @@ int inplace(const InplaceArgs &a, const uint8_t *prune, const uint64_t *thr,
 #undef AGN_L
 }
 
+InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
+    InplaceArgs a;
+    a.oc = in.oc;
+    a.mask = in.oc_mask;
+    a.txid = in.txid;
+    a.add = in.add_tok;
+    a.tok = in.rem_tok;
+    a.op_id = in.op_id;
+    a.tag = in.tag;
+    a.rem_off = in.rem_off;
+    a.eff = in.eff;
+    a.d_oc = (uint64_t *)out.oc;
+    a.d_mask = (uint64_t *)out.oc_mask;
+    a.d_txid = (uint64_t *)out.txid;
+    a.d_add = (uint64_t *)out.add_tok;
+    a.d_tok = (uint64_t *)out.rem_tok;
+    a.d_op_id = (uint32_t *)out.op_id;
+    a.d_tag = (uint32_t *)out.tag;
+    a.d_rem_off = (uint32_t *)out.rem_off;
+    a.d_eff = (int64_t *)out.eff;
+    a.key_off = in.key_off;
+    a.key_len = in.key_len;
+    a.d_key_len = (uint64_t *)out.key_len;
+    a.d_key_off = nullptr;
+    a.key_id0 = (uint32_t *)out.key_id0;
+    a.key_lcap = nullptr;
+    a.n_keys = in.n_keys;
+    a.D = in.n_dcs;
+    a.W = n_words(in.n_dcs);
+    a.copy_unselected = 0;
+    return a;
+}
+
 }  // namespace
 
 int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
@@ -550,26 +600,69 @@ int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_i
                          const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags,
                          hipStream_t st) {
     if (view.n_keys == 0) return AGN_OK;
-    InplaceArgs a;
-    a.oc = (uint64_t *)view.oc;
-    a.mask = (uint64_t *)view.oc_mask;
-    a.txid = (uint64_t *)view.txid;
-    a.add = (uint64_t *)view.add_tok;
-    a.tok = (uint64_t *)view.rem_tok;
-    a.op_id = (uint32_t *)view.op_id;
-    a.tag = (uint32_t *)view.tag;
-    a.rem_off = (uint32_t *)view.rem_off;
-    a.eff = (int64_t *)view.eff;
-    a.key_off = view.key_off;
+    agn_log out = view;  // in place: the destination arrays are the source arrays
+    out.key_len = key_len;
+    out.key_id0 = key_id0;
+    InplaceArgs a = seg_args(view, out);
     a.key_len = key_len;
-    a.key_id0 = key_id0;
     a.key_lcap = key_lcap;
-    a.n_keys = view.n_keys;
-    a.D = view.n_dcs;
-    a.W = n_words(view.n_dcs);
     const bool sparse = view.oc_mask || thr_mask;
     return sparse ? inplace<true>(a, prune, thr, thr_mask, meta, flags, st)
                   : inplace<false>(a, prune, thr, thr_mask, meta, flags, st);
+}
+
+// {kept entries, kept removal tokens} of a segmented output: block sums, one
+// atomic per block
+__global__ __launch_bounds__(256) void k_seg_totals(const uint64_t *__restrict__ key_off,
+                                                    const uint64_t *__restrict__ key_len,
+                                                    const uint32_t *__restrict__ rem_off,
+                                                    uint64_t n, unsigned long long *totals) {
+    __shared__ unsigned long long se[4], st[4];
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t e = 0, t = 0;
+    if (k < n) {
+        e = key_len[k];
+        if (rem_off && e) t = rem_off[key_off[k] + e] - rem_off[key_off[k]];
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        e += shfl_xor_u64(e, m);
+        t += shfl_xor_u64(t, m);
+    }
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        se[w] = e;
+        st[w] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(&totals[0], se[0] + se[1] + se[2] + se[3]);
+        atomicAdd(&totals[1], st[0] + st[1] + st[2] + st[3]);
+    }
+}
+
+int launch_seg_totals(const agn_log &out, uint64_t *totals, hipStream_t st) {
+    AGN_HIP(hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), st));
+    if (out.n_keys == 0) return AGN_OK;
+    hipLaunchKernelGGL(k_seg_totals, dim3((unsigned)((out.n_keys + 255) / 256)), dim3(256), 0, st,
+                       out.key_off, out.key_len, out.rem_off, out.n_keys,
+                       (unsigned long long *)totals);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+// agn_prune_ops into segmented output (out.key_len != NULL): one pass, every
+// key at its input segment start; out.key_off receives the starts.
+int launch_prune_segmented(const agn_log &log, const uint8_t *prune, const uint64_t *thr,
+                           const uint64_t *thr_mask, const agn_log &out, uint32_t *flags,
+                           hipStream_t st) {
+    if (log.n_keys == 0) return AGN_OK;
+    InplaceArgs a = seg_args(log, out);
+    a.d_key_off = (uint64_t *)out.key_off;
+    a.copy_unselected = 1;
+    const bool sparse = log.oc_mask || thr_mask;
+    return sparse ? inplace<true>(a, prune, thr, thr_mask, nullptr, flags, st)
+                  : inplace<false>(a, prune, thr, thr_mask, nullptr, flags, st);
 }
 
 // Two-phase prune_ops into a fresh segmented arena (agn_oplog_prune): the

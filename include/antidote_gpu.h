@@ -528,8 +528,14 @@ int agn_log_ingest(agn_ctx *ctx, const agn_log_records *recs, uint32_t crdt_type
  * out_flags[n_keys] (device, may be NULL): AGN_GC_ALL_PRUNED when no op of
  * a collected key survives (every op covered, or none to begin with) — the
  * reference then stores element(?FIRST_OP+Len) of the ETS tuple, an empty
- * slot, as a length-1 op list (:580-583); here the key keeps zero entries.  out_totals (device, may be NULL) receives
- * {kept entries, kept removal tokens}.  Asynchronous on `stream`. */
+ * slot, as a length-1 op list (:580-583); here the key keeps zero entries.
+ * out_totals (device, may be NULL) receives {kept entries, kept removal
+ * tokens}.  Asynchronous on `stream`.
+ * Segmented output (out->key_len != NULL): one pass instead of mark / scan /
+ * scatter -- every key keeps its input segment start in the output arrays
+ * (out->key_off[n_keys] receives the starts, out->key_len the kept lengths,
+ * removal tokens keep their input positions' ranges), unselected keys are
+ * copied, and out->key_id0 (if given) receives the consecutive-id index. */
 #define AGN_GC_ALL_PRUNED 0x1u
 int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
                   const uint64_t *threshold, const uint64_t *threshold_mask, agn_log *out,

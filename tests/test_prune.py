@@ -149,3 +149,54 @@ def test_prune_gpu_vs_oracle(eng, oracle_lib, crdt, D, sparse):
             assert np.array_equal(got[:nr], w[:nr]), name
             continue
         assert np.array_equal(got[:n_out], w[:n_out]), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("crdt,D,sparse", CASES + [(_abi.COUNTER_PN, 256, True),
+                                                   (_abi.SET_AW, 100, False)])
+def test_prune_segmented_gpu_vs_oracle(eng, oracle_lib, crdt, D, sparse):
+    """agn_prune_ops with out.key_len: the one-pass segmented form -- every
+    key's kept entries at its input segment start, bit-exact with the
+    oracle's CSR output key by key, unselected keys copied, plus the
+    consecutive-id index."""
+    from test_id_index import expected_index
+    log, _req, _ = random_case(91 * D + crdt + sparse, crdt, 200, D, 150 if D <= 16 else 60,
+                               sparse=sparse, multi=0.2 if crdt == _abi.SET_AW else 0.0,
+                               empty=0.1, txid=0.3)
+    prune, thr, tm = thresholds(D * 5 + crdt, log, sparse)
+    want, wflags, n_out = oracle_prune(oracle_lib, log, prune, thr, tm)
+    K = log.n_keys
+    dlog = eng.upload_log(log)
+    if log.oc_mask is None:
+        dlog.struct.oc_mask = None
+    dout = eng.alloc_log_like(log)
+    kl, kid = eng.empty(8 * K), eng.empty(4 * K)
+    dout.struct.key_len, dout.struct.key_id0 = kl.ptr, kid.ptr
+    bp, bt = eng.upload(prune), eng.upload(thr)
+    btm = eng.upload(tm) if tm is not None else None
+    fl, tot = eng.empty(4 * K), eng.empty(16)
+    eng.prune_ops(dlog, bp.ptr, bt.ptr, btm.ptr if btm else None, dout, fl.ptr, tot.ptr)
+    eng.sync()
+    totals = eng.download(tot, np.uint64, (2,))
+    assert int(totals[0]) == n_out
+    assert int(totals[1]) == int(want["rem_off"][n_out]) if log.rem_off is not None else True
+    assert np.array_equal(eng.download(fl, np.uint32, (K,)), wflags)
+    starts = eng.download(dout.bufs["key_off"], np.uint64, (K + 1,))[:K]
+    lens = eng.download(kl, np.uint64, (K,))
+    assert np.array_equal(starts, log.key_off[:K])
+    assert np.array_equal(lens, np.diff(want["key_off"]))
+    got = {n: eng.download(dout.bufs[n], *dout.shapes[n]) for n in dout.shapes}
+    for k in range(K):
+        a, b = int(starts[k]), int(starts[k]) + int(lens[k])
+        wa, wb = int(want["key_off"][k]), int(want["key_off"][k + 1])
+        for name in ("oc", "oc_mask", "op_id", "txid", "eff", "tag", "add_tok"):
+            if name in got:
+                assert np.array_equal(got[name][a:b], want[name][wa:wb]), (k, name)
+        if log.rem_off is not None:
+            ro, wro = got["rem_off"], want["rem_off"]
+            for e, we in zip(range(a, b), range(wa, wb)):
+                g = got["rem_tok"][int(ro[e]):int(ro[e + 1])]
+                w = want["rem_tok"][int(wro[we]):int(wro[we + 1])]
+                assert np.array_equal(g, w), (k, e)
+    ids = got["op_id"]
+    assert np.array_equal(eng.download(kid, np.uint32, (K,)), expected_index(starts, lens, ids))

@@ -139,9 +139,13 @@ def test_vnode_replay_threads_values(eng):
             Batcher(ol, max_batch=16, max_wait_us=100, cached=True) as bt:
         stop = threading.Event()
 
+        readers_done = threading.Event()
+
         def writer():
             try:
-                for s in range(3000):
+                for s in range(20_000):
+                    if readers_done.is_set() and s >= 3000:
+                        break
                     key = s % K if s < K else int(w.rng.integers(0, K))
                     # the clocks a reader may pick advance only with the append
                     with lock:
@@ -156,7 +160,9 @@ def test_vnode_replay_threads_values(eng):
         def reader(t):
             rng = np.random.default_rng(100 + t)
             try:
-                while not stop.is_set():
+                for _ in range(60):
+                    if errs:
+                        break
                     key = int(rng.integers(0, K))
                     with lock:
                         # ops at or below the published clocks are all appended
@@ -172,12 +178,15 @@ def test_vnode_replay_threads_values(eng):
                     stats["served"] += 1
             except Exception as e:  # noqa: BLE001
                 errs.append(e)
-        ts = [threading.Thread(target=writer)] + \
-            [threading.Thread(target=reader, args=(t,)) for t in range(8)]
-        for x in ts:
+        rs = [threading.Thread(target=reader, args=(t,)) for t in range(8)]
+        wt = threading.Thread(target=writer)
+        wt.start()
+        for x in rs:
             x.start()
-        for x in ts:
+        for x in rs:
             x.join()
+        readers_done.set()
+        wt.join()
         assert not errs, errs[0]
         # after the storm: every key read at the current clocks, served
         for key in range(K):
@@ -185,5 +194,5 @@ def test_vnode_replay_threads_values(eng):
             assert g["status"] in (_abi.SS_HIT, _abi.SS_NEW)
             assert g["value"] == sum(e for _, e in w.ops[key])
         st = ol.stats()
-    assert stats["served"] > 200, stats
+    assert stats["served"] > 100, stats
     assert st["entries"] < sum(len(x) for x in w.ops)   # the GC ran
