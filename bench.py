@@ -88,16 +88,22 @@ def fmt_keys(n):
     return str(n)
 
 
-def kernel_src_sha16():
-    """Hash of every source the device code is built from; a PMC traffic file
-    (profiles/pmc/*.json, scripts/pmc_traffic.py) is only used when it was
-    measured on a build of exactly these sources."""
-    import glob
+KERNEL_SOURCES = {   # the sources the dominant kernel of each config is built from
+    1: ("mat_counter_dense.hip", "filter.hpp", "common.hpp"),
+    2: ("mat_counter_dense.hip", "filter.hpp", "common.hpp"),
+    3: ("mat_tags.hip", "filter.hpp", "common.hpp"),
+    4: ("mat_tags.hip", "filter.hpp", "common.hpp"),
+}
+
+
+def kernel_src_sha16(config):
+    """Hash of the sources the config's dominant kernel is built from; a PMC
+    traffic file (profiles/pmc/cfgN.json, scripts/pmc_traffic.py) is only used
+    when it was measured on a build of exactly these sources."""
     import hashlib
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "antidote_amd", "csrc", "*.hip")) +
-                   glob.glob(os.path.join(ROOT, "antidote_amd", "csrc", "*.hpp")) +
-                   [os.path.join(ROOT, "include", "antidote_gpu.h")])
+    files = [os.path.join(ROOT, "antidote_amd", "csrc", f) for f in KERNEL_SOURCES[config]] + \
+        [os.path.join(ROOT, "include", "antidote_gpu.h")]
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
@@ -309,7 +315,7 @@ def main():
                    "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
         traffic, traffic_src = None, None
-        sha = kernel_src_sha16()
+        sha = kernel_src_sha16(a.config)
         pmc = os.path.join(ROOT, "profiles", "pmc", f"cfg{a.config}.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
