@@ -299,6 +299,8 @@ struct InplaceArgs {
     uint64_t n_keys;
     uint32_t D, W;
     int copy_unselected;       // out of place: keys with prune[k] == 0 are copied whole
+    int xcd;                   // XCD-aware block order
+    int late_fields;           // entry fields loaded after the filter (kept entries only)
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -310,15 +312,18 @@ __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32
 
 constexpr int PT = 4;  // removal tokens a lane buffers per entry
 
-template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS>
-__global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
                                                        const uint8_t *__restrict__ prune,
                                                        const uint64_t *__restrict__ thr,
                                                        const uint64_t *__restrict__ thr_mask,
                                                        uint32_t *__restrict__ meta,
                                                        uint32_t *__restrict__ flags) {
     using S = Shape<DPL, LPO>;
-    const uint64_t k = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    // XCD-aware key order: consecutive keys (whose per-key outputs share lines)
+    // run on one XCD's L2
+    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t k = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
     if (k >= a.n_keys) return;
     const uint64_t K = a.n_keys;
     const int lane = lane_id();
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
         uint32_t id = 0, tg = 0, r0 = 0, rl_ = 0;
         uint64_t tx = 0, ad = 0;
         int64_t ef = 0;
-        if (valid && sub == 0) {
+        auto load_fields = [&]() {
             id = a.op_id[e];
             tx = a.txid ? a.txid[e] : 0ull;
             if constexpr (TAGS) {
@@ -389,7 +394,9 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
             } else {
                 ef = a.eff[e];
             }
-        }
+        };
+        const bool late = a.late_fields < 0 ? TAGS : a.late_fields != 0;
+        if (!late && valid && sub == 0) load_fields();
         bool le = true;
 #pragma unroll
         for (int j = 0; j < DPL; ++j)
@@ -399,6 +406,10 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
             le = (ballot(!le) & grp) == 0ull;
         }
         const bool kp = valid && (!gc || !le);  // belongs_to_snapshot_op(Threshold, op)
+        // set_aw / register_mv: 32 B of fields per entry, loaded for the kept
+        // entries only once the filter has decided; counter_pn: 20 B, loaded
+        // with the row (one round trip less; measured, scripts/ab_prune.py)
+        if (late && kp && sub == 0) load_fields();
         const uint64_t km = ballot(kp && sub == 0);  // one bit per kept op (its sub-0 lane)
         const uint32_t nk = (uint32_t)__builtin_popcountll(km);
         const uint32_t rank = (uint32_t)__builtin_popcountll(km & ((1ull << (slot * LPO)) - 1ull) &
@@ -535,12 +546,24 @@ __global__ __launch_bounds__(256) void k_prune_inplace(InplaceArgs a,
 template <int DPL, int LPO, bool SPARSE>
 int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *thr,
                   const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags, hipStream_t st) {
-    const unsigned blocks = grid_for(a.n_keys, 4, 0x7fffffffu);
+    // waves per block: 1 (default; the grid is the key list, as the counter
+    // kernel) or 4 (AGN_PRUNE_WPB=4, A/B knob)
+    const char *ev = getenv("AGN_PRUNE_WPB");
+    const bool w4 = ev && ev[0] == '4';
+    const unsigned blocks = grid_for(a.n_keys, w4 ? 4 : 1, 0x7fffffffu);
     const bool full = !a.mask && (DPL % 2 == 0) && a.D == (uint32_t)(DPL * LPO);
     const bool tags = a.rem_off != nullptr;
-#define AGN_K(FULLV, TAGSV)                                                                \
-    hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV>), dim3(blocks),     \
-                       dim3(256), 0, st, a, prune, thr, thr_mask, meta, flags)
+#define AGN_K(FULLV, TAGSV)                                                                    \
+    do {                                                                                       \
+        if (w4)                                                                                \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 4>),           \
+                               dim3(blocks), dim3(256), 0, st, a, prune, thr, thr_mask, meta,  \
+                               flags);                                                         \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1>),           \
+                               dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
+                               flags);                                                         \
+    } while (0)
     if (full) {
         if (tags) AGN_K((DPL % 2 == 0), true);
         else AGN_K((DPL % 2 == 0), false);
@@ -590,6 +613,9 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.D = in.n_dcs;
     a.W = n_words(in.n_dcs);
     a.copy_unselected = 0;
+    a.xcd = xcd_remap() ? 1 : 0;
+    const char *lf = getenv("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
+    a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
     return a;
 }
 
@@ -611,18 +637,20 @@ int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_i
                   : inplace<false>(a, prune, thr, thr_mask, meta, flags, st);
 }
 
-// {kept entries, kept removal tokens} of a segmented output: block sums, one
-// atomic per block
-__global__ __launch_bounds__(256) void k_seg_totals(const uint64_t *__restrict__ key_off,
-                                                    const uint64_t *__restrict__ key_len,
-                                                    const uint32_t *__restrict__ rem_off,
-                                                    uint64_t n, unsigned long long *totals) {
-    __shared__ unsigned long long se[4], st[4];
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// {kept entries, kept removal tokens} of a segmented output: per-block sums
+// into scratch, then one block folds them (no same-address atomics)
+constexpr unsigned TOT_BLOCK = 1024;
+__global__ __launch_bounds__(TOT_BLOCK) void k_seg_totals(const uint64_t *__restrict__ key_off,
+                                                          const uint64_t *__restrict__ key_len,
+                                                          const uint32_t *__restrict__ rem_off,
+                                                          uint64_t n, uint64_t *__restrict__ part) {
+    __shared__ uint64_t se[TOT_BLOCK / 64], st[TOT_BLOCK / 64];
     uint64_t e = 0, t = 0;
-    if (k < n) {
-        e = key_len[k];
-        if (rem_off && e) t = rem_off[key_off[k] + e] - rem_off[key_off[k]];
+    for (uint64_t k = (uint64_t)blockIdx.x * TOT_BLOCK + threadIdx.x; k < n;
+         k += (uint64_t)gridDim.x * TOT_BLOCK) {
+        const uint64_t l = key_len[k];
+        e += l;
+        if (rem_off && l) t += rem_off[key_off[k] + l] - rem_off[key_off[k]];
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
@@ -636,18 +664,48 @@ __global__ __launch_bounds__(256) void k_seg_totals(const uint64_t *__restrict__
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        atomicAdd(&totals[0], se[0] + se[1] + se[2] + se[3]);
-        atomicAdd(&totals[1], st[0] + st[1] + st[2] + st[3]);
+        uint64_t a = 0, b = 0;
+        for (unsigned x = 0; x < TOT_BLOCK / 64; ++x) {
+            a += se[x];
+            b += st[x];
+        }
+        part[2 * blockIdx.x] = a;
+        part[2 * blockIdx.x + 1] = b;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_seg_totals_fold(const uint64_t *__restrict__ part,
+                                                         unsigned nb, uint64_t *__restrict__ out) {
+    uint64_t a = 0, b = 0;
+    for (unsigned x = threadIdx.x; x < nb; x += 64) {
+        a += part[2 * x];
+        b += part[2 * x + 1];
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        a += shfl_xor_u64(a, m);
+        b += shfl_xor_u64(b, m);
+    }
+    if (threadIdx.x == 0) {
+        out[0] = a;
+        out[1] = b;
     }
 }
 
 int launch_seg_totals(const agn_log &out, uint64_t *totals, hipStream_t st) {
-    AGN_HIP(hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), st));
-    if (out.n_keys == 0) return AGN_OK;
-    hipLaunchKernelGGL(k_seg_totals, dim3((unsigned)((out.n_keys + 255) / 256)), dim3(256), 0, st,
-                       out.key_off, out.key_len, out.rem_off, out.n_keys,
-                       (unsigned long long *)totals);
-    AGN_HIP(hipGetLastError());
+    if (out.n_keys == 0) {
+        AGN_HIP(hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), st));
+        return AGN_OK;
+    }
+    const unsigned nb = grid_for(out.n_keys, TOT_BLOCK, 2048);
+    uint64_t *part = nullptr;
+    AGN_HIP(pool_malloc(&part, (size_t)nb * 2 * sizeof(uint64_t), st));
+    hipLaunchKernelGGL(k_seg_totals, dim3(nb), dim3(TOT_BLOCK), 0, st, out.key_off, out.key_len,
+                       out.rem_off, out.n_keys, part);
+    hipLaunchKernelGGL(k_seg_totals_fold, dim3(1), dim3(64), 0, st, part, nb, totals);
+    const hipError_t e = hipGetLastError();
+    (void)hipFreeAsync(part, st);
+    AGN_HIP(e);
     return AGN_OK;
 }
 

@@ -1,0 +1,69 @@
+"""A/B of the one-pass prune kernel (agn_prune_ops segmented form, the kernel
+agn_oplog_prune runs in place) on the cfg2 log, variants alternated in one
+process (process-to-process HBM variance is several %):
+  AGN_PRUNE_WPB = 1 | 4 (waves per block) x AGN_PRUNE_LATE_FIELDS = 0 | 1
+  (entry fields with the rows, or only for kept entries after the filter).
+  Earlier runs also compared AGN_XCD_REMAP and non-temporal row loads /
+  stores (no effect, removed): profiles/r02/ab_prune_*.log.
+
+  python scripts/ab_prune.py [config] [rounds]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    import torch
+    from antidote_amd import _abi
+    from antidote_amd.engine import DeviceArrays, Engine
+    from bench import CONFIGS
+    config = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    cfg = CONFIGS[config]
+    D, N, K = cfg["n_dcs"], cfg["ops_per_key"], cfg["n_keys"]
+    E = K * N
+    torch.cuda.init()
+    eng = Engine(0)
+    g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=D, n_keys=K, ops_per_key=N,
+                       n_elems=cfg["n_elems"], seed=cfg["seed"], key_base=0, key_stride=1, warm=0)
+    dl, dr = eng.gen_dev(g)
+    s = _abi.AgnLog()
+    s.crdt_type, s.n_dcs, s.n_keys, s.n_entries = cfg["crdt_type"], D, K, E
+    out = DeviceArrays(s)
+    spec = {"key_off": 8 * (K + 1), "oc": 8 * E * D, "op_id": 4 * E, "txid": 8 * E,
+            "key_len": 8 * K}
+    if cfg["crdt_type"] == 1:
+        spec["eff"] = 8 * E
+    else:
+        n_rem = int(eng.download(type("B", (), {"ptr": dl.rem_off})(), np.uint32, (E + 1,))[-1])
+        spec.update({"tag": 4 * E, "add_tok": 8 * E, "rem_off": 4 * (E + 1),
+                     "rem_tok": 8 * max(n_rem, 1)})
+    for name, nb in spec.items():
+        out.bufs[name] = eng.empty(nb)
+        setattr(s, name, out.bufs[name].ptr)
+    din = DeviceArrays(dl)
+    variants = [("wpb1_early", "1", "0"), ("wpb1_late", "1", "1"), ("wpb4_early", "4", "0"),
+                ("wpb4_late", "4", "1")]
+    best = {v[0]: [] for v in variants}
+    for r in range(rounds):
+        for name, wpb, late in (variants if r % 2 == 0 else variants[::-1]):
+            os.environ["AGN_PRUNE_WPB"], os.environ["AGN_PRUNE_LATE_FIELDS"] = wpb, late
+            eng.prune_ops(din, None, dr.R, None, out)
+            torch.cuda.synchronize()
+            b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            b.record()
+            eng.prune_ops(din, None, dr.R, None, out)
+            e.record()
+            torch.cuda.synchronize()
+            best[name].append(b.elapsed_time(e))
+    print(json.dumps({"config": config, "ms_median": {k: float(np.median(v)) for k, v in best.items()},
+                      "ms_all": best}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
