@@ -44,6 +44,10 @@ CONFIGS = {
     3: dict(name="cfg3 set_aw materialize: {keys} keys x 256 add/remove ops, 16-DC clocks, "
                  "32 elems/key, order-aware tag resolution", crdt_type=2, n_dcs=16,
             n_keys=1_000_000, ops_per_key=256, n_elems=32, seed=20250112 + 2),
+    5: dict(name="cfg5 GST: 4096 partitions x 256-DC clocks (4096/G per GPU), 256 epochs per step, "
+                 "stable_time_functions:get_min_time elementwise min + RCCL ncclMin allreduce "
+                 "over xGMI (N > 1)", crdt_type=0, n_dcs=256, n_keys=4096, ops_per_key=0,
+            n_elems=0, seed=20250112 + 4, strong=True),
     4: dict(name="cfg4 register_mv materialize: {keys} keys x 100 ops on this GPU (100M ops total over G GPUs), "
                  "64-DC clocks, concurrent-write pruning", crdt_type=3, n_dcs=64,
             n_keys=1_000_000, ops_per_key=100, n_elems=16, seed=20250112 + 3, strong=True),
@@ -93,6 +97,7 @@ KERNEL_SOURCES = {   # the sources the dominant kernel of each config is built f
     2: ("mat_counter_dense.hip", "filter.hpp", "common.hpp"),
     3: ("mat_tags.hip", "filter.hpp", "common.hpp"),
     4: ("mat_tags.hip", "filter.hpp", "common.hpp"),
+    5: ("gst.hip", "common.hpp"),
 }
 
 
@@ -187,6 +192,26 @@ def cpu_baseline(cfg, n_keys, threads, target_s=10.0):
     return {nt: work[nt] / secs[nt] for nt in tcounts}, {nt: secs[nt] for nt in tcounts}, reps
 
 
+def pmc_traffic(config, n_units):
+    """HBM bytes per launch of the config's dominant kernel from
+    profiles/pmc/cfgN.json (scripts/pmc_traffic.py), only when it was measured
+    on this build of the kernel's sources and the same units per launch."""
+    sha = kernel_src_sha16(config)
+    pmc = os.path.join(ROOT, "profiles", "pmc", f"cfg{config}.json")
+    if not os.path.exists(pmc):
+        return None, f"null: no PMC pass for cfg{config} (profiles/pmc/)"
+    with open(pmc) as f:
+        p = json.load(f)
+    if p.get("n_keys") == n_units and p.get("kernel_src_sha16") == sha:
+        return p.get("hbm_bytes_per_launch"), (
+            f"profiles/pmc/cfg{config}.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of "
+            f"{p.get('kernel')} on this kernel build (sources sha {sha}), "
+            f"measured {p.get('measured', '?')}")
+    return None, (f"null: profiles/pmc/cfg{config}.json was measured on sources "
+                  f"{p.get('kernel_src_sha16')} / {p.get('n_keys')} units, this build is "
+                  f"{sha} / {n_units} units")
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -211,6 +236,8 @@ def main():
     from antidote_amd import _abi
     from antidote_amd.engine import Engine
 
+    if a.config == 5:
+        return gst_main(a, torch, dist, world, rank, local, backend)
     cfg = dict(CONFIGS[a.config])
     n_keys = a.keys or cfg["n_keys"]
     if cfg.get("strong") and not a.keys:
@@ -314,23 +341,7 @@ def main():
                              f"{secs[1]:.1f} s of CPU time",
                    "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
-        traffic, traffic_src = None, None
-        sha = kernel_src_sha16(a.config)
-        pmc = os.path.join(ROOT, "profiles", "pmc", f"cfg{a.config}.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                p = json.load(f)
-            if p.get("n_keys") == n_keys and p.get("kernel_src_sha16") == sha:
-                traffic = p.get("hbm_bytes_per_launch")
-                traffic_src = (f"profiles/pmc/cfg{a.config}.json: rocprofv3 FETCH_SIZE x2 + "
-                               f"WRITE_SIZE passes of {p.get('kernel')} on this kernel build "
-                               f"(sources sha {sha}), measured {p.get('measured', '?')}")
-            else:
-                traffic_src = (f"null: profiles/pmc/cfg{a.config}.json was measured on "
-                               f"sources {p.get('kernel_src_sha16')} / {p.get('n_keys')} keys, "
-                               f"this build is {sha} / {n_keys} keys")
-        else:
-            traffic_src = f"null: no PMC pass for cfg{a.config} (profiles/pmc/)"
+        traffic, traffic_src = pmc_traffic(a.config, n_keys)
         workload = cfg["name"].format(keys=fmt_keys(n_keys))
         line = {
             "metric": "materialized ops/sec + VC compares/sec (1/2/4/8 GPU), % of HBM roofline",
@@ -352,7 +363,7 @@ def main():
                          "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch,
                          "algorithmic_bytes_survey": bytes_survey,
                          "frac_survey_bytes": bytes_survey / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "kernel_src_sha16": sha,
+                         "kernel_src_sha16": kernel_src_sha16(a.config),
                          "probe_read_GBps": probe,
                          "frac_of_probe": achieved / probe if probe else None},
             "cpu_baseline": cpu,
@@ -657,11 +668,23 @@ def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
             moved = E * (8 * D + 1) + E + 2 * kept * (8 * D + per_f) + 16 * kept_rem + \
                 8 * 4 * n_keys
         else:
-            moved = alg + (E - kept) * per_f     # fields of dropped entries, loaded with rows
+            # counter_pn loads the fields with the rows (dropped entries' too);
+            # set_aw / register_mv only for kept entries (gc.hip late fields)
+            moved = alg + (0 if tags else (E - kept) * per_f)
         res[mode] = {"ms": ms, "kept": kept, "algorithmic_bytes": alg,
                      "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "bytes_moved_by_design": moved,
                      "frac_of_design_bytes": moved / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    # the box's read+write ceiling at the segmented kernel's write:read mix
+    # (tools/bwprobe.hip k_copy over the same arrays, wq of 4 chunks stored)
+    seg = res["segmented"]
+    rd = E * 8 * D + (E if not tags else kept) * per_f
+    wq = max(1, min(4, round(4 * (seg["bytes_moved_by_design"] - rd) / max(rd, 1))))
+    cp = probe_copy_gbs(eng, dl.oc, out.bufs["oc"].ptr, E * 8 * D, wq, sp, torch)
+    if cp:
+        seg["copy_probe_GBps"] = cp
+        seg["copy_probe_write_frac"] = wq / 4
+        seg["frac_of_copy_probe"] = seg["bytes_moved_by_design"] / (seg["ms"] * 1e-3) / 1e9 / cp
     for bb in list(out.bufs.values()) + [tot, key_len]:
         bb.free()
     return {"entries": E, **res,
@@ -741,6 +764,29 @@ def post_gc_bench(eng, cfg, n_keys, rank, world, sp, torch, steps):
             for k in logs} | {"keys_id0_none_frac": none_frac,
                               "note": "warm reads (SCT + base); post_gc = the same log "
                                       "pruned at SCT, op ids with gaps"}
+
+
+def probe_copy_gbs(eng, src, dst, nbytes, wq, sp, torch):
+    """The box's practical read+write rate: tools/libagn_probe.so k_copy reads
+    nbytes and writes wq/4 of them (one-shot 4 KiB waves, 16-B accesses);
+    GB/s of bytes read + written."""
+    path = os.path.join(ROOT, "tools", "libagn_probe.so")
+    if not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    lib.agn_probe_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p]
+    for _ in range(2):
+        if lib.agn_probe_copy(src, dst, nbytes, wq, sp) != 0:
+            return None
+    torch.cuda.synchronize()
+    b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b.record()
+    for _ in range(5):
+        lib.agn_probe_copy(src, dst, nbytes, wq, sp)
+    e.record()
+    torch.cuda.synchronize()
+    moved = (nbytes // 8192 * 8192) * (1 + wq / 4)
+    return moved / (b.elapsed_time(e) / 5 * 1e-3) / 1e9
 
 
 def probe_read_gbs(eng, dl, nbytes, sp, torch):
@@ -859,6 +905,161 @@ def gst_bench(eng, torch, dist, world, rank, sp, backend="nccl"):
             "rccl_ranks": world if rccl else None,
             "exchange_verified": verified,
             "epoch": "agn_gst_min -> exchange (min, D+1 words) -> agn_gst_finalize"}
+
+
+def gst_main(a, torch, dist, world, rank, local, backend):
+    """cfg5 as the measured workload: a step is one batch of E = 256 GST
+    epochs -- agn_gst_min over this GPU's 4096/G partition clocks for every
+    epoch, one exchange of the E x (D+1) words (RCCL ncclMin allreduce over
+    xGMI for N > 1, agn_gst_allreduce), agn_gst_finalize.  value = partition
+    clock compares per second (P x E per step, whole job: one D-wide
+    vectorclock compare per partition per epoch)."""
+    from antidote_amd import _abi
+    from antidote_amd.engine import Engine
+    cfg = CONFIGS[5]
+    D, P, E = cfg["n_dcs"], cfg["n_keys"], 256
+    Pl = P // world
+    eng = Engine(local)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(cfg["seed"] + rank)
+    clocks = (torch.randint(0, 10 ** 9, (E, Pl, D), device="cuda", dtype=torch.int64,
+                            generator=gen) + 1_700_000_000_000_000)
+    out = torch.empty((E, D + 1), device="cuda", dtype=torch.int64)
+    rccl = world > 1 and backend == "nccl"
+    if rccl:
+        uid = [Engine.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        eng.gst_min(D, Pl, E, clocks.data_ptr(), None, out.data_ptr(), sp)
+        if ev:
+            ev[1].record(stream)
+        if rccl:
+            eng.gst_allreduce(out.data_ptr(), E * (D + 1), sp)
+        elif world > 1:  # gloo rehearsal: the same words through torch.distributed
+            h = out.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MIN)
+            out.copy_(h)
+        eng.gst_finalize(D, E, out.data_ptr(), sp)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s_ in range(a.steps):
+        step(evs[s_])
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    # correctness: the exchanged result equals the min over every rank's local vectors
+    eng.gst_min(D, Pl, E, clocks.data_ptr(), None, out.data_ptr(), sp)
+    torch.cuda.synchronize()
+    local_v = out.clone()
+    step()
+    torch.cuda.synchronize()
+    want = local_v.clone()
+    if world > 1:
+        w = want.cpu() if backend != "nccl" else want
+        dist.all_reduce(w, op=dist.ReduceOp.MIN)
+        want = w.to(out.device)
+    ok = bool(torch.equal(out, want))
+    # the "some partition undefined => 0" rule (stable_time_functions.erl:78-84)
+    # across ranks: one undefined partition on the last rank
+    defined = torch.ones(Pl, device="cuda", dtype=torch.uint8)
+    if rank == world - 1:
+        defined[Pl // 2] = 0
+    one = out[:1]
+    eng.gst_min(D, Pl, 1, clocks.data_ptr(), defined.data_ptr(), one.data_ptr(), sp)
+    if rccl:
+        eng.gst_allreduce(one.data_ptr(), D + 1, sp)
+    elif world > 1:
+        h = one.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MIN)
+        one.copy_(h)
+    eng.gst_finalize(D, 1, one.data_ptr(), sp)
+    torch.cuda.synchronize()
+    ok = ok and int(one[0, D]) == 0 and bool((one[0, :D] == 0).all())
+
+    # single-epoch latency: one epoch through min -> exchange -> finalize
+    def epoch():
+        eng.gst_min(D, Pl, 1, clocks.data_ptr(), None, one.data_ptr(), sp)
+        if rccl:
+            eng.gst_allreduce(one.data_ptr(), D + 1, sp)
+        elif world > 1:
+            h = one.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.MIN)
+            one.copy_(h)
+        eng.gst_finalize(D, 1, one.data_ptr(), sp)
+    for _ in range(5):
+        epoch()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(50):
+        epoch()
+    torch.cuda.synchronize()
+    lat_us = (time.perf_counter() - t1) / 50 * 1e6
+    bytes_launch = E * Pl * D * 8 + E * (D + 1) * 8
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    value = P * E * a.steps / elapsed
+    if rank == 0:
+        traffic, traffic_src = pmc_traffic(5, Pl)
+        cpu = None
+        if world == 1 and a.cpu_keys != 0:
+            lib = _abi.bind(C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so")),
+                            _abi.ORACLE_PROTOTYPES)
+            Es = 16
+            host = np.ascontiguousarray(clocks[:Es].cpu().numpy().view(np.uint64))
+            res = np.zeros((Es, D + 1), np.uint64)
+            reps, secs = 0, 0.0
+            while secs < 5.0:
+                t1 = time.perf_counter()
+                lib.oracle_gst_min(D, Pl, Es, host.ctypes.data, None, res.ctypes.data, 1)
+                secs += time.perf_counter() - t1
+                reps += 1
+            cpu = {"value": P * Es * reps / secs, "unit": "VC compares/s", "cores": 1,
+                   "kind": "port", "sample": f"{Es} epochs x {Pl} partitions x {D} DCs, "
+                   f"oracle/oracle.c oracle_gst_min -O3, 1 thread, {reps} passes = {secs:.1f} s",
+                   "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
+        line = {
+            "metric": "materialized ops/sec + VC compares/sec (1/2/4/8 GPU), % of HBM roofline",
+            "value": value, "unit": "VC compares/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (torch device RNG, clocks near 1.7e15)",
+            "config": {"workload": cfg["name"], "partitions_total": P, "partitions_per_gpu": Pl,
+                       "n_dcs": D, "epochs_per_step": E, "parallelism": f"dp{world}",
+                       "exchange": ("rccl" if rccl else ("torch.distributed " + backend))
+                       if world > 1 else None},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel_src_sha16": kernel_src_sha16(5),
+                         "kernel_ms": kern_ms,
+                         "kernel": "agn_gst_min over 256 epochs (k_gst_init + k_gst_cols), HIP events",
+                         "algorithmic_bytes": bytes_launch},
+            "cpu_baseline": cpu, "exchange_verified": ok, "epoch_latency_us": lat_us,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -17,11 +17,15 @@ import sys
 
 
 def values(path, kern, counter):
+    """Per-dispatch values of the kernel, keeping only the full-size launches
+    (>= half the largest): a bench run also makes small launches of the same
+    kernel (parity checks, cfg5's single-epoch latency loop)."""
     out = []
     for r in csv.DictReader(open(path)):
         if kern in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
             out.append(float(r["Counter_Value"]))
-    return out
+    top = max(out)
+    return [v for v in out if v >= 0.5 * top]
 
 
 def main():

@@ -5,6 +5,11 @@
 // four non-temporal LDS-DMA loads (global_load_lds_dwordx4 nt); every byte is
 // read once.  bench.py reports the materialize kernel's bytes/s both against
 // the 8 TB/s spec peak and against this probe.
+//
+// agn_probe_copy: the same one-shot 4 KiB waves, plain 16-B loads, and the
+// first wq of every four 1 KiB chunks stored to dst (wq = 4: a copy; wq = 3:
+// the GC kernel's ~0.7 write:read mix) -- the practical ceiling for a kernel
+// that reads and writes, reported beside the GC numbers.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -30,6 +35,28 @@ __global__ __launch_bounds__(128) void k_read(const u64x2 *__restrict__ p, uint6
         acc ^= x.x ^ x.y;
     }
     if (acc == 0x9E3779B97F4A7C15ull) out[0] = acc;  // practically never taken
+}
+
+__global__ __launch_bounds__(128) void k_copy(const u64x2 *__restrict__ p, u64x2 *__restrict__ q,
+                                             uint64_t n, int wq) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * 2 + wv;
+    if (w * 256 + 255 >= n) return;
+    u64x2 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = p[w * 256 + j * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j < wq) q[w * 256 + j * 64 + lane] = x[j];
+}
+
+extern "C" int agn_probe_copy(const void *src, void *dst, uint64_t bytes, int wq, void *stream) {
+    const uint64_t n = bytes / 16;
+    const uint64_t nb = n / 512;
+    if (nb == 0 || nb > 0x7fffffffull || wq < 0 || wq > 4) return -1;
+    hipLaunchKernelGGL(k_copy, dim3((unsigned)nb), dim3(128), 0, (hipStream_t)stream,
+                       (const u64x2 *)src, (u64x2 *)dst, n, wq);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 extern "C" int agn_probe_read(const void *buf, uint64_t bytes, void *scratch, void *stream) {
