@@ -98,6 +98,7 @@ KERNEL_SOURCES = {   # the sources the dominant kernel of each config is built f
     3: ("mat_tags.hip", "filter.hpp", "common.hpp"),
     4: ("mat_tags.hip", "filter.hpp", "common.hpp"),
     5: ("gst.hip", "common.hpp"),
+    "gc": ("gc.hip", "filter.hpp", "common.hpp"),
 }
 
 
@@ -192,22 +193,23 @@ def cpu_baseline(cfg, n_keys, threads, target_s=10.0):
     return {nt: work[nt] / secs[nt] for nt in tcounts}, {nt: secs[nt] for nt in tcounts}, reps
 
 
-def pmc_traffic(config, n_units):
+def pmc_traffic(config, n_units, name=None):
     """HBM bytes per launch of the config's dominant kernel from
     profiles/pmc/cfgN.json (scripts/pmc_traffic.py), only when it was measured
     on this build of the kernel's sources and the same units per launch."""
     sha = kernel_src_sha16(config)
-    pmc = os.path.join(ROOT, "profiles", "pmc", f"cfg{config}.json")
+    name = name or f"cfg{config}"
+    pmc = os.path.join(ROOT, "profiles", "pmc", f"{name}.json")
     if not os.path.exists(pmc):
-        return None, f"null: no PMC pass for cfg{config} (profiles/pmc/)"
+        return None, f"null: no PMC pass for {name} (profiles/pmc/)"
     with open(pmc) as f:
         p = json.load(f)
     if p.get("n_keys") == n_units and p.get("kernel_src_sha16") == sha:
         return p.get("hbm_bytes_per_launch"), (
-            f"profiles/pmc/cfg{config}.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of "
+            f"profiles/pmc/{name}.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes of "
             f"{p.get('kernel')} on this kernel build (sources sha {sha}), "
             f"measured {p.get('measured', '?')}")
-    return None, (f"null: profiles/pmc/cfg{config}.json was measured on sources "
+    return None, (f"null: profiles/pmc/{name}.json was measured on sources "
                   f"{p.get('kernel_src_sha16')} / {p.get('n_keys')} units, this build is "
                   f"{sha} / {n_units} units")
 
@@ -315,7 +317,7 @@ def main():
 
     probe = probe_read_gbs(eng, dl, n_keys * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
 
-    gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch) if a.gc else None
+    gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.config) if a.gc else None
     warm = warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.steps) if a.warm else None
     ingest = ingest_bench(eng, cfg, sp, torch) if a.ingest else None
     e2e = e2e_bench(eng, dl, dr, res, cfg, n_keys, torch) if a.e2e else None
@@ -612,7 +614,7 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
             "error_keys": int((flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED)).astype(bool).sum())}
 
 
-def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
+def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch, cfg_id):
     """materializer_vnode GC (prune_ops) over every key of the device log, with
     each key's read snapshot R as the pruning threshold (a snapshot covering a
     random prefix of its ops), both agn_prune_ops output forms:
@@ -678,6 +680,7 @@ def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch):
     # the box's read+write ceiling at the segmented kernel's write:read mix
     # (tools/bwprobe.hip k_copy over the same arrays, wq of 4 chunks stored)
     seg = res["segmented"]
+    seg["traffic"], seg["traffic_source"] = pmc_traffic("gc", n_keys, f"gc_cfg{cfg_id}")
     rd = E * 8 * D + (E if not tags else kept) * per_f
     wq = max(1, min(4, round(4 * (seg["bytes_moved_by_design"] - rd) / max(rd, 1))))
     cp = probe_copy_gbs(eng, dl.oc, out.bufs["oc"].ptr, E * 8 * D, wq, sp, torch)

@@ -13,6 +13,8 @@
 
 -export([open/1, materialize/6, gst_min/5, select_base/7]).
 -export([materialize/4, get_min_time/1]).
+%% clocksi_materializer:new/1, materialize_eager/3; materializer:update_snapshot/3
+-export([new/1, materialize_eager/3, update_snapshot/3]).
 %% engine-owned partition (one per materializer_vnode)
 -export([part_open/5, part_update/5, part_read/5, part_materialize/6, part_gc/3,
          part_gc_due/2, part_stats/1, part_key_meta/2]).
@@ -82,6 +84,37 @@ materialize(Type, TxId, MinSnapshotTime,
                                  Base, {BaseOff, BaseTag, BaseTok}, Log),
     {ok, R} = materialize(ctx(), TypeId, D, Log, Read, CapOff),
     decode(Type, TypeId, Dcs, D, R, Terms, Tags, Toks).
+
+%% clocksi_materializer:new/1 (src/clocksi_materializer.erl:41-43) =
+%% materializer:create_snapshot/1 (src/materializer.erl:45-47).
+new(Type) -> Type:new().
+
+%% clocksi_materializer:materialize_eager/3 (src/clocksi_materializer.erl:
+%% 270-274) -> materializer:materialize_eager/3 (src/materializer.erl:61-70):
+%% every effect applied in order, no snapshot checks, the first failure
+%% returned.  Run as materialize/4 over ops whose only clock entry is one
+%% synthetic DC at time 0, read at that DC's time 0, SCT = ignore: every op
+%% passes the filter (oc <= R) and the fold is the eager fold.
+materialize_eager(Type, Snapshot, Effects) ->
+    N = length(Effects),
+    Ops = [{Id, #clocksi_payload{key = eager, type = Type, op_param = E,
+                                 snapshot_time = dict:new(), commit_time = {'$eager', 0},
+                                 txid = ignore}}
+           || {Id, E} <- lists:zip(lists:seq(N, 1, -1), lists:reverse(Effects))],
+    Resp = #snapshot_get_response{snapshot_time = ignore, ops_list = Ops, number_of_ops = N,
+                                  materialized_snapshot = #materialized_snapshot{last_op_id = 0,
+                                                                                 value = Snapshot}},
+    case materialize(Type, ignore, dict:store('$eager', 0, dict:new()), Resp) of
+        {ok, Value, _NewLastOp, _LastOpCt, _IsNewSS, _Count} -> Value;
+        {error, Reason} -> {error, Reason}
+    end.
+
+%% materializer:update_snapshot/3 (src/materializer.erl:51-58).
+update_snapshot(Type, Snapshot, Effect) ->
+    case materialize_eager(Type, Snapshot, [Effect]) of
+        {error, Reason} -> {error, Reason};
+        Value -> {ok, Value}
+    end.
 
 oldest_first(Ops) when is_list(Ops) -> lists:reverse(Ops);
 oldest_first(Tuple) when is_tuple(Tuple) ->

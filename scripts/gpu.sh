@@ -49,6 +49,13 @@ expand() {
         echo "fetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
         echo "write$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
         echo "pmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_fetch$c/run_counter_collection.csv gpurun_out/prof_write$c/run_counter_collection.csv $k $n $c gpurun_out/pmc/cfg$c.json"
+      done
+      # the one-pass GC kernel (segmented agn_prune_ops) on the cfg2 / cfg3 logs
+      for c in ${PMC_GC_CONFIGS:-2 3}; do
+        case $c in 2) n=10000000;; 3) n=1000000;; esac
+        echo "gcfetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_gcfetch$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "gcwrite$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_gcwrite$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "gcpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_gcfetch$c/run_counter_collection.csv gpurun_out/prof_gcwrite$c/run_counter_collection.csv k_prune_inplace $n gc gpurun_out/pmc/gc_cfg$c.json"
       done;;
     *) echo "$1";;
   esac

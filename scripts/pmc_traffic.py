@@ -3,7 +3,7 @@ each) into HBM bytes per launch of the dominant kernel, with the gfx950
 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of
 a wide coalesced stream (x2); WRITE_SIZE is exact for 16-B stores; both in KB.
 
-  python scripts/pmc_traffic.py <fetch.csv> <write.csv> <kernel-substring> <n_keys> <config> <out.json>
+  python scripts/pmc_traffic.py <fetch.csv> <write.csv> <kernel-substring> <n_keys> <config|gc> <out.json>
 
 The record carries the hash of the kernel's sources (bench.kernel_src_sha16),
 so bench.py uses it only for a build of exactly those sources.
@@ -41,7 +41,7 @@ def main():
            "hbm_read_bytes_per_launch": fb, "hbm_write_bytes_per_launch": wb,
            "hbm_bytes_per_launch": fb + wb,
            "correction": "FETCH_SIZE x2 (gfx950 wide-stream undercount), KB x1024",
-           "kernel_src_sha16": kernel_src_sha16(int(config)),
+           "kernel_src_sha16": kernel_src_sha16(int(config) if config.isdigit() else config),
            "measured": time.strftime("%Y-%m-%d %H:%M UTC", time.gmtime())}
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
     json.dump(rec, open(dst, "w"), indent=1)
