@@ -85,7 +85,7 @@ __global__ __launch_bounds__(GST_THREADS) void k_gst_min(const uint64_t *__restr
 // Undefined partitions only clear word D (they contribute no clock).
 typedef unsigned long long u64x2g __attribute__((ext_vector_type(2)));
 
-template <bool DEF>
+template <bool DEF, int U, bool NT>
 __global__ __launch_bounds__(GST_THREADS) void k_gst_cols(const uint64_t *__restrict__ clocks,
                                                           const uint8_t *__restrict__ defined,
                                                           uint64_t *out, uint32_t D, uint64_t P,
@@ -104,13 +104,15 @@ __global__ __launch_bounds__(GST_THREADS) void k_gst_cols(const uint64_t *__rest
     uint64_t m0 = ~0ull, m1 = ~0ull;
     const uint64_t *base = clocks + e * P * D + c;
     uint64_t p = p0 + r0;
-    for (; p + 3 * RG < p1; p += 4 * RG) {
-        u64x2g v[4];
+    for (; p + (U - 1) * RG < p1; p += U * RG) {
+        u64x2g v[U];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            v[k] = *reinterpret_cast<const u64x2g *>(base + (p + (uint64_t)k * RG) * D);
+        for (int k = 0; k < U; ++k) {
+            const u64x2g *q = reinterpret_cast<const u64x2g *>(base + (p + (uint64_t)k * RG) * D);
+            v[k] = NT ? __builtin_nontemporal_load(q) : *q;
+        }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < U; ++k) {
             bool ok = true;
             if (DEF) ok = defined[e * P + p + (uint64_t)k * RG] != 0;
             if (ok) {
@@ -251,9 +253,20 @@ int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
     if (P == 0 || E == 0) return AGN_OK;
     if (D <= 2u * GST_THREADS && ((2u * GST_THREADS) % D) == 0 && (D % 2u) == 0 &&
         ((uintptr_t)clocks % 16u) == 0) {
-        // column-resident kernel: ~1024 blocks over all epochs, >= 64 rows each
+        // column-resident kernel: ~target blocks over all epochs, >= 32 block
+        // steps each.  A/B knobs: AGN_GST_BLOCKS (target, default 1024),
+        // AGN_GST_UNROLL = 4 | 8 (rows in flight per thread)
+        const char *eb = getenv("AGN_GST_BLOCKS");
+        const char *eu = getenv("AGN_GST_UNROLL");
+        const uint64_t target = eb ? strtoull(eb, nullptr, 10) : 1024;
+        const int unroll = (eu && eu[0] == '8') ? 8 : 4;
+        // non-temporal row loads (default; AGN_GST_NT=0 for plain loads): the
+        // clocks are streamed once, 0.366 -> 0.311 ms on cfg5 (scripts/ab_gst.py,
+        // profiles/r02/ab_gst.log)
+        const char *en = getenv("AGN_GST_NT");
+        const bool nt = !(en && en[0] == '0');
         const uint64_t RG = (2u * GST_THREADS) / D;
-        uint64_t bands = (1024 + E - 1) / E;
+        uint64_t bands = ((target ? target : 1024) + E - 1) / E;
         uint64_t rows = (P + bands - 1) / bands;
         const uint64_t min_rows = 32 * RG;
         if (rows < min_rows) rows = min_rows;
@@ -261,12 +274,23 @@ int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
         bands = (P + rows - 1) / rows;
         const uint64_t blocks = E * bands;
         if (blocks > 0x7fffffffull) return fail(AGN_ENOTSUP, "gst: grid too large");
-        if (defined)
-            hipLaunchKernelGGL(k_gst_cols<true>, dim3((unsigned)blocks), dim3(GST_THREADS), 0, s,
-                               clocks, defined, out, D, P, rows, bands);
-        else
-            hipLaunchKernelGGL(k_gst_cols<false>, dim3((unsigned)blocks), dim3(GST_THREADS), 0, s,
-                               clocks, defined, out, D, P, rows, bands);
+#define AGN_G(DEFV, UV, NTV)                                                                    \
+    hipLaunchKernelGGL((k_gst_cols<DEFV, UV, NTV>), dim3((unsigned)blocks), dim3(GST_THREADS), 0, \
+                       s, clocks, defined, out, D, P, rows, bands)
+#define AGN_GU(DEFV)                                                                            \
+    do {                                                                                        \
+        if (unroll == 8) {                                                                      \
+            if (nt) AGN_G(DEFV, 8, true);                                                       \
+            else AGN_G(DEFV, 8, false);                                                         \
+        } else {                                                                                \
+            if (nt) AGN_G(DEFV, 4, true);                                                       \
+            else AGN_G(DEFV, 4, false);                                                         \
+        }                                                                                       \
+    } while (0)
+        if (defined) AGN_GU(true);
+        else AGN_GU(false);
+#undef AGN_GU
+#undef AGN_G
         AGN_HIP(hipGetLastError());
         return AGN_OK;
     }

@@ -43,7 +43,7 @@ expand() {
       echo "trace|400|rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5";;
     pmc)
       # one counter block per run (FETCH_SIZE, then WRITE_SIZE), per config
-      for c in ${PMC_CONFIGS:-1 2 3 4 5}; do
+      for c in ${PMC_CONFIGS-1 2 3 4 5}; do
         case $c in 1) k=k_counter_key; n=10000;; 2) k=k_counter_key; n=10000000;;
                    3) k=k_tags; n=1000000;; 4) k=k_tags; n=1000000;; 5) k=k_gst_cols; n=4096;; esac
         echo "fetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
@@ -51,7 +51,7 @@ expand() {
         echo "pmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_fetch$c/run_counter_collection.csv gpurun_out/prof_write$c/run_counter_collection.csv $k $n $c gpurun_out/pmc/cfg$c.json"
       done
       # the one-pass GC kernel (segmented agn_prune_ops) on the cfg2 / cfg3 logs
-      for c in ${PMC_GC_CONFIGS:-2 3}; do
+      for c in ${PMC_GC_CONFIGS-2 3}; do
         case $c in 2) n=10000000;; 3) n=1000000;; esac
         echo "gcfetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_gcfetch$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
         echo "gcwrite$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_gcwrite$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
