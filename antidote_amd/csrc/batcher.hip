@@ -17,8 +17,9 @@
 // partition's snapshot cache (agn_ss_cache), and a batch is
 // get_from_snapshot_cache (agn_ss_lookup: the base snapshot <= R) ->
 // materialize/4 from that base -> internal_store_ss / snapshot_insert_gc's
-// policy (agn_ss_store) -> prune_ops of the keys the policy selected
-// (agn_oplog_prune, in place, enqueued after the batch's results are out).
+// policy (agn_ss_store, prune flags per request) -> prune_ops of the keys
+// the policy selected (in place over the batch's key list, enqueued after the
+// batch's results are out; only those keys' segments are visited).
 // One batch holds distinct keys only (the cache's per-key state is
 // read-modify-write); a second read of a key waits for the next batch, so
 // reads of one key are applied in arrival order.
@@ -35,7 +36,7 @@
 #include <unordered_set>
 #include <vector>
 
-#include "common.hpp"
+#include "serve.hpp"
 
 using namespace agn;
 
@@ -49,6 +50,7 @@ struct Pending {
     Clock::time_point t;
     int rc = AGN_OK;
     bool done = false;
+    std::condition_variable cv;  // this caller's wake-up (no herd of every waiter per batch)
     char err[256] = "";
 };
 
@@ -65,7 +67,7 @@ struct agn_batcher {
     uint32_t max_batch = 0, max_wait_us = 0;
 
     std::mutex mu;
-    std::condition_variable cv_work, cv_done;
+    std::condition_variable cv_work;
     std::deque<Pending *> q;
     bool stop = false;
     std::thread worker;
@@ -78,7 +80,6 @@ struct agn_batcher {
     // cached mode: the partition's device snapshot cache + GC scratch
     bool cached = false;
     agn_ss_cache ss{};
-    uint8_t *prune = nullptr;   // [K] agn_ss_store's prune flags
     uint64_t *thr = nullptr;    // [K][D] prune thresholds
     uint64_t *thrm = nullptr;   // [K][W] (sparse logs)
 };
@@ -98,13 +99,6 @@ int grow(agn_batcher *B, size_t bytes) {
     return AGN_OK;
 }
 
-__global__ void __launch_bounds__(256) k_gather_u8(const uint8_t *__restrict__ src,
-                                                   const uint64_t *__restrict__ idx, uint64_t n,
-                                                   uint8_t *__restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = src[idx[i]];
-}
-
 // Cached mode: read/6 for a batch of distinct keys (see the file comment).
 int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
     const uint64_t n = b.size();
@@ -114,6 +108,7 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
     std::vector<uint64_t> keys(n);
     for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
     int rc;
+    size_t o_keys_saved = 0, o_pr_saved = 0;
     {
         std::shared_lock<std::shared_mutex> hold;
         rc = oplog_begin_read(B->log, B->stream, 0, nullptr, nullptr, hold);
@@ -133,6 +128,8 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
                      o_epos = slot(n * 4), o_st = slot(n), o_pr = slot(n);
         rc = grow(B, off);
         if (rc) return rc;
+        o_keys_saved = o_keys;
+        o_pr_saved = o_pr;
         char *h = B->hbuf, *d = B->dbuf;
         auto H = [&](size_t o) { return h + o; };
         uint64_t full[4] = {0, 0, 0, 0};
@@ -180,13 +177,13 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
         // through the kernel from the empty base; its result is discarded
         rc = agn_materialize(B->ctx, &view, &req, &res, B->stream);
         if (rc) return rc;
-        rc = agn_ss_store(B->ctx, &B->ss, &view, n, dkeys, (const uint8_t *)(d + o_first),
-                          (const uint8_t *)(d + o_st), (const uint8_t *)(d + o_gc), &res, nullptr,
-                          B->prune, B->thr, B->thrm, B->stream);
+        // internal_store_ss / snapshot_insert_gc's policy; its prune flags go
+        // per request straight into the batch's output block
+        rc = launch_ss_store_req(B->ss, view.key_off, view.key_len, n, dkeys,
+                                 (const uint8_t *)(d + o_first), (const uint8_t *)(d + o_st),
+                                 (const uint8_t *)(d + o_gc), res, (uint8_t *)(d + o_pr), B->thr,
+                                 B->thrm, B->stream);
         if (rc) return rc;
-        k_gather_u8<<<(unsigned)((n + 255) / 256), 256, 0, B->stream>>>(B->prune, dkeys, n,
-                                                                        (uint8_t *)(d + o_pr));
-        AGN_HIP(hipGetLastError());
         AGN_HIP(hipMemcpyAsync(h + out_start, d + out_start, off - out_start, hipMemcpyDeviceToHost,
                                B->stream));
         AGN_HIP(hipStreamSynchronize(B->stream));
@@ -207,9 +204,11 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
         }
         if (!any_prune) return AGN_OK;
     }  // the shared hold ends: the GC takes the log exclusively
-    // prune_ops of the collected keys (in place, asynchronous: the next
-    // read of the log waits for it)
-    return agn_oplog_prune(B->log, B->prune, B->thr, B->thrm, nullptr, B->stream);
+    // prune_ops of the batch's selected keys (in place, over the batch's key
+    // list and flags still in the device block -- stream-ordered before the
+    // next batch's copy-in -- asynchronous: the next read of the log waits)
+    return oplog_prune_keys(B->log, n, keys.data(), (const uint64_t *)(B->dbuf + o_keys_saved),
+                            (const uint8_t *)(B->dbuf + o_pr_saved), B->thr, B->thrm, B->stream);
 }
 
 // One batch: pack, copy in, materialize over the resident log, copy out, unpack.
@@ -399,8 +398,10 @@ void worker_main(agn_batcher *B) {
         B->n_batches.fetch_add(1, std::memory_order_relaxed);
         B->n_reads.fetch_add(n, std::memory_order_relaxed);
         lk.lock();
-        for (Pending *p : batch) p->done = true;
-        B->cv_done.notify_all();
+        for (Pending *p : batch) {
+            p->done = true;
+            p->cv.notify_one();
+        }
     }
 }
 
@@ -452,8 +453,7 @@ int agn_batcher_destroy(agn_batcher *B) {
     if (B->dbuf) (void)hipFree(B->dbuf);
     if (B->hbuf) (void)hipHostFree(B->hbuf);
     for (void *p : {(void *)B->ss.n, (void *)B->ss.clock, (void *)B->ss.clock_mask,
-                    (void *)B->ss.last_op, (void *)B->ss.value, (void *)B->prune, (void *)B->thr,
-                    (void *)B->thrm})
+                    (void *)B->ss.last_op, (void *)B->ss.value, (void *)B->thr, (void *)B->thrm})
         if (p) (void)hipFree(p);
     if (B->stream) (void)hipStreamDestroy(B->stream);
     delete B;
@@ -483,7 +483,6 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     c.n_dcs = D;
     c.slots = slots;
     c.n_keys = K;
-    uint8_t *prune = nullptr;
     uint64_t *thr = nullptr, *thrm = nullptr;
     hipError_t e = hipMalloc((void **)&c.n, K1 * 4);
     if (e == hipSuccess) e = hipMemset(c.n, 0, K1 * 4);
@@ -491,13 +490,12 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     if (e == hipSuccess && sparse) e = hipMalloc((void **)&c.clock_mask, K1 * slots * W * 8);
     if (e == hipSuccess) e = hipMalloc((void **)&c.last_op, K1 * slots * 8);
     if (e == hipSuccess) e = hipMalloc((void **)&c.value, K1 * slots * 8);
-    if (e == hipSuccess) e = hipMalloc((void **)&prune, K1);
     if (e == hipSuccess) e = hipMalloc((void **)&thr, K1 * D * 8);
     if (e == hipSuccess && sparse) e = hipMalloc((void **)&thrm, K1 * W * 8);
     if (e == hipSuccess) rc = agn_batcher_create(log, max_batch, max_wait_us, out);
     if (e != hipSuccess || rc != AGN_OK) {
         for (void *p : {(void *)c.n, (void *)c.clock, (void *)c.clock_mask, (void *)c.last_op,
-                        (void *)c.value, (void *)prune, (void *)thr, (void *)thrm})
+                        (void *)c.value, (void *)thr, (void *)thrm})
             if (p) (void)hipFree(p);
         return e != hipSuccess ? fail(AGN_ENOMEM, "batcher_create_cached: snapshot cache") : rc;
     }
@@ -505,7 +503,6 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     std::lock_guard<std::mutex> g((*out)->mu);
     (*out)->cached = true;
     (*out)->ss = c;
-    (*out)->prune = prune;
     (*out)->thr = thr;
     (*out)->thrm = thrm;
     return AGN_OK;
@@ -531,7 +528,7 @@ int agn_batcher_read(agn_batcher *B, const agn_key_read *rd, agn_key_result *out
     if (B->stop) return fail(AGN_EINVAL, "batcher_read: batcher is shutting down");
     B->q.push_back(&p);
     if (B->q.size() == 1 || B->q.size() >= B->max_batch) B->cv_work.notify_one();
-    B->cv_done.wait(lk, [&] { return p.done; });
+    p.cv.wait(lk, [&] { return p.done; });
     if (p.rc) return fail(p.rc, "%s", p.err);
     return AGN_OK;
 }

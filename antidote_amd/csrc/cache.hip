@@ -13,7 +13,7 @@
 // cached clocks (8D each, stops at the first <= R) + R and writes the SCT
 // row; store reads the materialize result row + the head clock and rewrites
 // at most SNAPSHOT_MIN + 1 rows.
-#include "common.hpp"
+#include "serve.hpp"
 
 namespace agn {
 namespace {
@@ -130,12 +130,15 @@ __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t
                                                   agn_result res, const int64_t *__restrict__ handle,
                                                   uint8_t *__restrict__ prune,
                                                   uint64_t *__restrict__ thr,
-                                                  uint64_t *__restrict__ thrm) {
+                                                  uint64_t *__restrict__ thrm, int by_req) {
     const Grp<G> g;
     const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
     if (i >= n_req) return;
     const uint32_t D = c.n_dcs, W = n_words(D), S = c.slots;
     const uint64_t k = keys ? keys[i] : i;
+    // by_req: prune flags per request (prune[i], every request written),
+    // otherwise per key (prune[k], the caller cleared the array)
+    if (by_req && g.sub == 0) prune[i] = 0;
     if (status[i] == AGN_SS_LOG) return;
     if (key_n(key_off, key_len, k) == 0) return;  // number_of_ops = 0 (:468-471)
     const uint32_t fl = res.flags[i];
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t
                 thrm[k * W + x] = u;
             }
         }
-        if (g.sub == 0) prune[k] = 1;
+        if (g.sub == 0) prune[by_req ? i : k] = 1;
     }
     if (g.sub == 0) c.n[k] = new_n;
 }
@@ -227,10 +230,10 @@ template <int G>
 int store_g(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len, uint64_t n_req, const uint64_t *keys,
             const uint8_t *is_first, const uint8_t *status, const uint8_t *should_gc,
             const agn_result &res, const int64_t *handle, uint8_t *prune, uint64_t *thr,
-            uint64_t *thrm, hipStream_t st) {
+            uint64_t *thrm, int by_req, hipStream_t st) {
     hipLaunchKernelGGL((k_ss_store<G>), dim3(grid_for(n_req, 256 / G, 0x7fffffffu)), dim3(256), 0,
                        st, c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, handle,
-                       prune, thr, thrm);
+                       prune, thr, thrm, by_req);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }
@@ -267,7 +270,21 @@ int launch_ss_store(const agn_ss_cache &c, const uint64_t *key_off, const uint64
     if (n_req == 0) return AGN_OK;
 #define AGN_C(G) \
     store_g<G>(c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, handle, prune, \
-               thr, thrm, st)
+               thr, thrm, 0, st)
+    AGN_GROUP_DISPATCH(c.n_dcs, AGN_C)
+#undef AGN_C
+}
+
+// The same store with the prune flags per request (prune_req[n_req], no
+// clearing of a per-key array): the cached batcher's form.
+int launch_ss_store_req(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len,
+                        uint64_t n_req, const uint64_t *keys, const uint8_t *is_first,
+                        const uint8_t *status, const uint8_t *should_gc, const agn_result &res,
+                        uint8_t *prune_req, uint64_t *thr, uint64_t *thrm, hipStream_t st) {
+    if (n_req == 0) return AGN_OK;
+#define AGN_C(G) \
+    store_g<G>(c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, nullptr, \
+               prune_req, thr, thrm, 1, st)
     AGN_GROUP_DISPATCH(c.n_dcs, AGN_C)
 #undef AGN_C
 }

@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "filter.hpp"
+#include "serve.hpp"
 
 namespace agn {
 namespace {
@@ -301,6 +302,10 @@ struct InplaceArgs {
     int copy_unselected;       // out of place: keys with prune[k] == 0 are copied whole
     int xcd;                   // XCD-aware block order
     int late_fields;           // entry fields loaded after the filter (kept entries only)
+    // key-list launch (n_keys = list length): entry i is key key_list[i], GC'd
+    // iff list_flags[i] != 0; meta is indexed by i.  NULL = every key, by prune[k].
+    const uint64_t *key_list;
+    const uint8_t *list_flags;
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -323,9 +328,10 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
     // XCD-aware key order: consecutive keys (whose per-key outputs share lines)
     // run on one XCD's L2
     const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t k = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
-    if (k >= a.n_keys) return;
-    const uint64_t K = a.n_keys;
+    const uint64_t i = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
+    if (i >= a.n_keys) return;
+    const uint64_t K = a.n_keys;   // launch size (meta stride)
+    const uint64_t k = a.key_list ? uniform_u64(a.key_list[i]) : i;
     const int lane = lane_id();
     const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -333,16 +339,16 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
     constexpr bool tags = TAGS;
     const uint64_t off = uniform_u64(a.key_off[k]);
     const uint64_t n = uniform_u64(key_n(a.key_off, a.key_len, k));
-    const bool gc = prune == nullptr || prune[k] != 0;
+    const bool gc = a.key_list ? a.list_flags[i] != 0 : (prune == nullptr || prune[k] != 0);
     const uint32_t tb = tags ? (uint32_t)uniform_u64(a.rem_off[off]) : 0u;
     if (lane == 0 && a.d_key_off) a.d_key_off[k] = off;
     if (!gc && !a.copy_unselected) {
         if (lane == 0) {
             if (meta) {
-                meta[k] = (uint32_t)n;
-                meta[K + k] = tags ? a.rem_off[off + n] - tb : 0u;
-                meta[2 * K + k] = a.key_lcap ? a.key_lcap[k] : 0u;
-                meta[3 * K + k] = a.key_id0 ? a.key_id0[k] : AGN_ID0_NONE;
+                meta[i] = (uint32_t)n;
+                meta[K + i] = tags ? a.rem_off[off + n] - tb : 0u;
+                meta[2 * K + i] = a.key_lcap ? a.key_lcap[k] : 0u;
+                meta[3 * K + i] = a.key_id0 ? a.key_id0[k] : AGN_ID0_NONE;
             }
             if (flags) flags[k] = 0u;
         }
@@ -534,10 +540,10 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         if (a.key_lcap) a.key_lcap[k] = lc;
         if (tags && l == 0) a.d_rem_off[off] = tb;  // an empty segment keeps its token base
         if (meta) {
-            meta[k] = l;
-            meta[K + k] = rwritten;
-            meta[2 * K + k] = lc;
-            meta[3 * K + k] = id0;
+            meta[i] = l;
+            meta[K + i] = rwritten;
+            meta[2 * K + i] = lc;
+            meta[3 * K + i] = id0;
         }
         if (flags) flags[k] = (gc && l == 0) ? AGN_GC_ALL_PRUNED : 0u;
     }
@@ -613,6 +619,8 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.D = in.n_dcs;
     a.W = n_words(in.n_dcs);
     a.copy_unselected = 0;
+    a.key_list = nullptr;
+    a.list_flags = nullptr;
     a.xcd = xcd_remap() ? 1 : 0;
     const char *lf = getenv("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
@@ -635,6 +643,29 @@ int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_i
     const bool sparse = view.oc_mask || thr_mask;
     return sparse ? inplace<true>(a, prune, thr, thr_mask, meta, flags, st)
                   : inplace<false>(a, prune, thr, thr_mask, meta, flags, st);
+}
+
+// prune_ops of a key list in place (the cached batcher's GC: the batch's keys,
+// flags[i] from the snapshot-cache policy): n waves instead of one per key of
+// the log; meta[4][n] per list entry.
+int launch_prune_keys(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
+                      uint32_t *key_lcap, uint64_t n, const uint64_t *keys, const uint8_t *flags,
+                      const uint64_t *thr, const uint64_t *thr_mask, uint32_t *meta,
+                      hipStream_t st) {
+    if (n == 0) return AGN_OK;
+    agn_log out = view;
+    out.key_len = key_len;
+    out.key_id0 = key_id0;
+    InplaceArgs a = seg_args(view, out);
+    a.key_len = key_len;
+    a.key_lcap = key_lcap;
+    a.n_keys = n;
+    a.key_list = keys;
+    a.list_flags = flags;
+    a.xcd = 0;
+    const bool sparse = view.oc_mask || thr_mask;
+    return sparse ? inplace<true>(a, nullptr, thr, thr_mask, meta, nullptr, st)
+                  : inplace<false>(a, nullptr, thr, thr_mask, meta, nullptr, st);
 }
 
 // {kept entries, kept removal tokens} of a segmented output: per-block sums

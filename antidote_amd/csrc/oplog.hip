@@ -42,7 +42,7 @@
 #include <shared_mutex>
 #include <vector>
 
-#include "common.hpp"
+#include "serve.hpp"
 
 namespace agn {
 namespace {
@@ -234,6 +234,11 @@ struct agn_oplog {
     uint32_t *d_meta = nullptr;    // [4][K] prune output, copied into `meta`
     hipEvent_t up_done = nullptr, gc_done = nullptr;
     bool up_pending = false, gc_pending = false;
+    // key-list prune (oplog_prune_keys): the keys, their [4][n] records
+    // (device, and the pinned copy the settle scatters)
+    std::vector<uint64_t> gc_list;
+    uint32_t *d_lmeta = nullptr, *h_lmeta = nullptr;
+    uint64_t lmeta_cap = 0, list_since_sum = 0;
     void *pinned = nullptr;
     size_t pinned_bytes = 0;
 
@@ -258,6 +263,25 @@ int settle(agn_oplog *L) {
     if (!L->gc_pending) return AGN_OK;
     L->gc_pending = false;
     AGN_HIP(hipEventSynchronize(L->gc_done));
+    if (!L->gc_list.empty()) {
+        // key-list prune: scatter the listed keys' records, totals by difference
+        const uint64_t n = L->gc_list.size();
+        const uint32_t *m = L->h_lmeta;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t k = L->gc_list[i];
+            L->n_entries = L->n_entries - L->len[k] + m[i];
+            L->n_tokens = L->n_tokens - L->tlen[k] + m[n + i];
+            L->len[k] = m[i];
+            L->tlen[k] = m[n + i];
+            L->lcap[k] = m[2 * n + i];
+            L->id0[k] = m[3 * n + i];
+        }
+        L->gc_list.clear();
+        // the relayout check is O(K): once per K/4 listed keys
+        L->list_since_sum += n;
+        if (L->list_since_sum < L->K / 4 + 1) return AGN_OK;
+    }
+    L->list_since_sum = 0;
     uint64_t ne = 0, nt = 0, want = 0;
     for (uint64_t k = 0; k < L->K; ++k) {
         ne += L->len[k];
@@ -636,10 +660,11 @@ int agn_oplog_destroy(agn_oplog *L) {
     for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
                     (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok,
                     (void *)L->key_off, (void *)L->key_len, (void *)L->key_id0,
-                    (void *)L->key_lcap, (void *)L->d_meta})
+                    (void *)L->key_lcap, (void *)L->d_meta, (void *)L->d_lmeta})
         if (p) (void)hipFree(p);
     if (L->pinned) (void)hipHostFree(L->pinned);
     if (L->meta) (void)hipHostFree(L->meta);
+    if (L->h_lmeta) (void)hipHostFree(L->h_lmeta);
     if (L->up_done) (void)hipEventDestroy(L->up_done);
     if (L->gc_done) (void)hipEventDestroy(L->gc_done);
     delete L;
@@ -895,6 +920,48 @@ int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *k
     return AGN_OK;
 }
 void oplog_view(const agn_oplog *L, agn_log *v) { fill_view(L, v); }
+
+int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uint64_t *d_keys,
+                     const uint8_t *d_flags, const uint64_t *thr, const uint64_t *thr_mask,
+                     hipStream_t st) {
+    if (n == 0) return AGN_OK;
+    if (L->sparse && !thr_mask) return fail(AGN_EINVAL, "oplog_prune_keys: sparse log needs threshold_mask");
+    int rc = use_device(L->ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(L->wmu);
+    std::unique_lock<std::shared_mutex> x(L->rw);
+    rc = settle(L);
+    if (rc) return rc;
+    try {
+        rc = do_flush(L, st);
+        if (rc == AGN_OK && L->relayout_wanted) (void)relayout(L, st);  // best effort
+        if (rc == AGN_OK) L->gc_list.reserve(n);
+    } catch (const std::bad_alloc &) {
+        rc = fail(AGN_ENOMEM, "oplog_prune_keys: host staging");
+    }
+    if (rc) return rc;
+    if (L->used > 0xffffffffull) return fail(AGN_ENOTSUP, "oplog_prune_keys: arena beyond 2^32 slots");
+    if (n > L->lmeta_cap) {
+        const uint64_t c = std::max<uint64_t>(n, 2 * L->lmeta_cap);
+        if (L->d_lmeta) AGN_HIP(hipFree(L->d_lmeta));
+        if (L->h_lmeta) AGN_HIP(hipHostFree(L->h_lmeta));
+        L->d_lmeta = L->h_lmeta = nullptr;
+        L->lmeta_cap = 0;
+        AGN_HIP(hipMalloc((void **)&L->d_lmeta, 4 * c * 4));
+        AGN_HIP(hipHostMalloc((void **)&L->h_lmeta, 4 * c * 4, hipHostMallocDefault));
+        L->lmeta_cap = c;
+    }
+    agn_log view;
+    fill_view(L, &view);
+    rc = launch_prune_keys(view, L->key_len, L->key_id0, L->key_lcap, n, d_keys, d_flags, thr,
+                           thr_mask, L->d_lmeta, st);
+    if (rc) return rc;
+    AGN_HIP(hipMemcpyAsync(L->h_lmeta, L->d_lmeta, 4 * n * 4, hipMemcpyDeviceToHost, st));
+    AGN_HIP(hipEventRecord(L->gc_done, st));
+    L->gc_list.assign(h_keys, h_keys + n);
+    L->gc_pending = true;
+    return AGN_OK;
+}
 void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, uint64_t *K) {
     *crdt = L->crdt;
     *D = L->D;

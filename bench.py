@@ -1037,9 +1037,24 @@ def gst_main(a, torch, dist, world, rank, local, backend):
                 lib.oracle_gst_min(D, Pl, Es, host.ctypes.data, None, res.ctypes.data, 1)
                 secs += time.perf_counter() - t1
                 reps += 1
+            # N threads: one epoch per thread (ctypes releases the GIL)
+            from concurrent.futures import ThreadPoolExecutor
+            thr = min(a.cpu_threads or 16, Es)
+            row = Pl * D * 8
+            def one(e):
+                lib.oracle_gst_min(D, Pl, 1, host.ctypes.data + e * row, None,
+                                   res.ctypes.data + e * (D + 1) * 8, 1)
+            mt_reps, mt_secs = 0, 0.0
+            with ThreadPoolExecutor(thr) as ex:
+                while mt_secs < 5.0:
+                    t1 = time.perf_counter()
+                    list(ex.map(one, range(Es)))
+                    mt_secs += time.perf_counter() - t1
+                    mt_reps += 1
             cpu = {"value": P * Es * reps / secs, "unit": "VC compares/s", "cores": 1,
                    "kind": "port", "sample": f"{Es} epochs x {Pl} partitions x {D} DCs, "
                    f"oracle/oracle.c oracle_gst_min -O3, 1 thread, {reps} passes = {secs:.1f} s",
+                   "value_mt": P * Es * mt_reps / mt_secs, "mt_threads": thr,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
         line = {
             "metric": "materialized ops/sec + VC compares/sec (1/2/4/8 GPU), % of HBM roofline",

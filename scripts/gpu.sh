@@ -12,6 +12,7 @@
 #   trace     : rocprofv3 --kernel-trace --stats of the driver's exact bench
 #               command (profiles/rNN/kernel_stats_*.csv)
 #   pmc       : FETCH_SIZE / WRITE_SIZE passes (one counter block per run)
+#   serve     : the native read/6 serving load generator (tools/serve_bench)
 #
 #   bash scripts/gpu.sh roundend        # expands to the three driver steps
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -57,6 +58,15 @@ expand() {
         echo "gcwrite$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_gcwrite$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
         echo "gcpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_gcfetch$c/run_counter_collection.csv gpurun_out/prof_gcwrite$c/run_counter_collection.csv k_prune_inplace $n gc gpurun_out/pmc/gc_cfg$c.json"
       done;;
+    serve)
+      # native read/6 serving (tools/serve_bench): 250k keys x 64 ops per
+      # partition, D = 8, 20 read servers per partition; 1 and 8 partitions
+      # (one batcher each); with writers (2000 updates/s per partition); and
+      # a 2000-key hot set (cache hits, stores, GC)
+      echo "serve1|150|./tools/serve_bench parts=1 threads=20 reads=20000"
+      echo "serve8|150|./tools/serve_bench parts=8 threads=20 reads=5000"
+      echo "serve8w|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000"
+      echo "serve8h|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000 hot=2000";;
     *) echo "$1";;
   esac
 }
