@@ -1,0 +1,153 @@
+// counter_scan.hpp -- the counter_pn per-key scan shared by the dense
+// counter kernel (mat_counter_dense.hip, the batched materialize/4) and the
+// fused cached read (read6.hip, read/6 from the snapshot cache): wave
+// reductions, row loads, scalar side loads, per-key metadata and the
+// newest-to-oldest filter + fold over a key's ops (one wave per key).
+#pragma once
+#include "common.hpp"
+
+namespace agn {
+namespace {
+
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v, int ctrl_id) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    switch (ctrl_id) {
+        case 0:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0xB1, 0xF, 0xF, false);
+            break;
+        case 1:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0x4E, 0xF, 0xF, false);
+            break;
+        case 2:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0x141, 0xF, 0xF, false);  // row_half_mirror
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0x141, 0xF, 0xF, false);
+            break;
+        default:
+            lo = __builtin_amdgcn_update_dpp(0u, lo, 0x140, 0xF, 0xF, false);  // row_mirror
+            hi = __builtin_amdgcn_update_dpp(0u, hi, 0x140, 0xF, 0xF, false);
+            break;
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Full-wave i64 sum: 4 DPP steps make every 16-lane row uniform, then the 4
+// row totals are read into SGPRs.
+__device__ __forceinline__ int64_t wave_sum_dpp(int64_t x) {
+    uint64_t v = (uint64_t)x;
+    v += dpp_u64(v, 0);
+    v += dpp_u64(v, 1);
+    v += dpp_u64(v, 2);
+    v += dpp_u64(v, 3);
+    uint64_t t = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, r * 16);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), r * 16);
+        t += ((uint64_t)hi << 32) | lo;
+    }
+    return (int64_t)t;
+}
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT, class T>
+__device__ __forceinline__ T ld(const T *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// One OpSSCommit row; 16-byte loads when the row is 16-byte aligned (D even).
+// NT: non-temporal (streamed once; keeps the log from thrashing L2/MALL).
+template <int D, bool NT>
+__device__ __forceinline__ void load_row(const uint64_t *__restrict__ p, uint64_t (&o)[D]) {
+    if constexpr (D % 2 == 0) {
+        const u64x2 *q = reinterpret_cast<const u64x2 *>(p);
+#pragma unroll
+        for (int j = 0; j < D / 2; ++j) {
+            const u64x2 x = ld<NT>(q + j);
+            o[2 * j] = x.x;
+            o[2 * j + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < D; ++j) o[j] = ld<NT>(p + j);
+    }
+}
+
+// Wave-uniform byte (key_type, sct_ignore) through the scalar cache: an s_load
+// of the aligned dword (byte arrays are read in 4-byte units; allocations are
+// rounded up far beyond that), so the check never waits on the vector-memory
+// queue, where it would drain the cross-key prefetch.
+__device__ __forceinline__ uint32_t byte_of(const uint8_t *__restrict__ p, uint64_t idx) {
+    const uint32_t w = reinterpret_cast<const uint32_t *>(p)[idx >> 2];
+    return (w >> ((uint32_t)(idx & 3u) * 8u)) & 0xffu;
+}
+
+// Per-key metadata as branch-free scalar loads, so key_off, the segment
+// length and the id base share one round trip (a conditional load would be
+// scheduled after the previous one's wait): absent arrays are replaced by an
+// in-bounds dummy address whose value is discarded.
+struct KeyMeta {
+    uint64_t off, n;
+    uint32_t id0;
+};
+__device__ __forceinline__ KeyMeta key_meta(uint64_t key, const uint64_t *__restrict__ key_off,
+                                            const uint64_t *__restrict__ key_len,
+                                            const uint32_t *__restrict__ key_id0) {
+    const uint64_t *lp = key_len ? key_len + key : key_off + key + 1;
+    const uint32_t *ip = key_id0 ? key_id0 + key : reinterpret_cast<const uint32_t *>(key_off + key);
+    const uint64_t off = uniform_u64(key_off[key]);
+    const uint64_t l = uniform_u64(*lp);
+    const uint32_t id = __builtin_amdgcn_readfirstlane(*ip);
+    return KeyMeta{off, key_len ? l : l - off, key_id0 ? id : AGN_ID0_NONE};
+}
+
+// Process the key's ops in chunks of 64 (lane = op), rows by 16-byte VGPR
+// loads.  The op id that defines NewLastOp is one scalar load after the scan:
+// loading every lane's op id with its row instead (+4 B per op, no dependent
+// load) measured 2.7 % slower (profiles/r01/ab_counter_ids_wpb.log).
+template <int D, bool WARM>
+__device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
+                                         const int64_t *__restrict__ eff,
+                                         const uint64_t *__restrict__ txid, uint64_t txr,
+                                         uint64_t off, uint64_t n, const uint64_t (&r)[D],
+                                         const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum,
+                                         uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+    const int lane = lane_id();
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        const uint64_t pos = b + (uint64_t)lane;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);  // in-bounds for idle lanes
+        uint64_t o[D];
+        load_row<D, false>(oc + e * D, o);
+        const int64_t ev = eff[e];
+        bool okR = true, leS = true;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            okR = okR && (o[j] <= r[j]);
+            if (WARM) leS = leS && (o[j] <= s[j]);
+        }
+        bool nip = WARM ? !leS : true;  // belongs_to_snapshot_op (ignore -> true)
+        if (txid != nullptr) nip = nip || (txid[e] == txr);
+        const bool incl = valid && nip && okR;
+        const bool excl = valid && nip && !okR;
+        if (first_excl < 0) {
+            const uint64_t bx = ballot(excl);
+            if (bx) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(bx);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) ct[j] = (incl && o[j] > ct[j]) ? o[j] : ct[j];
+        const bool bad = incl && ev == AGN_EFFECT_INVALID;
+        cnt += (uint32_t)__builtin_popcountll(ballot(incl));
+        if (first_err < 0) {
+            const uint64_t be = ballot(bad);
+            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+        }
+        sum += (incl && !bad) ? ev : 0;
+    }
+}
+
+}  // namespace
+}  // namespace agn

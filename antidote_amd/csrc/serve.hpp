@@ -30,3 +30,38 @@ int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uin
                      hipStream_t st);
 
 }  // namespace agn
+
+namespace agn {
+
+// The fused cached read (read6.hip): one kernel per batch runs the whole of
+// materializer_vnode:read/6 for counter_pn with dense clocks (D <= 8).
+// Requests in and results out live in pinned host memory the kernel reads
+// and writes directly (no copy operations); the batch's keys and prune flags
+// are also written to device memory for the stream-ordered GC that follows.
+struct Read6Args {
+    // the partition's log (device view)
+    const uint64_t *key_off, *key_len;
+    const uint32_t *key_id0;
+    const uint8_t *key_type;
+    const uint64_t *oc;
+    const uint32_t *op_id;
+    const int64_t *eff;
+    const uint64_t *log_txid;
+    uint32_t n_dcs, req_type;
+    // the batch (device-visible pinned host memory)
+    uint64_t n_req;
+    const uint64_t *keys, *R, *txid;
+    const uint8_t *gc;
+    int64_t *value, *hole;
+    uint64_t *lastct;
+    uint32_t *count, *flags, *err_pos;
+    uint8_t *status, *prune;
+    // device: the batch's keys and prune flags again, and the GC thresholds [K][D]
+    uint64_t *dkeys;
+    uint8_t *dprune;
+    uint64_t *thr;
+};
+bool read6_supported(const agn_log &view, uint32_t D);
+int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st);
+
+}  // namespace agn

@@ -3,8 +3,10 @@ SURVEY.md §8(b) Ownership / Threading) replayed through the C ABI:
 
   update/2  -> agn_oplog_append (op ids, op_insert_gc's GC trigger) and, when
                due, the GC read (agn_batcher_read with AGN_READ_GC);
-  read/6    -> agn_batcher_read on a cached batcher: agn_ss_lookup ->
-               agn_materialize -> agn_ss_store -> agn_oplog_prune (in place).
+  read/6    -> agn_batcher_read on a cached batcher: the fused one-kernel
+               batch (read6.hip: lookup -> materialize -> store) or, with
+               AGN_READ6=0, agn_ss_lookup -> agn_materialize -> agn_ss_store;
+               then the in-place GC of the batch's selected keys.
 
 Sequentially, every read must equal the reference's transcription
 (oracle/py_oracle.MaterializerVnode: ETS ops tuple, snapshot cache, GC,
@@ -77,7 +79,9 @@ def engine_update(ol, bt, key, ss, oc, eff, txid):
     return int(ids[0])
 
 
-def test_vnode_replay_sequential_vs_reference(eng):
+@pytest.mark.parametrize("read6", ["1", "0"])
+def test_vnode_replay_sequential_vs_reference(eng, monkeypatch, read6):
+    monkeypatch.setenv("AGN_READ6", read6)
     K, steps = 24, 4000
     w = Workload(11, K)
     vn = po.MaterializerVnode()
@@ -129,8 +133,10 @@ def test_vnode_replay_sequential_vs_reference(eng):
         assert (int(ln[k]), int(ll[k]), int(ct[k])) == (length, list_len, vn.ops_cache[k][2]), k
 
 
-def test_vnode_replay_threads_values(eng):
+@pytest.mark.parametrize("read6", ["1", "0"])
+def test_vnode_replay_threads_values(eng, monkeypatch, read6):
     """1 writer (the vnode: update/2 + GC reads) and 8 read servers."""
+    monkeypatch.setenv("AGN_READ6", read6)
     K = 16
     w = Workload(5, K)
     lock = threading.Lock()
