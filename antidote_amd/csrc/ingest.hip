@@ -11,8 +11,10 @@
 //   2. k_join        every update record looks up its transaction's commit c;
 //                    it is emitted iff c comes later in the log and
 //                    check_max_time(snapshot_time(c), Max[key]) holds; its
-//                    sort key is (key << 40) | c (else all ones);
-//   3. stable radix sort of (sort key, record index) — per key: commit order,
+//                    sort key is (key << pb) | c with pb = the bits of a
+//                    record index (else n_keys << pb, after every key);
+//   3. stable radix sort of (sort key, 32-bit record index) over only the
+//                    kb + pb bits a key can have — per key: commit order,
 //                    then update order, exactly dict:append's order;
 //   4. k_bounds      key_off from the sorted keys; k_rows / k_fields gather
 //                    the OpSSCommit rows (snapshot_time with the commit DC
@@ -26,30 +28,59 @@ namespace agn {
 namespace {
 
 constexpr uint64_t EMPTY = ~0ull;
-constexpr int KEY_SHIFT = 40;
-constexpr uint64_t POS_MASK = (1ull << KEY_SHIFT) - 1ull;
+
+// bits needed for the values 0..v
+inline int bits_for(uint64_t v) {
+    int b = 0;
+    while (b < 64 && (v >> b) != 0) ++b;
+    return b ? b : 1;
+}
 
 __device__ __forceinline__ uint64_t slot_of(uint64_t t, uint64_t mask) {
     return (t * 0x9E3779B97F4A7C15ull) >> 20 & mask;
 }
 
-__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t v) {
-    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+// The commit table: open addressing over {txid, first commit index} slot
+// pairs (one 16-byte access per probe), sized on the device from the number
+// of commit records (a power of two >= 1.5x, so a log of 10M commits probes a
+// 256 MiB table that the MALL can hold) -- tab[0] of the scratch holds the
+// mask, the slots follow.
+__global__ void k_count_commits(agn_log_records r, unsigned long long *cnt) {
+    uint64_t c = 0;
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < r.n;
          x += (uint64_t)gridDim.x * blockDim.x)
-        p[x] = v;
+        c += r.kind[x] == AGN_REC_COMMIT;
+    if (c) atomicAdd(cnt, (unsigned long long)c);
 }
 
-__global__ void k_commit_map(agn_log_records r, uint64_t *hk, uint64_t *hv, uint64_t mask) {
+__device__ __forceinline__ uint64_t table_mask(const unsigned long long *cnt) {
+    uint64_t T = 16;
+    const uint64_t want = *cnt + *cnt / 2 + 1;
+    while (T < want) T <<= 1;
+    return T - 1;
+}
+
+__global__ void k_fill(uint64_t *tab, const unsigned long long *cnt) {
+    const uint64_t mask = table_mask(cnt);
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x <= mask;
+         x += (uint64_t)gridDim.x * blockDim.x) {
+        tab[2 * x] = EMPTY;
+        tab[2 * x + 1] = EMPTY;
+    }
+}
+
+__global__ void k_commit_map(agn_log_records r, uint64_t *tab, const unsigned long long *cnt) {
+    const uint64_t mask = table_mask(cnt);
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < r.n;
          x += (uint64_t)gridDim.x * blockDim.x) {
         if (r.kind[x] != AGN_REC_COMMIT) continue;
         const uint64_t t = r.txid[x];
         uint64_t s = slot_of(t, mask);
         for (;;) {
-            const uint64_t prev = atomicCAS((unsigned long long *)&hk[s], (unsigned long long)EMPTY,
-                                            (unsigned long long)t);
+            const uint64_t prev = atomicCAS((unsigned long long *)&tab[2 * s],
+                                            (unsigned long long)EMPTY, (unsigned long long)t);
             if (prev == EMPTY || prev == t) {
-                atomicMin((unsigned long long *)&hv[s], (unsigned long long)x);
+                atomicMin((unsigned long long *)&tab[2 * s + 1], (unsigned long long)x);
                 break;
             }
             s = (s + 1) & mask;
@@ -57,29 +88,36 @@ __global__ void k_commit_map(agn_log_records r, uint64_t *hk, uint64_t *hv, uint
     }
 }
 
-__global__ void k_join(agn_log_records r, uint32_t D, const uint64_t *__restrict__ hk,
-                       const uint64_t *__restrict__ hv, uint64_t mask,
+typedef unsigned long long u64x2i __attribute__((ext_vector_type(2)));
+
+__global__ void k_join(agn_log_records r, uint32_t D, const uint64_t *__restrict__ tab,
+                       const unsigned long long *__restrict__ cnt,
                        const uint64_t *__restrict__ max_t, const uint64_t *__restrict__ max_m,
-                       uint64_t *__restrict__ skey, uint64_t *__restrict__ sval,
-                       unsigned long long *__restrict__ n_out) {
+                       int pb, uint64_t none, uint64_t *__restrict__ skey,
+                       uint32_t *__restrict__ sval, unsigned long long *__restrict__ n_out) {
     const uint32_t W = n_words(D);
+    const uint64_t mask = table_mask(cnt);
+    const u64x2i *slots = reinterpret_cast<const u64x2i *>(tab);
+    uint64_t emitted = 0;
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < r.n;
          x += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t key = EMPTY;
+        uint64_t key = none;
         if (r.kind[x] == AGN_REC_UPDATE) {
             const uint64_t t = r.txid[x];
             uint64_t s = slot_of(t, mask), c = EMPTY;
             for (;;) {
-                const uint64_t h = hk[s];
-                if (h == EMPTY) break;
-                if (h == t) {
-                    c = hv[s];
+                const u64x2i h = slots[s];
+                if (h.x == EMPTY) break;
+                if (h.x == t) {
+                    c = h.y;
                     break;
                 }
                 s = (s + 1) & mask;
             }
-            bool emit = c != EMPTY && c > x;  // the commit follows the update
             const uint64_t k = r.key[x];
+            // the commit follows the update; a key outside the log's key range
+            // is not this partition's (never emitted, never indexed)
+            bool emit = c != EMPTY && c > x && k < (none >> pb);
             if (emit && max_t) {  // check_max_time: le(SnapshotTime, Max), missing = 0
                 for (uint32_t d = 0; d < D && emit; ++d) {
                     const bool pa = !r.ss_mask || ((r.ss_mask[c * W + (d >> 6)] >> (d & 63)) & 1ull);
@@ -88,38 +126,41 @@ __global__ void k_join(agn_log_records r, uint32_t D, const uint64_t *__restrict
                     emit = r.ss[c * D + d] <= (pb ? max_t[k * D + d] : 0ull);
                 }
             }
-            if (emit) {
-                key = (k << KEY_SHIFT) | c;
-                atomicAdd(n_out, 1ull);
-            }
+            if (emit) key = (k << pb) | c;
         }
+        emitted += key != none;
         skey[x] = key;
-        sval[x] = x;
+        sval[x] = (uint32_t)x;
     }
+    // the emitted count: one same-address atomic per thread after the loop
+    // (the compiler folds a wave's into one), not one per record -- per-record
+    // atomics, even wave-aggregated, serialised k_join at 5.7 ms for 30M records
+    if (emitted) atomicAdd(n_out, (unsigned long long)emitted);
 }
 
 // key_off[k] = first sorted position with key >= k; positions [0, E) are
 // the emitted ops, sorted by key.
 __global__ void k_bounds(const uint64_t *__restrict__ skey, const unsigned long long *__restrict__ n_out,
-                         uint64_t n_keys, uint64_t *__restrict__ key_off) {
+                         uint64_t n_keys, int pb, uint64_t *__restrict__ key_off) {
     const uint64_t E = *n_out;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= E;
          p += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t lo = p == 0 ? 0ull : (skey[p - 1] >> KEY_SHIFT) + 1ull;
-        const uint64_t hi = p == E ? n_keys : (skey[p] >> KEY_SHIFT);
+        const uint64_t lo = p == 0 ? 0ull : (skey[p - 1] >> pb) + 1ull;
+        const uint64_t hi = p == E ? n_keys : (skey[p] >> pb);
         for (uint64_t k = lo; k <= hi && k <= n_keys; ++k) key_off[k] = p;
     }
 }
 
 __global__ void k_rows(agn_log_records r, uint32_t D, const uint64_t *__restrict__ skey,
-                       const unsigned long long *__restrict__ n_out, uint64_t *__restrict__ oc,
-                       uint64_t *__restrict__ ocm) {
+                       const unsigned long long *__restrict__ n_out, int pb,
+                       uint64_t *__restrict__ oc, uint64_t *__restrict__ ocm) {
     const uint64_t E = *n_out;
     const uint32_t W = n_words(D);
+    const uint64_t pmask = (1ull << pb) - 1ull;
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < E * D;
          x += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t p = x / D, d = x % D;
-        const uint64_t c = skey[p] & POS_MASK;
+        const uint64_t c = skey[p] & pmask;
         // OpSSCommit: snapshot_time with the commit DC replaced by the commit time
         oc[x] = (d == r.commit_dc[c]) ? r.commit_time[c] : r.ss[c * D + d];
         if (ocm && d < W) {
@@ -132,14 +173,14 @@ __global__ void k_rows(agn_log_records r, uint32_t D, const uint64_t *__restrict
 }
 
 __global__ void k_fields(agn_log_records r, const uint64_t *__restrict__ skey,
-                         const uint64_t *__restrict__ sval,
+                         const uint32_t *__restrict__ sval,
                          const unsigned long long *__restrict__ n_out,
-                         const uint64_t *__restrict__ key_off, uint32_t base, agn_log out,
+                         const uint64_t *__restrict__ key_off, uint32_t base, int pb, agn_log out,
                          uint32_t *__restrict__ rlen) {
     const uint64_t E = *n_out;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < E;
          p += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t u = sval[p], k = skey[p] >> KEY_SHIFT;
+        const uint64_t u = sval[p], k = skey[p] >> pb;
         ((uint32_t *)out.op_id)[p] = base + (uint32_t)(p - key_off[k]);
         if (out.txid) ((uint64_t *)out.txid)[p] = r.txid[u];
         if (out.eff) ((int64_t *)out.eff)[p] = r.eff[u];
@@ -149,7 +190,7 @@ __global__ void k_fields(agn_log_records r, const uint64_t *__restrict__ skey,
     }
 }
 
-__global__ void k_rem_copy(agn_log_records r, const uint64_t *__restrict__ sval,
+__global__ void k_rem_copy(agn_log_records r, const uint32_t *__restrict__ sval,
                            const unsigned long long *__restrict__ n_out, agn_log out) {
     const uint64_t E = *n_out;
     const uint64_t lane = threadIdx.x & 63u;
@@ -183,43 +224,52 @@ int launch_log_ingest(const agn_log_records &r, uint32_t D, uint64_t n_keys,
                       const uint64_t *max_t, const uint64_t *max_m, uint32_t base,
                       const agn_log &out, uint64_t *totals, hipStream_t st) {
     const uint64_t n = r.n;
-    uint64_t T = 1;
-    while (T < 2 * (n ? n : 1)) T <<= 1;
+    if (n > 0xffffffffull) return fail(AGN_ENOTSUP, "log_ingest: %llu records (max 2^32 - 1)",
+                                       (unsigned long long)n);
+    // sort key (key << pb) | commit index: pb bits for a record index, kb for
+    // a key or the "not emitted" marker n_keys
+    const int pb = bits_for(n ? n - 1 : 0), kb = bits_for(n_keys);
+    if (pb + kb > 64) return fail(AGN_ENOTSUP, "log_ingest: %d + %d sort-key bits", pb, kb);
+    const uint64_t none = n_keys << pb;
+    uint64_t T = 16;  // table slots for the worst case (every record a commit)
+    while (T < n + n / 2 + 1) T <<= 1;
     size_t sort_bytes = 0, scan_bytes = 0;
     AGN_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint64_t *)nullptr,
-                                               (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                               (uint64_t *)nullptr, (int)n, 0, 64, st));
+                                               (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                               (uint32_t *)nullptr, (int)n, 0, pb + kb, st));
     AGN_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr,
                                              (uint32_t *)nullptr, (int)n, st));
     const size_t tb = ((sort_bytes > scan_bytes ? sort_bytes : scan_bytes) + 255) / 256 * 256;
-    const size_t words = 2 * T + 4 * n + 2;
-    const size_t bytes = tb + words * 8 + (n + 1) * 4 + 512;
+    const size_t words = 2 * T + 2 * n + 4;  // table k0 k1 n_out cnt (+ v0 v1 as 32-bit)
+    const size_t bytes = tb + words * 8 + 2 * ((n + 1) / 2 * 2) * 4 + (n + 1) * 4 + 512;
     uint8_t *scratch = nullptr;
     AGN_HIP(pool_malloc((void **)&scratch, bytes, st));
     void *tmp = scratch;
-    uint64_t *hk = (uint64_t *)(scratch + tb);
-    uint64_t *hv = hk + T;
-    uint64_t *k0 = hv + T, *v0 = k0 + n, *k1 = v0 + n, *v1 = k1 + n;
-    unsigned long long *n_out = (unsigned long long *)(v1 + n);
-    uint32_t *rlen = (uint32_t *)(n_out + 2);
+    uint64_t *tab = (uint64_t *)(scratch + tb);
+    uint64_t *k0 = tab + 2 * T, *k1 = k0 + n;
+    unsigned long long *n_out = (unsigned long long *)(k1 + n);  // [0] emitted, [2] commits
+    uint32_t *v0 = (uint32_t *)(n_out + 4), *v1 = v0 + (n + 1) / 2 * 2;
+    uint32_t *rlen = v1 + (n + 1) / 2 * 2;
     const unsigned g = 2048;
     hipError_t e = hipSuccess;
-    hipLaunchKernelGGL(k_fill, dim3(g), dim3(256), 0, st, hk, 2 * T, EMPTY);  // hk and hv
-    hipLaunchKernelGGL(k_commit_map, dim3(g), dim3(256), 0, st, r, hk, hv, T - 1);
-    e = hipMemsetAsync(n_out, 0, 16, st);
+    e = hipMemsetAsync(n_out, 0, 32, st);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_join, dim3(g), dim3(256), 0, st, r, D, hk, hv, T - 1, max_t, max_m,
-                           k0, v0, n_out);
-        e = hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, k0, k1, v0, v1, (int)n, 0, 64, st);
+        hipLaunchKernelGGL(k_count_commits, dim3(g), dim3(256), 0, st, r, n_out + 2);
+        hipLaunchKernelGGL(k_fill, dim3(g), dim3(256), 0, st, tab, n_out + 2);
+        hipLaunchKernelGGL(k_commit_map, dim3(g), dim3(256), 0, st, r, tab, n_out + 2);
+        hipLaunchKernelGGL(k_join, dim3(g), dim3(256), 0, st, r, D, tab, n_out + 2, max_t, max_m,
+                           pb, none, k0, v0, n_out);
+        e = hipcub::DeviceRadixSort::SortPairs(tmp, sort_bytes, k0, k1, v0, v1, (int)n, 0, pb + kb,
+                                               st);
     }
     if (e == hipSuccess && r.rem_off) e = hipMemsetAsync(rlen, 0, (n + 1) * sizeof(uint32_t), st);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_bounds, dim3(g), dim3(256), 0, st, k1, n_out, n_keys,
+        hipLaunchKernelGGL(k_bounds, dim3(g), dim3(256), 0, st, k1, n_out, n_keys, pb,
                            (uint64_t *)out.key_off);
-        hipLaunchKernelGGL(k_rows, dim3(g), dim3(256), 0, st, r, D, k1, n_out, (uint64_t *)out.oc,
-                           (uint64_t *)out.oc_mask);
+        hipLaunchKernelGGL(k_rows, dim3(g), dim3(256), 0, st, r, D, k1, n_out, pb,
+                           (uint64_t *)out.oc, (uint64_t *)out.oc_mask);
         hipLaunchKernelGGL(k_fields, dim3(g), dim3(256), 0, st, r, k1, v1, n_out,
-                           (const uint64_t *)out.key_off, base, out,
+                           (const uint64_t *)out.key_off, base, pb, out,
                            r.rem_off ? rlen : (uint32_t *)nullptr);
         e = hipGetLastError();
     }

@@ -396,6 +396,7 @@ int oracle_log_ingest(const agn_log_records *r, uint32_t crdt, uint32_t D, uint6
             if (!tab[s].used || tab[s].head < 0) continue; /* dict:find -> error */
             for (int64_t u = tab[s].head; u >= 0; u = next[u]) {
                 const uint64_t k = r->key[u];
+                if (k >= K) continue; /* not this partition's key (agn_log_ingest skips it too) */
                 int ok = 1;
                 if (max_t) /* check_max_time: vectorclock:le(SnapshotTime, Max) */
                     ok = oracle_vc_le(D, r->ss + x * D, r->ss_mask ? r->ss_mask + x * W : NULL,

@@ -24,14 +24,18 @@ class Records:
     """A random interleaved log: transactions with updates then a commit (or an
     abort, or nothing yet), other record kinds mixed in."""
 
-    def __init__(self, seed, n_txn, K, D, crdt, sparse):
+    def __init__(self, seed, n_txn, K, D, crdt, sparse, foreign=0.0):
+        """foreign: the fraction of updates whose key is outside [0, K) -- not
+        this partition's; the ingest skips them."""
         rng = np.random.default_rng(seed)
         W = (D + 63) // 64
         self.K, self.D, self.W, self.crdt, self.sparse = K, D, W, crdt, sparse
         streams = []
         for t in range(n_txn):
             txid = 1000 + 7 * t
-            recs = [("u", txid, int(rng.integers(0, K))) for _ in range(int(rng.integers(1, 5)))]
+            recs = [("u", txid, int(rng.integers(K, K + 50) if rng.random() < foreign
+                                    else rng.integers(0, K)))
+                    for _ in range(int(rng.integers(1, 5)))]
             if rng.random() < 0.1:
                 recs.append(("o", txid, 0))  # prepare
             end = rng.random()
@@ -146,6 +150,8 @@ def py_filter_terms(rc):
             ss = vc(rc.ss[x], None if rc.ss_mask is None else rc.ss_mask[x], rc.D)
             for u in ops[t]:
                 k = int(rc.key[u])
+                if k >= rc.K:                               # another partition's key
+                    continue
                 if rc.max_t is not None:
                     mx = vc(rc.max_t[k], None if rc.max_m is None else rc.max_m[k], rc.D)
                     if not po.vc_le(ss, mx):            # check_max_time
@@ -162,9 +168,10 @@ CASES = [(_abi.COUNTER_PN, 3, False, False), (_abi.COUNTER_PN, 8, True, True),
          (_abi.COUNTER_PN, 70, True, True)]
 
 
+@pytest.mark.parametrize("foreign", [0.0, 0.05])
 @pytest.mark.parametrize("crdt,D,sparse,use_max", CASES)
-def test_oracle_ingest_vs_dict_transcription(oracle_lib, crdt, D, sparse, use_max):
-    rc = Records(D * 5 + crdt, 400, 37, D, crdt, sparse)
+def test_oracle_ingest_vs_dict_transcription(oracle_lib, crdt, D, sparse, use_max, foreign):
+    rc = Records(D * 5 + crdt, 400, 37, D, crdt, sparse, foreign)
     if use_max:
         rc.with_max(D)
     out, n_out = oracle_ingest(oracle_lib, rc, 0)
@@ -194,7 +201,8 @@ def test_oracle_ingest_vs_dict_transcription(oracle_lib, crdt, D, sparse, use_ma
 @pytest.mark.parametrize("crdt,D,sparse,use_max", CASES + [(_abi.SET_AW, 16, False, False)])
 @pytest.mark.parametrize("base", [0, 1])
 def test_ingest_gpu_vs_oracle(eng, oracle_lib, crdt, D, sparse, use_max, base):
-    rc = Records(D * 11 + crdt + base, 20000, 3000, D, crdt, sparse)
+    # base 1 also carries updates of keys outside the partition
+    rc = Records(D * 11 + crdt + base, 20000, 3000, D, crdt, sparse, 0.03 * base)
     if use_max:
         rc.with_max(D + 1)
     want, n_out = oracle_ingest(oracle_lib, rc, base)
