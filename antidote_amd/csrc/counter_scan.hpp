@@ -108,7 +108,46 @@ __device__ __forceinline__ KeyMeta key_meta(uint64_t key, const uint64_t *__rest
 // loads.  The op id that defines NewLastOp is one scalar load after the scan:
 // loading every lane's op id with its row instead (+4 B per op, no dependent
 // load) measured 2.7 % slower (profiles/r01/ab_counter_ids_wpb.log).
+//
+// PAIR (small D only, where the registers are free): a key longer than one
+// chunk is walked two chunks per step with both chunks' loads issued before
+// either is compared (unconditional loads, idle lanes clamped to the key's
+// first entry), so a 65..128-op key costs one row round trip instead of two --
+// the latency of a small batch (cfg1: 10k keys x 100 ops, one wave per key,
+// ~1.2 waves per wave slot) is a few such round trips.
 template <int D, bool WARM>
+__device__ __forceinline__ void scan_chunk(const uint64_t (&o)[D], int64_t ev, bool valid,
+                                           uint64_t b, const uint64_t *__restrict__ txid,
+                                           uint64_t txr, uint64_t e, const uint64_t (&r)[D],
+                                           const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum,
+                                           uint32_t &cnt, int64_t &first_excl,
+                                           int64_t &first_err) {
+    bool okR = true, leS = true;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        okR = okR && (o[j] <= r[j]);
+        if (WARM) leS = leS && (o[j] <= s[j]);
+    }
+    bool nip = WARM ? !leS : true;  // belongs_to_snapshot_op (ignore -> true)
+    if (txid != nullptr) nip = nip || (txid[e] == txr);
+    const bool incl = valid && nip && okR;
+    const bool excl = valid && nip && !okR;
+    if (first_excl < 0) {
+        const uint64_t bx = ballot(excl);
+        if (bx) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(bx);
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) ct[j] = (incl && o[j] > ct[j]) ? o[j] : ct[j];
+    const bool bad = incl && ev == AGN_EFFECT_INVALID;
+    cnt += (uint32_t)__builtin_popcountll(ballot(incl));
+    if (first_err < 0) {
+        const uint64_t be = ballot(bad);
+        if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+    }
+    sum += (incl && !bad) ? ev : 0;
+}
+
+template <int D, bool WARM, bool PAIR = false>
 __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
                                          const int64_t *__restrict__ eff,
                                          const uint64_t *__restrict__ txid, uint64_t txr,
@@ -116,6 +155,24 @@ __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
                                          const uint64_t (&s)[D], uint64_t (&ct)[D], int64_t &sum,
                                          uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
     const int lane = lane_id();
+    if constexpr (PAIR) {
+        if (n > (uint64_t)AGN_WAVE) {
+            for (uint64_t b = 0; b < n; b += 2 * AGN_WAVE) {
+                const uint64_t p0 = b + (uint64_t)lane, p1 = p0 + AGN_WAVE;
+                const bool v0 = p0 < n, v1 = p1 < n;
+                const uint64_t e0 = off + (v0 ? p0 : 0ull), e1 = off + (v1 ? p1 : 0ull);
+                uint64_t o0[D], o1[D];
+                load_row<D, false>(oc + e0 * D, o0);
+                load_row<D, false>(oc + e1 * D, o1);
+                const int64_t ev0 = eff[e0], ev1 = eff[e1];
+                scan_chunk<D, WARM>(o0, ev0, v0, b, txid, txr, e0, r, s, ct, sum, cnt,
+                                    first_excl, first_err);
+                scan_chunk<D, WARM>(o1, ev1, v1, b + AGN_WAVE, txid, txr, e1, r, s, ct, sum, cnt,
+                                    first_excl, first_err);
+            }
+            return;
+        }
+    }
     for (uint64_t b = 0; b < n; b += AGN_WAVE) {
         const uint64_t pos = b + (uint64_t)lane;
         const bool valid = pos < n;

@@ -40,6 +40,7 @@ struct DenseArgs {
     uint64_t n_entries;
     uint32_t req_type;
     uint32_t xcd;  // 1: XCD-aware block order (xcd_block)
+    uint32_t pair; // 1: D <= 4 keys longer than a chunk walk two chunks per step
 };
 
 typedef __attribute__((address_space(3))) void *lds_ptr;
@@ -219,6 +220,13 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
         else
             hid = scan_key_glds<D, ANY_WARM>(oc, eff, op_id, tx, txr, off, n, a.n_entries, r, s,
                                              ct, sum, cnt, first_excl, first_err, lds_all[w]);
+    } else if (D <= 4 && a.pair) {
+        if (!ANY_WARM || sct_ign)
+            scan_key<D, false, true>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                     first_err);
+        else
+            scan_key<D, ANY_WARM, true>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt,
+                                        first_excl, first_err);
     } else {
         if (!ANY_WARM || sct_ign)
             scan_key<D, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
@@ -276,6 +284,13 @@ inline const uint32_t *id0_index(const agn_log &log) {
     return (v && v[0] == '0') ? nullptr : log.key_id0;
 }
 
+// Two chunks per step for D <= 4 (scan_key PAIR), unless AGN_COUNTER_PAIR=0
+// (A/B knob).
+inline uint32_t pair_chunks() {
+    const char *v = getenv("AGN_COUNTER_PAIR");
+    return (v && v[0] == '0') ? 0u : 1u;
+}
+
 // LDS-DMA row path (even D: 16-byte aligned chunks).  Its speed is
 // box-dependent: on two MI355X boxes it beat the VGPR-load path by 7-10 %
 // (cfg2 7.29-7.55 vs 8.16-8.44 ms), on three others it lost by 6-14 %
@@ -300,7 +315,7 @@ inline bool counter_glds() {
 
 template <int D, int WPB, bool GLDS, bool KEYS>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u};
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, pair_chunks()};
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);

@@ -6,10 +6,13 @@
 // read once.  bench.py reports the materialize kernel's bytes/s both against
 // the 8 TB/s spec peak and against this probe.
 //
-// agn_probe_copy: the same one-shot 4 KiB waves, plain 16-B loads, and the
-// first wq of every four 1 KiB chunks stored to dst (wq = 4: a copy; wq = 3:
-// the GC kernel's ~0.7 write:read mix) -- the practical ceiling for a kernel
-// that reads and writes, reported beside the GC numbers.
+// agn_probe_copy: the same one-shot 4 KiB waves, non-temporal 16-B loads and
+// stores, the first wq of every four 1 KiB chunks stored to dst (wq = 4: a
+// copy; wq = 3: the GC kernel's ~0.7 write:read mix) -- the practical ceiling
+// for a kernel that reads and writes, reported beside the GC numbers.  The
+// fastest of nine read+write idioms (tools/copyprobe_ab.hip,
+// profiles/r02/ab_copy.log): 6.18-6.20 TB/s of bytes read + written against
+// 5.76-5.84 with plain loads and stores, 5.24-5.48 in place.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,10 +47,10 @@ __global__ __launch_bounds__(128) void k_copy(const u64x2 *__restrict__ p, u64x2
     if (w * 256 + 255 >= n) return;
     u64x2 x[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = p[w * 256 + j * 64 + lane];
+    for (int j = 0; j < 4; ++j) x[j] = __builtin_nontemporal_load(p + w * 256 + j * 64 + lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        if (j < wq) q[w * 256 + j * 64 + lane] = x[j];
+        if (j < wq) __builtin_nontemporal_store(x[j], q + w * 256 + j * 64 + lane);
 }
 
 extern "C" int agn_probe_copy(const void *src, void *dst, uint64_t bytes, int wq, void *stream) {
