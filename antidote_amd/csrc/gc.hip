@@ -276,7 +276,8 @@ int launch_prune_ops(const agn_log &log, const uint8_t *prune, const uint64_t *t
 // Per key it then writes the new key_len, key_id0 (consecutive-id base or
 // AGN_ID0_NONE), the ETS ListLen after the resize policy (:540-558, with
 // prune_ops' NewLength = 1 when nothing survives, :580-583) and
-// meta[4][K] = {len, token len, ListLen, id0} for the host's bookkeeping.
+// meta[4][K] = {len, token len, ListLen, id0} for the host's bookkeeping
+// (the engine-owned log: [6][K], the last two rows 0 here -- see k_prune_tail).
 //
 // The same kernel runs out of place into segmented output (agn_prune_ops
 // with out.key_len): every key keeps its input segment start in the output
@@ -306,6 +307,9 @@ struct InplaceArgs {
     // iff list_flags[i] != 0; meta is indexed by i.  NULL = every key, by prune[k].
     const uint64_t *key_list;
     const uint8_t *list_flags;
+    // engine-owned log: meta has 6 rows, the last two the key's live range
+    // start after the prune (entry slot, token slot; arenas < 2^32 slots)
+    int meta6;
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -349,6 +353,10 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
                 meta[K + i] = tags ? a.rem_off[off + n] - tb : 0u;
                 meta[2 * K + i] = a.key_lcap ? a.key_lcap[k] : 0u;
                 meta[3 * K + i] = a.key_id0 ? a.key_id0[k] : AGN_ID0_NONE;
+                if (a.meta6) {
+                    meta[4 * K + i] = (uint32_t)off;
+                    meta[5 * K + i] = tb;
+                }
             }
             if (flags) flags[k] = 0u;
         }
@@ -544,8 +552,279 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
             meta[K + i] = rwritten;
             meta[2 * K + i] = lc;
             meta[3 * K + i] = id0;
+            if (a.meta6) {  // the live range still starts at the segment start
+                meta[4 * K + i] = (uint32_t)off;
+                meta[5 * K + i] = tb;
+            }
         }
         if (flags) flags[k] = (gc && l == 0) ? AGN_GC_ALL_PRUNED : 0u;
+    }
+}
+
+// ---- in-place prune toward the END of the live range (the engine-owned log) --
+// Ops are appended in commit order, so the ops a GC drops (covered by the
+// stored snapshot) are, in the common case, a prefix of the key's log.
+// Compacting the kept entries toward the END of the key's live range instead
+// of its start leaves every kept entry with no dropped entry above it where it
+// is: its row, fields and removal tokens are neither read (fields) nor
+// written.  The live range then starts later in the key's segment: the kernel
+// writes the new key_off, and meta rows 4/5 carry the new live range start
+// (entry slot, token slot) to the host; an append that no longer fits behind
+// the range moves the key to a fresh segment (oplog.hip).
+// Walk: chunks from the newest down; a kept entry's destination is end - 1 -
+// (kept entries above it), so no destination is below its source, every load
+// of a chunk precedes its stores, and a chunk writes only above the next
+// (lower) chunk's sources.  Removal tokens slide the same way (an entry that
+// stays has no token that moves); the token end of a chunk's top entry is
+// carried from the chunk above, whose stores may have rewritten that rem_off
+// slot.  Consecutive-id index: with an index before the GC the kept ids are
+// id0 + position, so it survives iff the kept positions are contiguous and no
+// id is loaded; without one the kept entries' ids are loaded and checked.
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS>
+__global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
+                                                   const uint8_t *__restrict__ prune,
+                                                   const uint64_t *__restrict__ thr,
+                                                   const uint64_t *__restrict__ thr_mask,
+                                                   uint32_t *__restrict__ meta,
+                                                   uint32_t *__restrict__ flags) {
+    using S = Shape<DPL, LPO>;
+    constexpr int OPI = S::OPI;
+    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t i = blk;
+    if (i >= a.n_keys) return;
+    const uint64_t K = a.n_keys;  // launch size (meta stride)
+    const uint64_t k = a.key_list ? uniform_u64(a.key_list[i]) : i;
+    const int lane = lane_id();
+    const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
+    const int hl = slot * LPO;  // the lane holding this op's fields
+    const uint32_t D = a.D, W = a.W;
+    const uint64_t off = uniform_u64(a.key_off[k]);
+    const uint64_t n = uniform_u64(key_n(a.key_off, a.key_len, k));
+    const bool gc = a.key_list ? a.list_flags[i] != 0 : (prune == nullptr || prune[k] != 0);
+    // token range [tb, te) of the key, read before any store
+    const uint32_t tb = TAGS ? __builtin_amdgcn_readfirstlane(a.rem_off[off]) : 0u;
+    const uint32_t te = TAGS ? __builtin_amdgcn_readfirstlane(a.rem_off[off + n]) : 0u;
+    const uint32_t id0_old = a.key_id0 ? __builtin_amdgcn_readfirstlane(a.key_id0[k]) : AGN_ID0_NONE;
+    if (!gc) {
+        if (lane == 0) {
+            if (meta) {
+                meta[i] = (uint32_t)n;
+                meta[K + i] = te - tb;
+                meta[2 * K + i] = a.key_lcap ? a.key_lcap[k] : 0u;
+                meta[3 * K + i] = id0_old;
+                meta[4 * K + i] = (uint32_t)off;
+                meta[5 * K + i] = tb;
+            }
+            if (flags) flags[k] = 0u;
+        }
+        return;
+    }
+    uint64_t t[DPL];
+    const uint32_t tbits = chunk_bits<DPL, SPARSE>(thr_mask, k, W, d0, D);
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) t[j] = ((tbits >> j) & 1u) ? thr[k * D + (uint32_t)(d0 + j)] : 0ull;
+    const agn_log rl = [&] {
+        agn_log l;
+        l.oc = a.oc;
+        l.oc_mask = a.mask;
+        return l;
+    }();
+    const bool derive = id0_old != AGN_ID0_NONE;
+    uint64_t written = 0;             // kept entries above the current chunk
+    uint32_t twritten = 0;            // their tokens
+    uint32_t rtop = te;               // token start of the entry just above the chunk
+    uint32_t low_id = 0;              // id of the lowest kept entry so far (loaded ids)
+    bool consec = true;
+    int64_t lo_pos = -1, hi_pos = -1;  // lowest / highest kept position (derived ids)
+    for (uint64_t c = (n + OPI - 1) / OPI; c-- > 0;) {
+        const uint64_t b = c * (uint64_t)OPI;
+        const uint64_t pos = b + (uint64_t)slot;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);
+        uint64_t o[DPL];
+        uint32_t obits;
+        if constexpr (FULL) {
+            load_rows<DPL, SPARSE, FULL>(rl, e, d0, D, W, o, obits);
+        } else {
+            obits = chunk_bits<DPL, SPARSE>(a.mask, e, W, d0, D);
+#pragma unroll
+            for (int j = 0; j < DPL; ++j)
+                o[j] = ((uint32_t)(d0 + j) < D) ? a.oc[e * D + (uint32_t)(d0 + j)] : 0ull;
+        }
+        uint32_t r0 = 0;
+        if constexpr (TAGS) r0 = (valid && sub == 0) ? a.rem_off[e] : 0u;
+        if (!valid) obits = 0u;
+        bool le = true;
+#pragma unroll
+        for (int j = 0; j < DPL; ++j)
+            if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
+        if (LPO > 1) {
+            const uint64_t grp = ((1ull << LPO) - 1ull) << hl;
+            le = (ballot(!le) & grp) == 0ull;
+        }
+        const bool kp = valid && !le;  // belongs_to_snapshot_op(Threshold, op)
+        const bool head = kp && sub == 0;
+        const uint64_t km = ballot(head);  // one bit per kept op (its head lane)
+        const uint32_t nk = (uint32_t)__builtin_popcountll(km);
+        const uint64_t above = hl >= 63 ? 0ull : (km & (~0ull << (hl + 1)));
+        const uint64_t dst = off + n - 1ull - written - (uint64_t)__builtin_popcountll(above);
+        const bool mv = kp && dst != e;
+        // removal lists: the entry's token end is the start of the entry
+        // above it (the next op's head lane), or the carried start of the
+        // chunk above for the chunk's top op (te for the key's newest)
+        uint32_t rl_ = 0, suf = 0, tdst = 0;
+        if constexpr (TAGS) {
+            const int nx = hl + LPO;
+            uint32_t r1 = (uint32_t)__shfl((int)r0, nx < AGN_WAVE ? nx : 0, AGN_WAVE);
+            if (nx >= AGN_WAVE || pos + 1 >= n) r1 = rtop;
+            rl_ = head ? r1 - r0 : 0u;
+            suf = rl_;  // tokens of the kept entries at or above this lane
+#pragma unroll
+            for (int x = 1; x < AGN_WAVE; x <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_down((int)suf, x, AGN_WAVE);
+                if (lane + x < AGN_WAVE) suf += v;
+            }
+            tdst = te - twritten - suf;
+        }
+        // fields: only the entries that move (and, without an id index, the
+        // ids of every kept entry)
+        uint32_t id = 0, tg = 0;
+        uint64_t tx = 0, ad = 0;
+        int64_t ef = 0;
+        const bool mvh = mv && sub == 0;
+        if (mvh) {
+            id = a.op_id[e];
+            tx = a.txid ? a.txid[e] : 0ull;
+            if constexpr (TAGS) {
+                tg = a.tag[e];
+                ad = a.add[e];
+            } else {
+                ef = a.eff[e];
+            }
+        } else if (!derive && head) {
+            id = a.op_id[e];
+        }
+        uint64_t tk[PT];
+        const bool long_list = TAGS && ballot(mvh && rl_ > (uint32_t)PT) != 0ull;
+        if (TAGS && !long_list && mvh) {
+#pragma unroll
+            for (int x = 0; x < PT; ++x) tk[x] = (uint32_t)x < rl_ ? a.tok[r0 + x] : 0ull;
+        }
+        const uint64_t mw = (SPARSE && a.mask && mv && (uint32_t)sub < W) ? a.mask[e * W + (uint32_t)sub] : 0ull;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // stores: the moving entries only
+        if (mv) {
+            if constexpr (FULL) {
+                u64x2 *q = reinterpret_cast<u64x2 *>(a.d_oc + dst * D + (uint32_t)d0);
+#pragma unroll
+                for (int j = 0; j < DPL / 2; ++j) {
+                    u64x2 x;
+                    x.x = o[2 * j];
+                    x.y = o[2 * j + 1];
+                    q[j] = x;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < DPL; ++j)
+                    if ((uint32_t)(d0 + j) < D) a.d_oc[dst * D + (uint32_t)(d0 + j)] = o[j];
+            }
+            if (SPARSE && a.mask && (uint32_t)sub < W) a.d_mask[dst * W + (uint32_t)sub] = mw;
+        }
+        if (mvh) {
+            a.d_op_id[dst] = id;
+            if (a.d_txid) a.d_txid[dst] = tx;
+            if constexpr (TAGS) {
+                a.d_tag[dst] = tg;
+                a.d_add[dst] = ad;
+            } else {
+                a.d_eff[dst] = ef;
+            }
+        }
+        if constexpr (TAGS) {
+            if (!long_list) {
+                if (mvh) {
+#pragma unroll
+                    for (int x = 0; x < PT; ++x)
+                        if ((uint32_t)x < rl_) a.d_tok[tdst + x] = tk[x];
+                }
+            } else {
+                // newest moving entry first, each list from its top 64 tokens
+                // down: a destination is never below its source
+                uint64_t rest = ballot(mvh);
+                while (rest) {
+                    const int src_lane = 63 - __builtin_clzll(rest);
+                    rest &= ~(1ull << src_lane);
+                    const uint32_t s0 = (uint32_t)__shfl((int)r0, src_lane, AGN_WAVE);
+                    const uint32_t sl = (uint32_t)__shfl((int)rl_, src_lane, AGN_WAVE);
+                    const uint32_t sd = (uint32_t)__shfl((int)tdst, src_lane, AGN_WAVE);
+                    for (uint32_t cc = (sl + AGN_WAVE - 1) / AGN_WAVE; cc-- > 0;) {
+                        const uint32_t j = cc * AGN_WAVE + (uint32_t)lane;
+                        const bool in = j < sl;
+                        const uint64_t v = in ? a.tok[s0 + j] : 0ull;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        if (in) a.d_tok[sd + j] = v;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+            }
+            if (mvh) {
+                a.d_rem_off[dst] = tdst;
+                a.d_rem_off[dst + 1] = tdst + rl_;
+            }
+            twritten += (uint32_t)__builtin_amdgcn_readlane((int)suf, 0);
+            rtop = (uint32_t)__builtin_amdgcn_readlane((int)r0, 0);
+        }
+        // consecutive-id index
+        if (nk) {
+            if (derive) {
+                if (hi_pos < 0) hi_pos = (int64_t)b + (63 - __builtin_clzll(km)) / LPO;
+                lo_pos = (int64_t)b + __builtin_ctzll(km) / LPO;
+            } else {
+                // each kept entry's successor (the next kept above it, or the
+                // lowest kept entry of the chunks above) carries id + 1
+                const int nl = above ? __builtin_ctzll(above) : 0;
+                const uint32_t nid = (uint32_t)__shfl((int)id, nl, AGN_WAVE);
+                bool ok = true;
+                if (head) ok = above ? (nid == id + 1u) : (written == 0 || low_id == id + 1u);
+                consec = consec && (ballot(head && !ok) == 0ull);
+                low_id = (uint32_t)__shfl((int)id, __builtin_ctzll(km), AGN_WAVE);
+            }
+        }
+        written += nk;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) {
+        const uint32_t l = (uint32_t)written;
+        uint32_t id0 = AGN_ID0_NONE;
+        if (l) {
+            if (derive) {
+                if (hi_pos - lo_pos + 1 == (int64_t)l) id0 = id0_old + (uint32_t)lo_pos;
+            } else if (consec && (uint64_t)low_id + (l - 1u) < (uint64_t)AGN_ID0_NONE) {
+                id0 = low_id;
+            }
+        }
+        uint32_t lc = a.key_lcap ? a.key_lcap[k] : 0u;
+        if (lc) {
+            lc = resize_list_len_dev(l ? l : 1u, lc);  // prune_ops' NewLength (1 if none kept)
+            if (lc < l) lc = l;
+        }
+        a.d_key_len[k] = written;
+        a.d_key_off[k] = off + n - written;
+        if (a.key_id0) a.key_id0[k] = id0;
+        if (a.key_lcap) a.key_lcap[k] = lc;
+        if (meta) {
+            meta[i] = l;
+            meta[K + i] = twritten;
+            meta[2 * K + i] = lc;
+            meta[3 * K + i] = id0;
+            meta[4 * K + i] = (uint32_t)(off + n - written);
+            meta[5 * K + i] = te - twritten;
+        }
+        if (flags) flags[k] = l == 0 ? AGN_GC_ALL_PRUNED : 0u;
     }
 }
 
@@ -559,6 +838,20 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     const unsigned blocks = grid_for(a.n_keys, w4 ? 4 : 1, 0x7fffffffu);
     const bool full = !a.mask && (DPL % 2 == 0) && a.D == (uint32_t)(DPL * LPO);
     const bool tags = a.rem_off != nullptr;
+    if (a.d_key_off && a.meta6) {  // the engine-owned log: toward the end of the live range
+#define AGN_T(FULLV, TAGSV)                                                                    \
+    hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV>), dim3(grid_for(a.n_keys, 1, 0x7fffffffu)), \
+                       dim3(64), 0, st, a, prune, thr, thr_mask, meta, flags)
+        if (full) {
+            if (tags) AGN_T((DPL % 2 == 0), true);
+            else AGN_T((DPL % 2 == 0), false);
+        } else {
+            if (tags) AGN_T(false, true);
+            else AGN_T(false, false);
+        }
+#undef AGN_T
+        return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_tail launch");
+    }
 #define AGN_K(FULLV, TAGSV)                                                                    \
     do {                                                                                       \
         if (w4)                                                                                \
@@ -624,7 +917,16 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.xcd = xcd_remap() ? 1 : 0;
     const char *lf = getenv("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
+    a.meta6 = 0;
     return a;
+}
+
+// The engine-owned log's prune: toward the end of the live range (k_prune_tail)
+// unless AGN_PRUNE_TAIL=0 (A/B knob: the start-anchored k_prune_inplace).
+void engine_log_mode(InplaceArgs &a, const agn_log &view) {
+    const char *v = getenv("AGN_PRUNE_TAIL");
+    a.meta6 = 1;
+    a.d_key_off = (v && v[0] == '0') ? nullptr : const_cast<uint64_t *>(view.key_off);
 }
 
 }  // namespace
@@ -640,6 +942,7 @@ int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_i
     InplaceArgs a = seg_args(view, out);
     a.key_len = key_len;
     a.key_lcap = key_lcap;
+    engine_log_mode(a, view);
     const bool sparse = view.oc_mask || thr_mask;
     return sparse ? inplace<true>(a, prune, thr, thr_mask, meta, flags, st)
                   : inplace<false>(a, prune, thr, thr_mask, meta, flags, st);
@@ -647,7 +950,7 @@ int launch_prune_inplace(const agn_log &view, uint64_t *key_len, uint32_t *key_i
 
 // prune_ops of a key list in place (the cached batcher's GC: the batch's keys,
 // flags[i] from the snapshot-cache policy): n waves instead of one per key of
-// the log; meta[4][n] per list entry.
+// the log; meta[6][n] per list entry (the engine-owned log's records).
 int launch_prune_keys(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
                       uint32_t *key_lcap, uint64_t n, const uint64_t *keys, const uint8_t *flags,
                       const uint64_t *thr, const uint64_t *thr_mask, uint32_t *meta,
@@ -663,6 +966,7 @@ int launch_prune_keys(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
     a.key_list = keys;
     a.list_flags = flags;
     a.xcd = 0;
+    engine_log_mode(a, view);
     const bool sparse = view.oc_mask || thr_mask;
     return sparse ? inplace<true>(a, nullptr, thr, thr_mask, meta, nullptr, st)
                   : inplace<false>(a, nullptr, thr, thr_mask, meta, nullptr, st);

@@ -20,12 +20,18 @@
 // move segments, scatter entries, update key_off/key_len.  The arenas grow by
 // doubling with stream-ordered alloc/copy/free.
 //
-// GC.  agn_oplog_prune is one in-place kernel (gc.hip k_prune_inplace): per
+// GC.  agn_oplog_prune is one in-place kernel (gc.hip k_prune_tail): per
 // selected key the VC filter and the compaction of the kept entries toward
-// the segment start, the new key_len / key_id0 and the ETS ListLen after the
-// resize policy (snapshot_insert_gc, :540-558), all on the device; the
-// per-key lengths come back to the host asynchronously (one D2H into the
-// pinned metadata block) and are settled by the next host-side call.  The
+// the END of the key's live range (kept entries with no dropped entry above
+// them -- the common case, GC drops the oldest ops -- are not touched), the
+// new key_off / key_len / key_id0 and the ETS ListLen after the resize policy
+// (snapshot_insert_gc, :540-558), all on the device; the per-key records come
+// back to the host asynchronously (one D2H into the pinned metadata block,
+// with the log's totals reduced on the device) and are settled by the next
+// host-side call.  A key's live entries are [lstart, lstart + len) of its
+// segment [start, start + cap] (tokens [ltstart, ltstart + tlen) of theirs); a
+// prune advances lstart, and an append that no longer fits behind the live
+// range moves the key to a fresh segment.  Slots are u32 (arenas < 2^32).  The
 // physical segments stay where they are; ListLen (`lcap`, what op_insert_gc's
 // GC trigger and the resize policy see) is kept apart from the segment's
 // physical capacity (`cap`).  When the arenas hold more than twice the slots
@@ -167,6 +173,55 @@ __global__ void __launch_bounds__(256) k_relayout(Arena a, Arena b, uint32_t D, 
     copy_segment(a, b, D, W, m.src, m.dst, m.len, m.tsrc, m.tdst, m.tlen, lane_id());
 }
 
+// Totals of a whole-log prune's records [6][stride] on the device, so the
+// host's settle is O(1): {entries, tokens, slots the keys want = sum over the
+// keys with a segment (ListLen != 0) of max(ListLen, length) + 1}.  Per-block
+// partials, then one folding block (no same-address atomics).
+constexpr unsigned TOT_B = 1024;
+__global__ __launch_bounds__(TOT_B) void k_oplog_totals(const uint32_t *__restrict__ meta,
+                                                        uint64_t K, uint64_t stride,
+                                                        uint64_t *__restrict__ part) {
+    __shared__ uint64_t sh[3][TOT_B / 64];
+    uint64_t e = 0, t = 0, w = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * TOT_B + threadIdx.x; k < K;
+         k += (uint64_t)gridDim.x * TOT_B) {
+        const uint32_t l = meta[k], lc = meta[2 * stride + k];
+        e += l;
+        t += meta[stride + k];
+        if (lc) w += (uint64_t)(lc > l ? lc : l) + 1u;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        e += shfl_xor_u64(e, m);
+        t += shfl_xor_u64(t, m);
+        w += shfl_xor_u64(w, m);
+    }
+    const int wv = threadIdx.x >> 6;
+    if (lane_id() == 0) {
+        sh[0][wv] = e;
+        sh[1][wv] = t;
+        sh[2][wv] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint64_t a = 0;
+        for (unsigned x = 0; x < TOT_B / 64; ++x) a += sh[threadIdx.x][x];
+        part[3 * blockIdx.x + threadIdx.x] = a;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_oplog_totals_fold(const uint64_t *__restrict__ part,
+                                                          unsigned nb, uint64_t *__restrict__ out) {
+    uint64_t v[3] = {0, 0, 0};
+    for (unsigned x = threadIdx.x; x < nb; x += 64)
+        for (int j = 0; j < 3; ++j) v[j] += part[3 * x + j];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+        for (int j = 0; j < 3; ++j) v[j] += shfl_xor_u64(v[j], m);
+    if (threadIdx.x == 0)
+        for (int j = 0; j < 3; ++j) out[j] = v[j];
+}
+
 template <class T>
 hipError_t grow_array(T *&p, uint64_t old_n, uint64_t new_n, hipStream_t st) {
     if (!p && old_n) return hipErrorInvalidValue;
@@ -212,10 +267,14 @@ struct agn_oplog {
     std::vector<uint64_t> start, tstart;     // physical segments
     std::vector<uint32_t> cap, tcap, counter;
     std::vector<uint32_t> s_cnt, s_tcnt;     // staged (not yet flushed) entries / tokens
-    // pinned [4][K]: length (staged included), token length, ListLen, key_id0;
-    // a prune's D2H lands here directly (settled by the next host call)
+    // pinned [6][K]: length (staged included), token length, ListLen, key_id0,
+    // live range start (entry slot, token slot); a prune's D2H lands here
+    // directly (settled by the next host call), then [3] u64 totals
+    // {entries, tokens, slots wanted} reduced on the device
     uint32_t *meta = nullptr;
     uint32_t *len = nullptr, *tlen = nullptr, *lcap = nullptr, *id0 = nullptr;
+    uint32_t *lstart = nullptr, *ltstart = nullptr;
+    uint64_t *tot = nullptr;
     std::vector<uint8_t> dirty;
     std::vector<uint64_t> dirty_keys;
     std::vector<int64_t> move_of;  // index into moves, -1 = none pending
@@ -231,10 +290,10 @@ struct agn_oplog {
     uint64_t *key_off = nullptr, *key_len = nullptr;
     uint32_t *key_id0 = nullptr;   // consecutive-id index, kept with key_off / key_len
     uint32_t *key_lcap = nullptr;  // ListLen (the in-place prune applies the resize policy)
-    uint32_t *d_meta = nullptr;    // [4][K] prune output, copied into `meta`
+    uint32_t *d_meta = nullptr;    // [6][K] prune output, copied into `meta`
     hipEvent_t up_done = nullptr, gc_done = nullptr;
     bool up_pending = false, gc_pending = false;
-    // key-list prune (oplog_prune_keys): the keys, their [4][n] records
+    // key-list prune (oplog_prune_keys): the keys, their [6][n] records
     // (device, and the pinned copy the settle scatters)
     std::vector<uint64_t> gc_list;
     uint32_t *d_lmeta = nullptr, *h_lmeta = nullptr;
@@ -275,20 +334,28 @@ int settle(agn_oplog *L) {
             L->tlen[k] = m[n + i];
             L->lcap[k] = m[2 * n + i];
             L->id0[k] = m[3 * n + i];
+            L->lstart[k] = m[4 * n + i];
+            L->ltstart[k] = m[5 * n + i];
         }
         L->gc_list.clear();
         // the relayout check is O(K): once per K/4 listed keys
         L->list_since_sum += n;
         if (L->list_since_sum < L->K / 4 + 1) return AGN_OK;
+        L->list_since_sum = 0;
+        uint64_t ne = 0, nt = 0, want = 0;
+        for (uint64_t k = 0; k < L->K; ++k) {
+            ne += L->len[k];
+            nt += L->tlen[k];
+            if (L->cap[k]) want += (uint64_t)std::max(L->lcap[k], L->len[k]) + 1;
+        }
+        L->tot[0] = ne;
+        L->tot[1] = nt;
+        L->tot[2] = want;
     }
-    L->list_since_sum = 0;
-    uint64_t ne = 0, nt = 0, want = 0;
-    for (uint64_t k = 0; k < L->K; ++k) {
-        ne += L->len[k];
-        nt += L->tlen[k];
-        if (L->cap[k]) want += (uint64_t)std::max(L->lcap[k], L->len[k]) + 1;
-    }
-    L->n_entries = ne;
+    // totals: summed above, or (a whole-log prune) reduced on the device with
+    // the records (k_oplog_totals)
+    const uint64_t want = L->tot[2], nt = L->tot[1];
+    L->n_entries = L->tot[0];
     L->n_tokens = nt;
     L->relayout_wanted = L->used > 2 * want + 1024 || (L->tags && L->tused > 2 * nt + 1024 + 16 * L->K);
     return AGN_OK;
@@ -300,35 +367,46 @@ void oplog_new_segment(agn_oplog *L, uint64_t k, uint32_t need, uint32_t tneed) 
     uint32_t lc = L->lcap[k] ? L->lcap[k] : L->init_slots;
     while (lc < need) lc *= 2;
     L->lcap[k] = lc;
-    // Physical entry segment: a new one at the arena's end when too small.
-    if (need > L->cap[k]) {
+    // A key the GC emptied restarts at its segment start (len counts staged
+    // entries: none exist, on the device or staged); this append marks it
+    // dirty, so the flush writes its key_off.
+    if (L->len[k] == 0) {
+        L->lstart[k] = (uint32_t)L->start[k];
+        L->ltstart[k] = (uint32_t)L->tstart[k];
+    }
+    // Physical entry segment: a new one at the arena's end when the live
+    // range [lstart, lstart + need) does not fit behind the segment start (a
+    // prune's advance included); the live entries move to its start.
+    if ((uint64_t)L->lstart[k] - L->start[k] + need > L->cap[k]) {
         const uint32_t c = std::max(lc, need);
-        const uint64_t old = L->start[k];
+        const uint64_t old = L->lstart[k];
         L->live += (uint64_t)c + 1 - (L->cap[k] ? (uint64_t)L->cap[k] + 1 : 0);
         L->start[k] = L->used;
         L->used += (uint64_t)c + 1;
         L->cap[k] = c;
+        L->lstart[k] = (uint32_t)L->start[k];
         const uint32_t dl = dlen_of(L, k), dt = dtlen_of(L, k);
         if (dl || dt || L->move_of[k] >= 0) {
             if (L->move_of[k] < 0) {
                 L->move_of[k] = (int64_t)L->moves.size();
-                L->moves.push_back(Move{old, 0, L->tstart[k], 0, dl, dt});
+                L->moves.push_back(Move{old, 0, L->ltstart[k], 0, dl, dt});
             }
         }
     }
-    if (L->tags && tneed > L->tcap[k]) {
+    if (L->tags && (uint64_t)L->ltstart[k] - L->tstart[k] + tneed > L->tcap[k]) {
         uint32_t c = L->tcap[k] ? L->tcap[k] : 16u;
         while (c < tneed) c *= 2;
-        const uint64_t old = L->tstart[k];
+        const uint64_t old = L->ltstart[k];
         L->tlive += c - L->tcap[k];
         L->tstart[k] = L->tused;
         L->tused += c;
         L->tcap[k] = c;
+        L->ltstart[k] = (uint32_t)L->tstart[k];
         const uint32_t dl = dlen_of(L, k), dt = dtlen_of(L, k);
         if (dl || dt || L->move_of[k] >= 0) {
             if (L->move_of[k] < 0) {
                 L->move_of[k] = (int64_t)L->moves.size();
-                L->moves.push_back(Move{L->start[k], 0, old, 0, dl, dt});
+                L->moves.push_back(Move{L->lstart[k], 0, old, 0, dl, dt});
             }
         }
     }
@@ -350,6 +428,8 @@ int ensure_pinned(agn_oplog *L, size_t bytes) {
 }
 
 int ensure_arena(agn_oplog *L, hipStream_t st) {
+    if (L->used >= 0xffffffffull)  // slots are u32 (live starts, rem_off)
+        return fail(AGN_ENOTSUP, "oplog: entry arena beyond 2^32 slots");
     if (L->used > L->dcap || !L->a.op_id) {
         uint64_t c = std::max<uint64_t>(L->used, 2 * L->dcap);
         Arena &a = L->a;
@@ -405,14 +485,14 @@ int do_flush(agn_oplog *L, hipStream_t st) {
     // Resolve staged (key, position) to arena slots now that segments are final.
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t k = L->s_key[i];
-        L->s_dst[i] = L->start[k] + L->s_pos[i];
-        L->s_tdst[i] = L->tstart[k] + L->s_tpos[i];
+        L->s_dst[i] = (uint64_t)L->lstart[k] + L->s_pos[i];
+        L->s_tdst[i] = (uint64_t)L->ltstart[k] + L->s_tpos[i];
     }
     for (uint64_t k : L->dirty_keys)
         if (L->move_of[k] >= 0) {
             Move &m = L->moves[L->move_of[k]];
-            m.dst = L->start[k];
-            m.tdst = L->tstart[k];
+            m.dst = L->lstart[k];
+            m.tdst = L->ltstart[k];
         }
     // Pack: moves | dst | tdst | toff | txid | add | tlen | opid | tag | eff | oc | mask | tok | keys
     size_t off = 0;
@@ -448,7 +528,7 @@ int do_flush(agn_oplog *L, hipStream_t st) {
         for (uint64_t j = 0; j < nk; ++j) {
             const uint64_t k = L->dirty_keys[j];
             kv[KV * j] = k;
-            kv[KV * j + 1] = L->start[k];
+            kv[KV * j + 1] = L->lstart[k];
             kv[KV * j + 2] = L->len[k];
             kv[KV * j + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
             kv[KV * j + 4] = L->lcap[k];
@@ -514,7 +594,7 @@ int relayout(agn_oplog *L, hipStream_t st) {
         if (nc[k]) used += (uint64_t)nc[k] + 1;
         tused += ntc[k];
         if (L->cap[k] || L->tcap[k])
-            mv.push_back(Move{L->start[k], ns[k], L->tstart[k], nts[k], L->len[k], L->tlen[k]});
+            mv.push_back(Move{L->lstart[k], ns[k], L->ltstart[k], nts[k], L->len[k], L->tlen[k]});
     }
     const uint64_t U = std::max<uint64_t>(used, 1), TU = std::max<uint64_t>(tused, 1);
     Arena b;
@@ -582,6 +662,10 @@ int relayout(agn_oplog *L, hipStream_t st) {
     L->tused = L->tlive = tused;
     L->start.swap(ns);
     L->tstart.swap(nts);
+    for (uint64_t k = 0; k < K; ++k) {
+        L->lstart[k] = (uint32_t)L->start[k];
+        L->ltstart[k] = (uint32_t)L->tstart[k];
+    }
     L->cap.swap(nc);
     L->tcap.swap(ntc);
     L->relayout_wanted = false;
@@ -624,13 +708,17 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
                     (unsigned long long)n_keys);
     }
     const uint64_t K1 = std::max<uint64_t>(n_keys, 1);
-    hipError_t e = hipHostMalloc((void **)&L->meta, 4 * K1 * 4, hipHostMallocDefault);
+    // [6][K] u32 rows, then 3 u64 totals (8-byte aligned: K1 * 6 * 4 is)
+    hipError_t e = hipHostMalloc((void **)&L->meta, 6 * K1 * 4 + 3 * 8, hipHostMallocDefault);
     if (e == hipSuccess) {
         L->len = L->meta;
         L->tlen = L->meta + K1;
         L->lcap = L->meta + 2 * K1;
         L->id0 = L->meta + 3 * K1;
-        std::memset(L->meta, 0, 3 * K1 * 4);
+        L->lstart = L->meta + 4 * K1;
+        L->ltstart = L->meta + 5 * K1;
+        L->tot = reinterpret_cast<uint64_t *>(L->meta + 6 * K1);
+        std::memset(L->meta, 0, 6 * K1 * 4 + 3 * 8);
         for (uint64_t k = 0; k < K1; ++k) L->id0[k] = AGN_ID0_NONE;
     }
     if (e == hipSuccess) e = hipMalloc((void **)&L->key_off, K1 * 8);
@@ -641,7 +729,7 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
     if (e == hipSuccess) e = hipMemset(L->key_id0, 0xff, K1 * 4);
     if (e == hipSuccess) e = hipMalloc((void **)&L->key_lcap, K1 * 4);
     if (e == hipSuccess) e = hipMemset(L->key_lcap, 0, K1 * 4);
-    if (e == hipSuccess) e = hipMalloc((void **)&L->d_meta, 4 * K1 * 4);
+    if (e == hipSuccess) e = hipMalloc((void **)&L->d_meta, 6 * K1 * 4 + 3 * 8);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L->up_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L->gc_done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -819,9 +907,27 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     rc = launch_prune_inplace(view, L->key_len, L->key_id0, L->key_lcap, prune, threshold,
                               threshold_mask, L->d_meta, out_flags, st);
     if (rc) return rc;
-    // the host's copy of {len, token len, ListLen, id0}: settled by the next call
-    AGN_HIP(hipMemcpyAsync(L->meta, L->d_meta, 4 * std::max<uint64_t>(L->K, 1) * 4,
-                           hipMemcpyDeviceToHost, st));
+    // the log's totals, then the host's copy of {len, token len, ListLen,
+    // id0, live start, token live start} + totals (counter logs: without the
+    // token rows), settled by the next call
+    const uint64_t K1 = std::max<uint64_t>(L->K, 1);
+    {
+        const unsigned nb = (unsigned)std::min<uint64_t>((L->K + TOT_B - 1) / TOT_B, 2048);
+        uint64_t *part = nullptr;
+        AGN_HIP(pool_malloc((void **)&part, (size_t)nb * 3 * 8, st));
+        k_oplog_totals<<<nb, TOT_B, 0, st>>>(L->d_meta, L->K, K1, part);
+        k_oplog_totals_fold<<<1, 64, 0, st>>>(part, nb, reinterpret_cast<uint64_t *>(L->d_meta + 6 * K1));
+        const hipError_t e = hipGetLastError();
+        (void)hipFreeAsync(part, st);
+        AGN_HIP(e);
+    }
+    if (L->tags) {
+        AGN_HIP(hipMemcpyAsync(L->meta, L->d_meta, 6 * K1 * 4 + 3 * 8, hipMemcpyDeviceToHost, st));
+    } else {
+        AGN_HIP(hipMemcpyAsync(L->meta, L->d_meta, K1 * 4, hipMemcpyDeviceToHost, st));
+        AGN_HIP(hipMemcpyAsync(L->meta + 2 * K1, L->d_meta + 2 * K1, 4 * K1 * 4 + 3 * 8,
+                               hipMemcpyDeviceToHost, st));
+    }
     AGN_HIP(hipEventRecord(L->gc_done, st));
     L->gc_pending = true;
     return AGN_OK;
@@ -947,8 +1053,8 @@ int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uin
         if (L->h_lmeta) AGN_HIP(hipHostFree(L->h_lmeta));
         L->d_lmeta = L->h_lmeta = nullptr;
         L->lmeta_cap = 0;
-        AGN_HIP(hipMalloc((void **)&L->d_lmeta, 4 * c * 4));
-        AGN_HIP(hipHostMalloc((void **)&L->h_lmeta, 4 * c * 4, hipHostMallocDefault));
+        AGN_HIP(hipMalloc((void **)&L->d_lmeta, 6 * c * 4));
+        AGN_HIP(hipHostMalloc((void **)&L->h_lmeta, 6 * c * 4, hipHostMallocDefault));
         L->lmeta_cap = c;
     }
     agn_log view;
@@ -956,7 +1062,7 @@ int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uin
     rc = launch_prune_keys(view, L->key_len, L->key_id0, L->key_lcap, n, d_keys, d_flags, thr,
                            thr_mask, L->d_lmeta, st);
     if (rc) return rc;
-    AGN_HIP(hipMemcpyAsync(L->h_lmeta, L->d_lmeta, 4 * n * 4, hipMemcpyDeviceToHost, st));
+    AGN_HIP(hipMemcpyAsync(L->h_lmeta, L->d_lmeta, 6 * n * 4, hipMemcpyDeviceToHost, st));
     AGN_HIP(hipEventRecord(L->gc_done, st));
     L->gc_list.assign(h_keys, h_keys + n);
     L->gc_pending = true;

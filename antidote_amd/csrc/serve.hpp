@@ -15,7 +15,7 @@ int launch_ss_store_req(const agn_ss_cache &c, const uint64_t *key_off, const ui
                         uint8_t *prune_req, uint64_t *thr, uint64_t *thrm, hipStream_t st);
 
 // prune_ops in place over a key list (entry i: key keys[i], GC'd iff
-// flags[i] != 0); meta[4][n] per entry.
+// flags[i] != 0); meta[6][n] per entry.
 int launch_prune_keys(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,
                       uint32_t *key_lcap, uint64_t n, const uint64_t *keys, const uint8_t *flags,
                       const uint64_t *thr, const uint64_t *thr_mask, uint32_t *meta,

@@ -1,7 +1,8 @@
 """Times agn_oplog_prune (engine-owned op log GC) on a synthetic counter log:
 K keys x N ops, D = 8 dense clocks (each rep a fresh log) increasing along each key's log, threshold
 per key = the clock of a random position, so the ops up to it are pruned.
-AGN_LIB selects the library (A/B against tools/libagn_prev.so).
+AGN_LIB selects the library (A/B against tools/libagn_prev.so); AGN_PRUNE_TAIL=0
+selects the start-anchored in-place kernel instead of k_prune_tail.
 
   python scripts/bench_oplog_prune.py [K] [N] [reps]
 """
@@ -56,10 +57,19 @@ def main():
             gpu_ms.append(b.elapsed_time(e))
     kept = st["entries"]
     ms = float(np.median(times))
-    # bytes the GC must move at least: read every OpSSCommit row (the filter),
-    # read the kept entries' effect + id + txid, write the kept entries
+    # bytes a start-anchored compaction must move: read every OpSSCommit row
+    # (the filter), read the kept entries' effect + id + txid, write them
     per = 8 * D + 8 + 4 + 8
     alg = K * N * 8 * D + kept * (per - 8 * D) + kept * per
+    # the end-anchored kernel (k_prune_tail) moves only kept entries with a
+    # dropped entry above them: every row read once, movers read + written,
+    # per key its metadata (key_off, len, id0, ListLen, threshold; new len,
+    # key_off, id0, ListLen, 4 record rows, flag)
+    drop = np.all(oc.reshape(K, N, D) <= thr[:, None, :], axis=2)
+    above = np.flip(np.logical_or.accumulate(np.flip(drop, 1), 1), 1)
+    above = np.concatenate([above[:, 1:], np.zeros((K, 1), bool)], 1)
+    moved = int((~drop & above).sum())
+    tail = K * N * 8 * D + moved * (2 * per - 8 * D) + K * (24 + 8 * D + 44)
     print(json.dumps({"lib": os.path.basename(os.environ.get("AGN_LIB", "libantidote_gpu.so")),
                       "keys": K, "ops_per_key": N, "n_dcs": D, "kept": int(kept),
                       "ms_median": ms, "ms_all": times,
@@ -68,6 +78,8 @@ def main():
                       "wall_over_gpu": ms / float(np.median(gpu_ms)),
                       "min_bytes": alg, "GBps_min_bytes": alg / ms / 1e6,
                       "GBps_min_bytes_gpu": alg / float(np.median(gpu_ms)) / 1e6,
+                      "moved": moved, "tail_bytes": tail,
+                      "prune_tail": os.environ.get("AGN_PRUNE_TAIL", "1") != "0",
                       "note": "ms = prune call + settle (stats); gpu_ms = events around the "
                               "prune on its stream (kernel + metadata copy)"}), flush=True)
 

@@ -201,8 +201,17 @@ def test_oplog_append_materialize(eng, oracle_lib, crdt, D, sparse, init):
         assert not materialize_view(eng, oracle_lib, view, log2, req, sparse)
 
 
+@pytest.fixture(params=["tail", "front"])
+def anchor(request, monkeypatch):
+    """The engine-owned log's prune kernel: k_prune_tail (kept entries compacted
+    toward the end of the live range, the default) or the start-anchored
+    k_prune_inplace (AGN_PRUNE_TAIL=0)."""
+    monkeypatch.setenv("AGN_PRUNE_TAIL", "1" if request.param == "tail" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("crdt,D,sparse,init", CASES)
-def test_oplog_prune_then_append(eng, oracle_lib, crdt, D, sparse, init):
+def test_oplog_prune_then_append(eng, oracle_lib, anchor, crdt, D, sparse, init):
     rng = np.random.default_rng(D * 11 + crdt + init)
     tags = crdt != _abi.COUNTER_PN
     W = (D + 63) // 64
@@ -260,6 +269,88 @@ def test_oplog_prune_then_append(eng, oracle_lib, crdt, D, sparse, init):
         for b in (bp, bt, btm, fl):
             if b is not None:
                 b.free()
+
+
+def pruned_log(want, n_out, crdt, D, K, sparse):
+    """The oracle's prune_ops output (CSR) as an EncodedLog."""
+    tags = crdt != _abi.COUNTER_PN
+    out = EncodedLog(crdt_type=crdt, n_dcs=D, key_off=want["key_off"],
+                     key_type=np.full(K, crdt, np.uint8), oc=want["oc"][:n_out],
+                     oc_mask=want["oc_mask"][:n_out] if sparse else None,
+                     op_id=want["op_id"][:n_out], txid=want["txid"][:n_out])
+    if tags:
+        nr = int(want["rem_off"][n_out])
+        out.tag, out.add_tok = want["tag"][:n_out], want["add_tok"][:n_out]
+        out.rem_off = want["rem_off"][:n_out + 1]
+        out.rem_tok = want["rem_tok"][:max(nr, 1)]
+    else:
+        out.eff = want["eff"][:n_out]
+    return out
+
+
+@pytest.mark.parametrize("crdt,D,sparse", [(_abi.COUNTER_PN, 8, False), (_abi.SET_AW, 5, False),
+                                           (_abi.SET_AW, 16, True), (_abi.REGISTER_MV, 64, False)])
+def test_oplog_prefix_gc_cycles(eng, oracle_lib, monkeypatch, crdt, D, sparse):
+    """The common GC shape: clocks grow along each key's log, so a prune drops
+    (mostly) a prefix and the tail-anchored kernel leaves the kept entries in
+    place and advances the key's live range.  Six rounds of append -> prune
+    (per key: nothing / a prefix / everything / not selected) -> check the
+    segments, flags, id index and reads against the oracle, so live ranges
+    advance, run into their segment ends, move, restart after an all-pruned
+    GC, and the arenas are re-laid out."""
+    monkeypatch.setenv("AGN_PRUNE_TAIL", "1")
+    rng = np.random.default_rng(D * 31 + crdt)
+    K, W, tags = 48, (D + 63) // 64, crdt != _abi.COUNTER_PN
+    expect = None
+    counters = np.zeros(K, np.int64)
+    with OpLog(eng, crdt, D, K, sparse=sparse, init_slots=4) as ol:
+        for cycle in range(6):
+            more, req, _ = random_case(97 * cycle + D + crdt, crdt, K, D, 24, sparse=sparse,
+                                       multi=0.2 if crdt == _abi.SET_AW else 0.0, empty=0.2)
+            shift = np.uint64(100_000 * (cycle + 1))     # later rounds are newer
+            more.oc = more.oc + shift
+            req.R = req.R + shift
+            got = append_ops(ol, more, interleave(rng, ops_of(more)), rng)
+            expect_counter_ids(more, got, counters)
+            for k in range(K):
+                a, b = int(more.key_off[k]), int(more.key_off[k + 1])
+                counters[k] = max([counters[k]] + [got[e] for e in range(a, b)])
+            new = renumbered(more, got)
+            expect = new if expect is None else concat(expect, new)
+            view = ol.flush()
+            assert not materialize_view(eng, oracle_lib, view, expect, req, sparse)
+            # prefix thresholds: the max OpSSCommit of the key's first `cut` ops
+            thr = np.zeros((K, D), np.uint64)
+            prune = (rng.random(K) < 0.85).astype(np.uint8)
+            for k in range(K):
+                a, b = int(expect.key_off[k]), int(expect.key_off[k + 1])
+                r = rng.random()
+                cut = 0 if r < 0.1 else (b - a) if r < 0.25 else int(rng.integers(0, b - a + 1))
+                if cut:
+                    thr[k] = expect.oc[a:a + cut].max(axis=0)
+            tm = np.full((K, W), ~np.uint64(0), np.uint64) if sparse else None
+            want, wflags, n_out = oracle_prune(oracle_lib, expect, prune, thr, tm)
+            bp, bt = eng.upload(prune), eng.upload(thr)
+            btm = eng.upload(tm) if tm is not None else None
+            fl = eng.empty(4 * K)
+            ol.prune(bp.ptr, bt.ptr, btm.ptr if btm else None, fl.ptr)
+            assert np.array_equal(eng.download(fl, np.uint32, (K,)), wflags), cycle
+            assert ol.stats()["entries"] == n_out
+            view = ol.flush()
+            check_id_index(eng, view, K)
+            segs = segments(eng, view, K, D, W, tags, sparse)
+            for k in range(K):
+                for name, v in csr_key(want, k, tags).items():
+                    g = segs[k][name]
+                    if name == "rems":
+                        assert g == v, (cycle, k, name)
+                    else:
+                        assert np.array_equal(np.asarray(g), np.asarray(v)), (cycle, k, name)
+            expect = pruned_log(want, n_out, crdt, D, K, sparse)
+            assert not materialize_view(eng, oracle_lib, view, expect, req, sparse), cycle
+            for bf in (bp, bt, btm, fl):
+                if bf is not None:
+                    bf.free()
 
 
 def concat(a, b):
