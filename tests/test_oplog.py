@@ -353,6 +353,65 @@ def test_oplog_prefix_gc_cycles(eng, oracle_lib, monkeypatch, crdt, D, sparse):
                     bf.free()
 
 
+def long_list_log(seed, crdt, K, D, nmax):
+    """A tag log whose removal lists are often long (5..150 tokens), with
+    random clocks, so a prune drops entries scattered through each key and
+    entries with long lists move (the kernels' entry-by-entry token copy)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(nmax // 2, nmax + 1, K)
+    key_off = np.zeros(K + 1, np.uint64)
+    key_off[1:] = np.cumsum(lens)
+    E = int(key_off[-1])
+    rl = rng.integers(0, 3, E)
+    longs = rng.random(E) < 0.3
+    rl[longs] = rng.integers(5, 151, int(longs.sum()))
+    rem_off = np.zeros(E + 1, np.uint32)
+    rem_off[1:] = np.cumsum(rl)
+    op_id = np.concatenate([np.arange(1, n + 1) for n in lens]).astype(np.uint32)
+    log = EncodedLog(crdt_type=crdt, n_dcs=D, key_off=key_off,
+                     key_type=np.full(K, crdt, np.uint8),
+                     oc=rng.integers(1, 1000, (E, D)).astype(np.uint64), oc_mask=None,
+                     op_id=op_id, txid=rng.integers(1, 6, E).astype(np.uint64))
+    log.tag = rng.integers(0, 5, E).astype(np.uint32)
+    log.add_tok = np.arange(1, E + 1, dtype=np.uint64) << np.uint64(8)
+    log.rem_off = rem_off
+    log.rem_tok = rng.integers(1, 1 << 40, max(int(rem_off[-1]), 1)).astype(np.uint64)
+    return log
+
+
+@pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])
+def test_oplog_prune_long_removal_lists(eng, oracle_lib, anchor, crdt):
+    """Entries with removal lists longer than the kernels' register buffer
+    move during an in-place prune (both anchors), twice, with appends between."""
+    rng = np.random.default_rng(5 + crdt)
+    K, D, W = 24, 6, 1
+    log = long_list_log(41 + crdt, crdt, K, D, 70)
+    _, req, _ = random_case(43 + crdt, crdt, K, D, 10)
+    with OpLog(eng, crdt, D, K, init_slots=2) as ol:
+        got = append_ops(ol, log, interleave(rng, ops_of(log)), rng)
+        cur = renumbered(log, got)
+        for rnd in range(2):
+            prune, thr, _ = thresholds(61 + rnd + crdt, cur, False)
+            want, wflags, n_out = oracle_prune(oracle_lib, cur, prune, thr, None)
+            bp, bt, fl = eng.upload(prune), eng.upload(thr), eng.empty(4 * K)
+            ol.prune(bp.ptr, bt.ptr, None, fl.ptr)
+            assert np.array_equal(eng.download(fl, np.uint32, (K,)), wflags), rnd
+            assert ol.stats()["entries"] == n_out
+            view = ol.flush()
+            check_id_index(eng, view, K)
+            check_segments(eng, view, want, K, D, W, True, False)
+            cur = pruned_log(want, n_out, crdt, D, K, False)
+            assert not materialize_view(eng, oracle_lib, view, cur, req, False), rnd
+            more = long_list_log(71 + rnd + crdt, crdt, K, D, 20)
+            more.add_tok = more.add_tok + np.uint64(1 << 50)
+            got2 = append_ops(ol, more, interleave(rng, ops_of(more)), rng)
+            cur = concat(cur, renumbered(more, got2))
+            view = ol.flush()
+            assert not materialize_view(eng, oracle_lib, view, cur, req, False), rnd
+            for b in (bp, bt, fl):
+                b.free()
+
+
 def concat(a, b):
     """Per key: a's entries then b's (both CSR)."""
     K, tags = a.n_keys, a.crdt_type != _abi.COUNTER_PN
