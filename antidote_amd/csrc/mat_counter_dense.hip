@@ -6,13 +6,14 @@
 //     arguments + readfirstlane keep them in SGPRs (s_load, no VGPRs);
 //   * no presence masks (every DC present), so "+1 encoding" and per-DC
 //     branches disappear;
-//   * rows are 16-byte VGPR loads (scan_key); an opt-in variant for even D
-//     (AGN_COUNTER_GLDS=1, scan_key_glds) streams each chunk of 64 entries
+//   * rows are 16-byte VGPR loads (scan_key); for D = 8 a lane-contiguous
+//     "quad rows" variant (scan_key_q8, non-temporal); for even D
+//     (scan_key_glds) each chunk of 64 entries is streamed
 //     (OpSSCommit rows, effects, op ids) into LDS by non-temporal LDS-DMA
 //     (global_load_lds), the fastest pure-read idiom measured (7.1-7.2 TB/s
 //     against 6.0 for 16-byte VGPR loads, profiles/r01/ab_read_probe.log),
 //     and reads the NewLastOp op id from LDS instead of a dependent load --
-//     faster on some boxes, slower on others (counter_glds below);
+//     faster on some boxes, slower on others (counter_variant below);
 //   * cold (SCT = ignore) and warm reads run separate loop bodies, so the
 //     cold body does one D-wide compare per op, exactly the reference's
 //     VC compare count;
@@ -41,6 +42,7 @@ struct DenseArgs {
     uint32_t req_type;
     uint32_t xcd;  // 1: XCD-aware block order (xcd_block)
     uint32_t pair; // 1: D <= 4 keys longer than a chunk walk two chunks per step
+    uint32_t qnt;  // quad rows, non-temporal loads: bit 0 rows, bit 1 effects (AGN_COUNTER_QUAD_NT)
 };
 
 typedef __attribute__((address_space(3))) void *lds_ptr;
@@ -147,6 +149,85 @@ __device__ __forceinline__ int64_t scan_key_glds(
     return hid;
 }
 
+// Bit q of the result = some bit of nibble q of b (q = 0..15), on the scalar
+// unit: the per-op verdict of a ballot whose 4 lanes per op are its 4 parts.
+__device__ __forceinline__ uint64_t nib_any16(uint64_t b) {
+    b |= b >> 1;
+    b |= b >> 2;
+    b &= 0x1111111111111111ull;
+    b = (b | (b >> 3)) & 0x0303030303030303ull;
+    b = (b | (b >> 6)) & 0x000F000F000F000Full;
+    b = (b | (b >> 12)) & 0x000000FF000000FFull;
+    return (b | (b >> 24)) & 0xFFFFull;
+}
+
+// scan_key for D = 8 with lane-CONTIGUOUS row loads ("quad rows"): load j of a
+// 64-op chunk reads bytes [1 KiB j, 1 KiB (j+1)) of the chunk's rows, so
+// every instruction covers 8 whole 128-byte lines -- the row-per-lane loads
+// of scan_key touch 32 lines per instruction, 32 bytes of each, and request
+// every line four times.  Lane l holds DCs 2p, 2p+1 (p = l & 3) of op
+// 16 j + (l >> 2): the per-op verdicts are nibbles of wave ballots folded on
+// the scalar unit into 64-bit op masks (incl / excl), and the LastOpCt maxima
+// stay per part (ctA, ctB) until one xor-shuffle fold at the end of the key.
+// The effect (and TxId) loads stay lane = op.  Same results as scan_key.
+template <bool WARM, bool NT, bool EFF_NT = false>
+__device__ __forceinline__ void scan_key_q8(
+    const uint64_t *__restrict__ oc, const int64_t *__restrict__ eff,
+    const uint64_t *__restrict__ txid, uint64_t txr, uint64_t off, uint64_t n,
+    uint64_t n_entries, uint64_t rA, uint64_t rB, uint64_t sA, uint64_t sB, uint64_t &ctA,
+    uint64_t &ctB, int64_t &sum, uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+    const int lane = lane_id();
+    const int q = lane >> 2;
+    const u64x2 *rows = reinterpret_cast<const u64x2 *>(oc);
+    const uint64_t lim = n_entries * 4u - 1u, lim_e = n_entries - 1u;
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        u64x2 x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t u = (off + b) * 4u + (uint64_t)(j * AGN_WAVE + lane);
+            u = u < lim ? u : lim;  // past the log's end: clamped, masked below
+            x[j] = ld<NT>(rows + u);
+        }
+        uint64_t e = off + b + (uint64_t)lane;
+        e = e < lim_e ? e : lim_e;
+        const int64_t ev = ld<NT && EFF_NT>(eff + e);
+        // every load of the chunk is in flight before the first verdict (left
+        // alone, the scheduler interleaves the ballots with the loads and
+        // waits for each row load in turn)
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t valid = (n - b >= (uint64_t)AGN_WAVE) ? ~0ull : ((1ull << (n - b)) - 1ull);
+        uint64_t bad = 0, gt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bad |= nib_any16(ballot(x[j].x > rA || x[j].y > rB)) << (16 * j);
+            if (WARM) gt |= nib_any16(ballot(x[j].x > sA || x[j].y > sB)) << (16 * j);
+        }
+        uint64_t nip = WARM ? gt : ~0ull;  // belongs_to_snapshot_op: not covered by SCT
+        if (txid != nullptr) nip |= ballot(txid[e] == txr);
+        const uint64_t incl = valid & nip & ~bad, excl = valid & nip & bad;
+        if (first_excl < 0 && excl) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(excl);
+        cnt += (uint32_t)__builtin_popcountll(incl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool in = ((incl >> (16 * j + q)) & 1ull) != 0ull;
+            ctA = (in && x[j].x > ctA) ? x[j].x : ctA;
+            ctB = (in && x[j].y > ctB) ? x[j].y : ctB;
+        }
+        const bool mine = ((incl >> lane) & 1ull) != 0ull;
+        const bool badv = mine && ev == AGN_EFFECT_INVALID;
+        if (first_err < 0) {
+            const uint64_t be = ballot(badv);
+            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+        }
+        sum += (mine && !badv) ? ev : 0;
+    }
+}
+
+// Row-load variants of k_counter_key (bit-identical results; agn_tune picks
+// per device): VGPR rows (scan_key), LDS-DMA rows (scan_key_glds, even D),
+// quad rows (scan_key_q8, D = 8, non-temporal).
+enum { ROWS_VGPR = 0, ROWS_GLDS = 1, ROWS_QUAD = 2 };
+
 // One wave = one request, no loop: the grid is the batch (ceil(n_req / WPB)
 // blocks).  Measured on cfg2 this beats every software-pipelined variant
 // above: with ~10M short-lived waves the dispatcher keeps every CU's wave
@@ -165,7 +246,7 @@ __device__ __forceinline__ int64_t scan_key_glds(
 // (writing 16 B instead: 8.33 -> 7.57 ms), full 128 B record lines 1 %,
 // non-temporal stores +7 % worse.  The HBM read/write turnaround, not the
 // instruction stream, is the remaining bound.
-template <int D, bool ANY_WARM, int WPB, bool GLDS, bool KEYS>
+template <int D, bool ANY_WARM, int WPB, int VAR, bool KEYS>
 __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
     const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
@@ -179,7 +260,9 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     uint32_t *__restrict__ o_err) {
     constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
     constexpr int V = DCP;                                          // op slots per lane
-    constexpr int LW = GLDS ? GldsLds<D>::WORDS : DCP * AGN_WAVE;
+    constexpr bool GLDS = VAR == ROWS_GLDS;
+    constexpr bool QUAD = VAR == ROWS_QUAD && D == 8;
+    constexpr int LW = GLDS ? GldsLds<D>::WORDS : QUAD ? 1 : DCP * AGN_WAVE;
     __shared__ uint64_t lds_all[WPB][LW];  // GLDS: chunk rows/effects/ids; then the ct stage
 
     const int lane = lane_id();
@@ -213,7 +296,30 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
     int64_t hid = -1;
-    if constexpr (GLDS && D % 2 == 0) {
+    uint64_t ctA = 0, ctB = 0;  // QUAD: LastOpCt of DCs 2p, 2p+1 (p = lane & 3)
+    if constexpr (QUAD) {
+        const int p = lane & 3;
+        const uint64_t rA = p == 0 ? r[0] : p == 1 ? r[2 % D] : p == 2 ? r[4 % D] : r[6 % D];
+        const uint64_t rB = p == 0 ? r[1 % D] : p == 1 ? r[3 % D] : p == 2 ? r[5 % D] : r[7 % D];
+        const uint64_t sA = p == 0 ? s[0] : p == 1 ? s[2 % D] : p == 2 ? s[4 % D] : s[6 % D];
+        const uint64_t sB = p == 0 ? s[1 % D] : p == 1 ? s[3 % D] : p == 2 ? s[5 % D] : s[7 % D];
+        ctA = sA;
+        ctB = sB;
+#define AGN_Q8(W, NT, ENT)                                                                     \
+    scan_key_q8<W, NT, ENT>(oc, eff, tx, txr, off, n, a.n_entries, rA, rB, sA, sB, ctA, ctB, sum, \
+                            cnt, first_excl, first_err)
+        const bool warm = ANY_WARM && !sct_ign;
+        if (!warm) {
+            if (a.qnt & 2u) AGN_Q8(false, true, true);
+            else if (a.qnt & 1u) AGN_Q8(false, true, false);
+            else AGN_Q8(false, false, false);
+        } else {
+            if (a.qnt & 2u) AGN_Q8(ANY_WARM, true, true);
+            else if (a.qnt & 1u) AGN_Q8(ANY_WARM, true, false);
+            else AGN_Q8(ANY_WARM, false, false);
+        }
+#undef AGN_Q8
+    } else if constexpr (GLDS && D % 2 == 0) {
         if (!ANY_WARM || sct_ign)
             hid = scan_key_glds<D, false>(oc, eff, op_id, tx, txr, off, n, a.n_entries, r, s, ct,
                                           sum, cnt, first_excl, first_err, lds_all[w]);
@@ -246,23 +352,39 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)base_value[i]) : 0;
 
     const int64_t total = wave_sum_dpp(sum);
-    // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots of
-    // one DC -> xor-shuffle across the 64/DCP lanes that share it
-    uint64_t(*stage)[AGN_WAVE] = reinterpret_cast<uint64_t(*)[AGN_WAVE]>(lds_all[w]);
-#pragma unroll
-    for (int j = 0; j < D; ++j) stage[j][lane] = ct[j];
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int c = lane % DCP, g = lane / DCP;
-    uint64_t m = 0;
-    if (c < D) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) m = umax64(m, stage[c][g * V + v]);
-    }
-#pragma unroll
-    for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
     const bool ct_ign = sct_ign && cnt == 0u;
-    if (g == 0 && c < D) o_lastct[i * D + (uint64_t)c] = ct_ign ? 0ull : m;
+    if constexpr (QUAD) {
+        // LastOpCt: the 16 lanes of each part fold by xor-shuffles; lanes 0..3
+        // write the row's 4 x 16 bytes
+#pragma unroll
+        for (int x = 4; x < AGN_WAVE; x <<= 1) {
+            ctA = umax64(ctA, shfl_xor_u64(ctA, x));
+            ctB = umax64(ctB, shfl_xor_u64(ctB, x));
+        }
+        if (lane < 4) {
+            u64x2 v;
+            v.x = ct_ign ? 0ull : ctA;
+            v.y = ct_ign ? 0ull : ctB;
+            reinterpret_cast<u64x2 *>(o_lastct + i * D)[lane] = v;
+        }
+    } else {
+        // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots
+        // of one DC -> xor-shuffle across the 64/DCP lanes that share it
+        uint64_t(*stage)[AGN_WAVE] = reinterpret_cast<uint64_t(*)[AGN_WAVE]>(lds_all[w]);
+#pragma unroll
+        for (int j = 0; j < D; ++j) stage[j][lane] = ct[j];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int c = lane % DCP, g = lane / DCP;
+        uint64_t m = 0;
+        if (c < D) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) m = umax64(m, stage[c][g * V + v]);
+        }
+#pragma unroll
+        for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
+        if (g == 0 && c < D) o_lastct[i * D + (uint64_t)c] = ct_ign ? 0ull : m;
+    }
     if (lane == 0) {
         // NewLastOp = id(oldest excluded) - 1, else get_first_id (:49-63)
         const int64_t hole = first_excl >= 0 ? hid - 1 : hid;
@@ -291,15 +413,24 @@ inline uint32_t pair_chunks() {
     return (v && v[0] == '0') ? 0u : 1u;
 }
 
-// LDS-DMA row path (even D: 16-byte aligned chunks).  Its speed is
-// box-dependent: on two MI355X boxes it beat the VGPR-load path by 7-10 %
-// (cfg2 7.29-7.55 vs 8.16-8.44 ms), on three others it lost by 6-14 %
-// (8.86-9.28 vs 7.95-8.39 ms), consistently across processes on one box
-// (profiles/r01/ab_counter_glds*.log).  So the choice is made per process and
-// device by agn_tune (timing both bit-identical variants on the caller's
-// batch); until then the VGPR path runs.  AGN_COUNTER_GLDS=0/1 forces it.
+// Row-load variant per device.  LDS-DMA rows (even D) are box-dependent: on
+// two MI355X boxes they beat the VGPR-load path by 7-10 % (cfg2 7.29-7.55 vs
+// 8.16-8.44 ms), on three others they lost by 6-14 % (8.86-9.28 vs 7.95-8.39
+// ms), consistently across processes on one box (profiles/r01/ab_counter_
+// glds*.log).  Quad rows (D = 8) beat VGPR rows by 4-6 % on the boxes
+// measured (cfg2 7.81 vs 8.24-8.30 ms, warm 8.35 vs 8.68 ms;
+// profiles/r02/ab_counter_quad*.log), so they are the untuned default for
+// D = 8 and VGPR rows for other D.  agn_tune times the bit-identical variants
+// on the caller's batch and keeps another one for the device only when it is
+// at least 3 % faster than that default.  AGN_COUNTER_VARIANT=0/1/2 (or the
+// older AGN_COUNTER_GLDS=0/1) forces the choice.
 constexpr int kMaxDev = 64;
-std::atomic<int> g_glds_choice[kMaxDev];  // 0: untuned / VGPR rows, 1: LDS-DMA rows
+// per device: 0 untuned (the default of the shape), else 1 + ROWS_VGPR /
+// ROWS_GLDS / ROWS_QUAD
+std::atomic<int> g_rows_choice[kMaxDev];
+
+template <int D>
+constexpr int default_variant() { return D == 8 ? ROWS_QUAD : ROWS_VGPR; }
 
 inline int cur_dev() {
     int d = 0;
@@ -307,26 +438,42 @@ inline int cur_dev() {
     return d >= 0 && d < kMaxDev ? d : 0;
 }
 
-inline bool counter_glds() {
-    const char *v = getenv("AGN_COUNTER_GLDS");
-    if (v && (v[0] == '0' || v[0] == '1')) return v[0] == '1';
-    return g_glds_choice[cur_dev()].load(std::memory_order_relaxed) == 1;
+inline int forced_variant() {
+    const char *v = getenv("AGN_COUNTER_VARIANT");
+    if (v && v[0] >= '0' && v[0] <= '2') return v[0] - '0';
+    v = getenv("AGN_COUNTER_GLDS");
+    if (v && (v[0] == '0' || v[0] == '1')) return v[0] - '0';
+    return -1;
 }
 
-template <int D, int WPB, bool GLDS, bool KEYS>
+inline int tuned_variant() {  // -1 = untuned
+    return g_rows_choice[cur_dev()].load(std::memory_order_relaxed) - 1;
+}
+
+template <int D>
+int counter_variant() {
+    const int f = forced_variant();
+    if (f >= 0) return f;
+    const int t = tuned_variant();
+    return t >= 0 ? t : default_variant<D>();
+}
+
+template <int D, int WPB, int VAR, bool KEYS>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, pair_chunks()};
+    const char *qv = getenv("AGN_COUNTER_QUAD_NT");
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, pair_chunks(),
+                (qv && qv[0] >= '0' && qv[0] <= '3') ? (uint32_t)(qv[0] - '0') : 1u};
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);
     if (req.sct)
-        hipLaunchKernelGGL((k_counter_key<D, true, WPB, GLDS, KEYS>), dim3((unsigned)nb),
+        hipLaunchKernelGGL((k_counter_key<D, true, WPB, VAR, KEYS>), dim3((unsigned)nb),
                            dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
                            log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
                            req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
                            out.hole, out.lastct, out.count, out.flags, out.err_pos);
     else
-        hipLaunchKernelGGL((k_counter_key<D, false, WPB, GLDS, KEYS>), dim3((unsigned)nb),
+        hipLaunchKernelGGL((k_counter_key<D, false, WPB, VAR, KEYS>), dim3((unsigned)nb),
                            dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
                            log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
                            req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
@@ -335,18 +482,32 @@ int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out,
     return AGN_OK;
 }
 
-template <int D, int WPB, bool GLDS>
+template <int D, int WPB, int VAR>
 int launch_key_g(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    return req.keys ? launch_key_k<D, WPB, GLDS, true>(log, req, out, st)
-                    : launch_key_k<D, WPB, GLDS, false>(log, req, out, st);
+    return req.keys ? launch_key_k<D, WPB, VAR, true>(log, req, out, st)
+                    : launch_key_k<D, WPB, VAR, false>(log, req, out, st);
+}
+
+// The variants this D has: VGPR rows always, LDS-DMA rows for even D, quad
+// rows for D = 8.
+template <int D>
+constexpr bool has_variant(int v) {
+    return v == ROWS_VGPR || (v == ROWS_GLDS && D % 2 == 0) || (v == ROWS_QUAD && D == 8);
+}
+
+template <int D, int WPB>
+int launch_var(int v, const agn_log &log, const agn_read &req, const agn_result &out,
+               hipStream_t st) {
+    if constexpr (D % 2 == 0)
+        if (v == ROWS_GLDS) return launch_key_g<D, WPB, ROWS_GLDS>(log, req, out, st);
+    if constexpr (D == 8)
+        if (v == ROWS_QUAD) return launch_key_g<D, WPB, ROWS_QUAD>(log, req, out, st);
+    return launch_key_g<D, WPB, ROWS_VGPR>(log, req, out, st);
 }
 
 template <int D, int WPB>
 int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    if constexpr (D % 2 == 0) {
-        if (counter_glds()) return launch_key_g<D, WPB, true>(log, req, out, st);
-    }
-    return launch_key_g<D, WPB, false>(log, req, out, st);
+    return launch_var<D, WPB>(counter_variant<D>(), log, req, out, st);
 }
 
 // Waves (= requests) per block: 1 measured 1.4-3.4 % faster than 2 and
@@ -394,11 +555,12 @@ int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st) {
     return AGN_OK;
 }
 
-// agn_tune for the dense counter path: alternate the VGPR-row and LDS-DMA-row
-// kernels over the caller's batch (`rounds` launches each, on `st`), keep each
-// variant's fastest launch, and select LDS-DMA for this device only when it
-// is at least 3 % faster (the VGPR path is the robust default).  Both write
-// the same results, so `out` holds the batch's results afterwards.
+// agn_tune for the dense counter path: alternate the row-load variants this
+// D has over the caller's batch (`rounds` launches each, on `st`), keep each
+// variant's fastest launch, and select another variant than the shape's
+// default for this device only when it is at least 3 % faster.  All write
+// the same results, so `out` holds the batch's results afterwards.  ms[v] =
+// fastest launch of variant v (0 when absent).
 template <int D>
 int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st,
                int rounds, int *choice, float *ms) {
@@ -408,14 +570,15 @@ int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, h
         (void)hipEventDestroy(e0);
         return fail(AGN_EHIP, "tune: hipEventCreate");
     }
-    float best[2] = {3.4e38f, 3.4e38f};
+    constexpr int NV = 3;
+    float best[NV] = {3.4e38f, 3.4e38f, 3.4e38f};
     int rc = AGN_OK;
     for (int r = 0; r < rounds && rc == AGN_OK; ++r) {
-        for (int v = 0; v < 2 && rc == AGN_OK; ++v) {
-            const int var = (r & 1) ? 1 - v : v;  // alternate which variant goes first
+        for (int k = 0; k < NV && rc == AGN_OK; ++k) {
+            const int var = (r & 1) ? NV - 1 - k : k;  // alternate which variant goes first
+            if (!has_variant<D>(var)) continue;
             if (hipEventRecord(e0, st) != hipSuccess) { rc = fail(AGN_EHIP, "tune: record"); break; }
-            rc = var ? launch_key_g<D, 1, true>(log, req, out, st)
-                     : launch_key_g<D, 1, false>(log, req, out, st);
+            rc = launch_var<D, 1>(var, log, req, out, st);
             if (rc) break;
             float t = 0.f;
             if (hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
@@ -429,13 +592,14 @@ int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, h
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (rc) return rc;
-    const int c = best[1] < 0.97f * best[0] ? 1 : 0;
-    g_glds_choice[cur_dev()].store(c, std::memory_order_relaxed);
+    const int d0 = default_variant<D>();
+    int c = d0;
+    for (int v = 0; v < NV; ++v)
+        if (v != d0 && has_variant<D>(v) && best[v] < 0.97f * best[d0] && best[v] < best[c]) c = v;
+    g_rows_choice[cur_dev()].store(c + 1, std::memory_order_relaxed);
     *choice = c;
-    if (ms) {
-        ms[0] = best[0];
-        ms[1] = best[1];
-    }
+    if (ms)
+        for (int v = 0; v < NV; ++v) ms[v] = has_variant<D>(v) ? best[v] : 0.f;
     return AGN_OK;
 }
 

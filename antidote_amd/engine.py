@@ -219,16 +219,17 @@ class Engine:
     def tune(self, dlog, dreq, dres, stream=None, rounds=3):
         """agn_tune: time the bit-identical kernel variants of this batch's
         path, select the fastest for this device; returns (choice, ms) with
-        choice -1 (nothing to tune), 0 (VGPR rows) or 1 (LDS-DMA rows) and
-        ms = fastest launch per variant.  Blocks; dres holds the results."""
+        choice -1 (nothing to tune), 0 (VGPR rows), 1 (LDS-DMA rows) or 2
+        (quad rows, D = 8) and ms = fastest launch per variant (0 where the
+        shape lacks it).  Blocks; dres holds the results."""
         ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
         rs = dreq.struct if isinstance(dreq, DeviceArrays) else dreq
         os_ = dres.struct if isinstance(dres, DeviceArrays) else dres
         choice = C.c_int(-1)
-        ms = (C.c_float * 2)()
+        ms = (C.c_float * 3)()
         check(self.lib.agn_tune(self.ctx, C.byref(ls), C.byref(rs), C.byref(os_), stream,
                                 int(rounds), C.byref(choice), ms), "agn_tune")
-        return choice.value, (ms[0], ms[1])
+        return choice.value, (ms[0], ms[1], ms[2])
 
     # ---------------------------------------------------------------- generator
     def gen_dev(self, cfg: _abi.AgnGenCfg, stream=None):

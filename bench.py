@@ -270,12 +270,15 @@ def main():
     if a.tune_rounds > 0:
         choice, tms = eng.tune(dl, dr, res, stream=sp, rounds=a.tune_rounds)
         if choice >= 0:
-            forced = os.environ.get("AGN_COUNTER_GLDS", "")[:1]
-            if forced in ("0", "1"):       # the environment overrides the selection
+            names = ["vgpr_rows", "lds_dma_rows", "quad_rows"]
+            forced = os.environ.get("AGN_COUNTER_VARIANT", "")[:1]
+            if forced not in ("0", "1", "2"):
+                forced = os.environ.get("AGN_COUNTER_GLDS", "")[:1]
+            if forced in ("0", "1", "2"):  # the environment overrides the selection
                 choice = int(forced)
-            tune = {"selected": ["vgpr_rows", "lds_dma_rows"][choice],
-                    "forced_by_env": forced in ("0", "1"),
-                    "best_ms": {"vgpr_rows": tms[0], "lds_dma_rows": tms[1]},
+            tune = {"selected": names[choice],
+                    "forced_by_env": forced in ("0", "1", "2"),
+                    "best_ms": {n: t for n, t in zip(names, tms) if t > 0},
                     "rounds": a.tune_rounds}
     torch.cuda.synchronize()
     barrier()

@@ -192,13 +192,15 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req,
  * variant its shape has, `rounds` launches per variant alternated on
  * `stream`, and selects the fastest for later agn_materialize calls of the
  * same path.  Today that is the dense counter_pn path with even D: VGPR row
- * loads vs non-temporal LDS-DMA rows, whose order differs between MI355X
- * boxes; the environment variable AGN_COUNTER_GLDS=0/1
+ * loads vs non-temporal LDS-DMA rows (and, for D = 8, lane-contiguous "quad"
+ * rows), whose order differs between MI355X boxes; the
+ * environment variable AGN_COUNTER_VARIANT=0/1/2 (or AGN_COUNTER_GLDS=0/1)
  * overrides the selection.  Blocks until done; `out` then holds the batch's
  * results.  *choice: -1 = nothing to tune (the batch ran once), 0 = VGPR
- * rows, 1 = LDS-DMA rows; ms (may be NULL) receives the fastest launch of
- * each variant in milliseconds ([2]).  Not part of the reference's API: an
- * engine-setup call, e.g. on the first batch of a partition. */
+ * rows, 1 = LDS-DMA rows, 2 = quad rows; ms (may be NULL) receives the
+ * fastest launch of each variant in milliseconds ([3], 0 for a variant the
+ * shape lacks).  Not part of the reference's API: an engine-setup call
+ * (INTEGRATION.md), e.g. on the first batch of a partition. */
 int agn_tune(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *out,
              void *stream, int rounds, int *choice, float *ms);
 

@@ -17,7 +17,8 @@ scratch = torch.zeros(8, dtype=torch.int64, device="cuda")
 sp = torch.cuda.current_stream().cuda_stream
 names = {0: "gridstride 4x16B", 1: "one-shot wave 4KiB", 2: "one-shot wave 4KiB nt",
          3: "glds 4KiB", 4: "glds 4KiB aux=2", 5: "gridstride nt", 6: "glds 4KiB wpb4",
-         7: "one-shot wpb4", 8: "glds aux=1", 9: "glds aux=3", 10: "glds 4-byte nt"}
+         7: "one-shot wpb4", 8: "glds aux=1", 9: "glds aux=3", 10: "glds 4-byte nt",
+         11: "wpb1 contiguous", 12: "wpb1 contiguous nt", 13: "wpb1 rows", 14: "wpb1 rows nt"}
 V = [int(x) for x in sys.argv[1:]] or sorted(names)
 t = {v: [] for v in V}
 for rnd in range(int(os.environ.get("AGN_PROBE_ROUNDS", "8"))):

@@ -71,7 +71,7 @@ def test_kat_system_txn_gpu(eng, oracle_lib, c):
 # ------------------------------------------------------------------ randomised differential
 # counter_pn runs through every counter kernel: the dense fast path (auto),
 # its opt-in LDS-DMA row path (glds, even D only) and the general kernel
-COUNTER_IMPLS = ("auto", "glds", "general")
+COUNTER_IMPLS = ("auto", "glds", "quad", "general")
 DIFF = []
 for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
     for D in (1, 2, 3, 5, 8, 12, 16, 17, 33, 64, 100, 256):
@@ -83,12 +83,13 @@ for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
 
 def _set_impl(monkeypatch, impl):
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
-    # "auto" = the VGPR-row dense kernel whatever agn_tune selected in this process
-    monkeypatch.setenv("AGN_COUNTER_GLDS", "0")
+    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    # "auto" = the VGPR-row dense kernel whatever agn_tune selected in this
+    # process; "glds" / "quad" = the LDS-DMA / quad-row variants where the
+    # shape has them (even D / D = 8), else VGPR rows
+    monkeypatch.setenv("AGN_COUNTER_VARIANT", {"glds": "1", "quad": "2"}.get(impl, "0"))
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
-    elif impl == "glds":
-        monkeypatch.setenv("AGN_COUNTER_GLDS", "1")
 
 
 @pytest.fixture(params=COUNTER_IMPLS)
@@ -169,6 +170,7 @@ def test_tune_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sparse):
     batch's results in `out` (bit-exact vs the oracle) and its selection then
     drives agn_materialize (results unchanged)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    monkeypatch.delenv("AGN_COUNTER_VARIANT", raising=False)
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
     log, req, cap = random_case(4243 + 7 * D + crdt, crdt, 400, D, 150, sparse=sparse, warm=0.4,
                                 txid=0.3, invalid=0.02, corrupt=0.03, base=0.4,
@@ -182,9 +184,9 @@ def test_tune_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sparse):
     res = eng.alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)
     choice, ms = eng.tune(dl, dr, res, rounds=2)
     tunable = crdt == _abi.COUNTER_PN and D % 2 == 0 and not sparse
-    assert choice in ((0, 1) if tunable else (-1,))
+    assert choice in ((0, 1, 2) if tunable else (-1,))
     if tunable:
-        assert ms[0] > 0 and ms[1] > 0
+        assert ms[0] > 0 and ms[1] > 0 and (ms[2] > 0) == (D == 8)
     bad = compare(crdt, D, eng.fetch_result(res), res_o, sparse, req.n_req)
     assert not bad, bad[:10]
     res2 = eng.alloc_result(req.n_req, D, sparse=sparse, cap_off=cap)

@@ -90,6 +90,28 @@ __global__ __launch_bounds__(128) void k_glds4(const uint32_t *__restrict__ p, u
     if (acc == 0x9E3779B97F4A7C15ull) out[0] = acc;
 }
 
+// v11/v12: one-shot waves, 4 KiB each, lane-CONTIGUOUS 16-byte loads (load j
+// covers bytes [1 KiB j, 1 KiB (j+1)) of the chunk: every instruction reads
+// 8 whole 128-byte lines), default / non-temporal policy; one wave per block
+// like the counter kernel.  v13: the counter kernel's row-per-lane pattern
+// (lane l reads the 64-byte row l: every instruction touches 32 lines,
+// 32 bytes of each), one wave per block.
+template <bool NT, bool ROWS>
+__global__ __launch_bounds__(64) void k_chunk1(const u64x2 *__restrict__ p, uint64_t n,
+                                              uint64_t *__restrict__ out) {
+    const uint64_t w = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (w * 256 + 255 >= n) return;
+    u64x2 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u64x2 *a = p + w * 256 + (ROWS ? (uint64_t)lane * 4 + j : (uint64_t)j * 64 + lane);
+        x[j] = NT ? __builtin_nontemporal_load(a) : *a;
+    }
+    const uint64_t acc = x[0].x ^ x[0].y ^ x[1].x ^ x[1].y ^ x[2].x ^ x[2].y ^ x[3].x ^ x[3].y;
+    if (acc == 0x9E3779B97F4A7C15ull) out[0] = acc;
+}
+
 // v5: grid-stride with non-temporal loads
 __global__ __launch_bounds__(256) void k_gs_nt(const u64x2 *__restrict__ p, uint64_t n,
                                               uint64_t *__restrict__ out) {
@@ -126,6 +148,10 @@ extern "C" int agn_probe_variant(int v, const void *buf, uint64_t bytes, void *s
         case 8: hipLaunchKernelGGL((k_glds<1, 2>), dim3(nw / 2), dim3(128), 0, s, p, n, o); break;
         case 9: hipLaunchKernelGGL((k_glds<3, 2>), dim3(nw / 2), dim3(128), 0, s, p, n, o); break;
         case 10: hipLaunchKernelGGL(k_glds4, dim3(nw / 2), dim3(128), 0, s, (const uint32_t *)buf, n, o); break;
+        case 11: hipLaunchKernelGGL((k_chunk1<false, false>), dim3(nw), dim3(64), 0, s, p, n, o); break;
+        case 12: hipLaunchKernelGGL((k_chunk1<true, false>), dim3(nw), dim3(64), 0, s, p, n, o); break;
+        case 13: hipLaunchKernelGGL((k_chunk1<false, true>), dim3(nw), dim3(64), 0, s, p, n, o); break;
+        case 14: hipLaunchKernelGGL((k_chunk1<true, true>), dim3(nw), dim3(64), 0, s, p, n, o); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
