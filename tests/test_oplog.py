@@ -290,7 +290,7 @@ def pruned_log(want, n_out, crdt, D, K, sparse):
 
 @pytest.mark.parametrize("crdt,D,sparse", [(_abi.COUNTER_PN, 8, False), (_abi.SET_AW, 5, False),
                                            (_abi.SET_AW, 16, True), (_abi.REGISTER_MV, 64, False)])
-def test_oplog_prefix_gc_cycles(eng, oracle_lib, monkeypatch, crdt, D, sparse):
+def test_oplog_prefix_gc_cycles(eng, oracle_lib, anchor, crdt, D, sparse):
     """The common GC shape: clocks grow along each key's log, so a prune drops
     (mostly) a prefix and the tail-anchored kernel leaves the kept entries in
     place and advances the key's live range.  Six rounds of append -> prune
@@ -298,7 +298,6 @@ def test_oplog_prefix_gc_cycles(eng, oracle_lib, monkeypatch, crdt, D, sparse):
     segments, flags, id index and reads against the oracle, so live ranges
     advance, run into their segment ends, move, restart after an all-pruned
     GC, and the arenas are re-laid out."""
-    monkeypatch.setenv("AGN_PRUNE_TAIL", "1")
     rng = np.random.default_rng(D * 31 + crdt)
     K, W, tags = 48, (D + 63) // 64, crdt != _abi.COUNTER_PN
     expect = None

@@ -153,7 +153,8 @@ def test_prune_gpu_vs_oracle(eng, oracle_lib, crdt, D, sparse):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("crdt,D,sparse", CASES + [(_abi.COUNTER_PN, 256, True),
-                                                   (_abi.SET_AW, 100, False)])
+                                                   (_abi.SET_AW, 100, False),
+                                                   (_abi.COUNTER_PN, 8, False)])
 def test_prune_segmented_gpu_vs_oracle(eng, oracle_lib, crdt, D, sparse):
     """agn_prune_ops with out.key_len: the one-pass segmented form -- every
     key's kept entries at its input segment start, bit-exact with the
