@@ -181,12 +181,37 @@ __device__ __forceinline__ Side load_side(const agn_log &log, uint64_t off, uint
     return s;
 }
 
+// Bit g of the result = some bit of group g (P consecutive bits) of the wave
+// ballot b, on the scalar unit: the per-op verdict of a ballot whose P lanes
+// per op hold its P 16-byte parts.
+template <int P>
+__device__ __forceinline__ uint64_t group_any(uint64_t b) {
+#pragma unroll
+    for (int sh = 1; sh < P; sh <<= 1) b |= b >> sh;
+    uint64_t m = 0;
+#pragma unroll
+    for (int g = 0; g < AGN_WAVE / P; ++g) m |= ((b >> (g * P)) & 1ull) << g;
+    return m;
+}
+
+__device__ __forceinline__ uint64_t low_bits(uint64_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
+
+// CT ("contiguous rows", dense clocks with D = 4 LPO): a sub-iteration's OPI
+// OpSSCommit rows (2 KiB) are read by two lane-contiguous 16-byte loads, 1 KiB
+// each, non-temporal -- every instruction covers whole 128-byte lines, where
+// the LPO-lanes-by-4-DCs loads cover half of each line per instruction.  Lane
+// l holds DCs 2 (l % P), 2 (l % P) + 1 (P = D / 2 parts per op) of op l / P
+// of each half; the per-op verdicts are group-any folds of wave ballots
+// (scalar), LastOpCt stays per part until the end of the key.
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, int CAP, int WPB, int RB,
-          bool WARM, bool SLOW>
+          bool WARM, bool SLOW, bool CT>
 __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, agn_result out,
                                                    uint32_t *wl, uint32_t *wl_n, uint32_t xcd) {
     using S = Shape<DPL, LPO>;
     constexpr int OPI = S::OPI;
+    static_assert(!CT || (DPL == 4 && FULL && !SPARSE), "CT: dense rows, 4 DCs per lane");
+    constexpr int P = CT ? DPL * LPO / 2 : 1;  // 16-byte parts per op
+    constexpr int OPH = AGN_WAVE / P;          // ops per 1 KiB load (OPI / 2)
     __shared__ CandLds<CAP> Lall[WPB];
     const int w = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
     CandLds<CAP> &L = Lall[w];
@@ -229,6 +254,19 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         }
         const uint64_t txr = req.txid ? uniform_u64(req.txid[i]) : 0ull;
         const bool use_tx = txr != 0ull && log.txid != nullptr;
+        // CT: this lane's parts of R / SCT / LastOpCt (DCs dp, dp + 1)
+        uint64_t rA = 0, rB = 0, sA = 0, sB = 0, ctA = 0, ctB = 0;
+        if constexpr (CT) {
+            const uint32_t dp = 2u * (uint32_t)(lane % P);
+            rA = req.R[i * D + dp];
+            rB = req.R[i * D + dp + 1];
+            if (!sct_ign) {
+                sA = req.sct[i * D + dp];
+                sB = req.sct[i * D + dp + 1];
+            }
+            ctA = sA;
+            ctB = sB;
+        }
 
         // ---- base snapshot state: candidates with ord = index (< B)
         heads_clear<CAP>(L);
@@ -254,8 +292,18 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         if (n != 0) {
             Side side = load_side(log, off, n, 0);
             uint64_t nx[DPL];
-            uint32_t nxbits;
-            {
+            uint32_t nxbits = 0;
+            u64x2 cx0, cx1;  // CT: the next sub-iteration's two 1 KiB halves
+            const u64x2 *rows16 = reinterpret_cast<const u64x2 *>(log.oc);
+            const uint64_t ue = (off + n) * (uint64_t)P - 1u;  // the key's last 16-byte unit
+            auto load_ct = [&](uint64_t sb) {
+                const uint64_t u = (off + sb) * (uint64_t)P + (uint64_t)lane;
+                cx0 = __builtin_nontemporal_load(rows16 + (u < ue ? u : ue));
+                cx1 = __builtin_nontemporal_load(rows16 + (u + AGN_WAVE < ue ? u + AGN_WAVE : ue));
+            };
+            if constexpr (CT) {
+                load_ct(0);
+            } else {
                 const uint64_t p = (uint64_t)slot < n ? (uint64_t)slot : n - 1;
                 load_rows<DPL, SPARSE, FULL>(log, off + p, d0, D, W, nx, nxbits);
             }
@@ -280,7 +328,44 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 // ---- snapshot filter over the chunk's sub-iterations
                 const uint32_t nsub = (nvalid + OPI - 1) / OPI;
                 bool incl_e = false;
-                for (uint32_t j = 0; j < nsub; ++j) {
+                for (uint32_t j = 0; j < nsub && CT; ++j) {
+                    const u64x2 o0 = cx0, o1 = cx1;
+                    const uint64_t b = c0 + (uint64_t)j * OPI;
+                    const uint64_t nb = (j + 1 < nsub) ? b + OPI : c0 + AGN_WAVE;
+                    if (j + 1 == nsub) side = load_side(log, off, n, nb < n ? nb : c0);
+                    load_ct(nb < n ? nb : n - 1);
+                    const uint64_t vm = low_bits(n - b < (uint64_t)OPI ? n - b : (uint64_t)OPI);
+                    const uint64_t bad = group_any<P>(ballot(o0.x > rA || o0.y > rB)) |
+                                         (group_any<P>(ballot(o1.x > rA || o1.y > rB)) << OPH);
+                    uint64_t nipm = ~0ull;  // belongs_to_snapshot_op(SCT, ...)
+                    if (WARM && !sct_ign)
+                        nipm = group_any<P>(ballot(o0.x > sA || o0.y > sB)) |
+                               (group_any<P>(ballot(o1.x > sA || o1.y > sB)) << OPH);
+                    if (use_tx) {  // or (TxId == op.txid)  (:219-220)
+                        const bool tv = lane < OPI && b + (uint64_t)lane < n &&
+                                        log.txid[off + b + (uint64_t)lane] == txr;
+                        nipm |= ballot(tv);
+                    }
+                    const uint64_t inc = vm & nipm & ~bad, exc = vm & nipm & bad;
+                    if (first_excl < 0 && exc) {
+                        first_excl = (int64_t)b + (int64_t)__builtin_ctzll(exc);
+                        // its op id is in the chunk's side fields: no dependent load
+                        hid = (int64_t)(uint32_t)__shfl((int)cs.id, (int)(first_excl - (int64_t)c0));
+                    }
+                    const int q = lane / P;
+                    if ((inc >> q) & 1ull) {
+                        ctA = umax64(ctA, o0.x);
+                        ctB = umax64(ctB, o0.y);
+                    }
+                    if ((inc >> (q + OPH)) & 1ull) {
+                        ctA = umax64(ctA, o1.x);
+                        ctB = umax64(ctB, o1.y);
+                    }
+                    // per-op verdict -> lane = entry
+                    if ((uint32_t)lane / (uint32_t)OPI == j)
+                        incl_e = (inc >> ((uint32_t)lane % (uint32_t)OPI)) & 1ull;
+                }
+                for (uint32_t j = 0; j < nsub && !CT; ++j) {
                     uint64_t o[DPL];
                     const uint32_t obits0 = nxbits;
 #pragma unroll
@@ -439,12 +524,25 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         wave_sync();
 
         // ---- LastOpCt: max over the lanes that hold the same DC slice
+        const bool ct_ign = sct_ign && cnt == 0u;
+        if constexpr (CT) {
+#pragma unroll
+            for (int x = P; x < AGN_WAVE; x <<= 1) {
+                ctA = umax64(ctA, shfl_xor_u64(ctA, x));
+                ctB = umax64(ctB, shfl_xor_u64(ctB, x));
+            }
+            if (lane < P) {
+                u64x2 v;
+                v.x = ct_ign ? 0ull : ctA;
+                v.y = ct_ign ? 0ull : ctB;
+                reinterpret_cast<u64x2 *>(out.lastct + i * D)[lane] = v;
+            }
+        } else {
 #pragma unroll
         for (int x = LPO; x < AGN_WAVE; x <<= 1) {
 #pragma unroll
             for (int j = 0; j < DPL; ++j) ct[j] = umax64(ct[j], shfl_xor_u64(ct[j], x));
         }
-        const bool ct_ign = sct_ign && cnt == 0u;
         if (slot == 0) {
 #pragma unroll
             for (int j = 0; j < DPL; ++j) {
@@ -456,6 +554,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                     out.lastct[i * D + d] = v;
                 }
             }
+        }
         }
         if (SPARSE && out.lastct_mask != nullptr) {
             uint64_t part = 0;
@@ -494,7 +593,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 // profiles/r01/ab_tags_wpb_unbiased.log)
 constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 1, RBATCH = 2;
 
-template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM>
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM, bool CT>
 int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
     // worklist of keys whose live state overflows the fast table: [0] = count
@@ -510,14 +609,14 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
             grid_for(req.n_req, FAST_WPB, ge ? (unsigned)atoi(ge) : 0x7fffffffu);
         if (e == hipSuccess) {
             hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH,
-                                       WARM, false>),
+                                       WARM, false, CT>),
                                dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, wl + 1,
                                wl, xcd_remap() ? 1u : 0u);
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
             hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM,
-                                       true>),
+                                       true, CT>),
                                dim3(256), dim3(64), 0, st, log, req, out, wl + 1, wl, 0u);
             e = hipGetLastError();
         }
@@ -529,19 +628,31 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
     return rc;
 }
 
+// Contiguous row loads for dense clocks with 4 DCs per lane (k_tags CT);
+// AGN_TAGS_CT=0 (A/B knob) keeps the LPO-lanes-by-4-DCs loads.
+inline bool tags_ct() {
+    const char *v = getenv("AGN_TAGS_CT");
+    return !(v && v[0] == '0');
+}
+
 template <int DPL, int LPO, bool SPARSE, bool SET>
 int launch_full(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     const bool warm = req.sct != nullptr;
     // FULL: dense rows that split exactly into 16-byte loads
     const bool full = !SPARSE && (DPL % 2 == 0) && log.n_dcs == (uint32_t)(DPL * LPO);
+    if constexpr (!SPARSE && DPL == 4) {
+        if (full && tags_ct())
+            return warm ? launch_shape<DPL, LPO, false, true, SET, true, true>(log, req, out, st)
+                        : launch_shape<DPL, LPO, false, true, SET, false, true>(log, req, out, st);
+    }
     if constexpr (!SPARSE && DPL % 2 == 0) {
         if (full)
-            return warm ? launch_shape<DPL, LPO, false, true, SET, true>(log, req, out, st)
-                        : launch_shape<DPL, LPO, false, true, SET, false>(log, req, out, st);
+            return warm ? launch_shape<DPL, LPO, false, true, SET, true, false>(log, req, out, st)
+                        : launch_shape<DPL, LPO, false, true, SET, false, false>(log, req, out, st);
     }
     (void)full;
-    return warm ? launch_shape<DPL, LPO, SPARSE, false, SET, true>(log, req, out, st)
-                : launch_shape<DPL, LPO, SPARSE, false, SET, false>(log, req, out, st);
+    return warm ? launch_shape<DPL, LPO, SPARSE, false, SET, true, false>(log, req, out, st)
+                : launch_shape<DPL, LPO, SPARSE, false, SET, false, false>(log, req, out, st);
 }
 
 // Dense clocks wider than 8 DCs run 4 DCs per lane: 83 VGPRs (5 waves/SIMD)
