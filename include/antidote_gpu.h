@@ -229,7 +229,10 @@ int agn_state_capacity(const agn_log *host_log, const agn_read *host_req,
  * readers through agn_oplog_read / agn_batcher; the engine holds the device
  * log shared for the duration of each read kernel and exclusive while a
  * flush or prune moves segments.  A view returned by agn_oplog_flush is for
- * single-threaded use and is invalidated by the next flush or prune. */
+ * single-threaded use and is invalidated by the next flush or prune.  Slots
+ * are 32-bit: a log holds fewer than 2^32 entry slots (segments included;
+ * e.g. ~370 GB of 8-DC entries, beyond one MI355X) and token slots; past
+ * that, flush / prune return AGN_ENOTSUP. */
 #define AGN_OPS_THRESHOLD 50 /* src/materializer_vnode.erl:41 */
 #define AGN_RESIZE_THRESHOLD 5 /* :44 */
 typedef struct agn_oplog agn_oplog;
