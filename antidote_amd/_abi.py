@@ -145,6 +145,8 @@ PROTOTYPES = {
                                 P, P]),
     "agn_ss_store": (C.c_int, [P, C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P, P,
                                P, C.POINTER(AgnResult), P, P, P, P, P]),
+    "agn_read_cached": (C.c_int, [P, C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P,
+                                  P, P, C.POINTER(AgnResult), P, P, P, P]),
     "agn_prune_ops": (C.c_int, [P, C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P, P, P]),
     "agn_gst_scalar": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P]),
     "agn_oplog_create": (C.c_int, [P, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_uint32,

@@ -17,6 +17,7 @@
 
 #include "common.hpp"
 #include "gen.hpp"
+#include "serve.hpp"
 
 namespace agn {
 // host-staged materialize (agn_materialize_host): a non-blocking stream plus
@@ -650,6 +651,59 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
     if (rc) return rc;
     return launch_ss_store(*cache, log->key_off, log->key_len, n_req, keys, is_first, status, should_gc, *res,
                            handle, prune, threshold, threshold_mask, (hipStream_t)stream);
+}
+
+int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
+                    const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
+                    const uint8_t *should_gc, agn_result *out, uint8_t *status, uint8_t *prune,
+                    uint64_t *threshold, void *stream) {
+    int rc = check_cache(cache);
+    if (rc) return rc;
+    if (!log || !out || !log->key_off) return fail(AGN_EINVAL, "read_cached: null argument");
+    if (log->n_keys != cache->n_keys || log->n_dcs != cache->n_dcs)
+        return fail(AGN_EINVAL, "read_cached: log and cache disagree on keys / DCs");
+    if (!read6_supported(*log, log->n_dcs) || cache->clock_mask)
+        return fail(AGN_ENOTSUP, "read_cached: counter_pn with dense clocks, D <= 8");
+    if (n_req == 0) return AGN_OK;
+    if (!keys || !R || !status || !prune || !threshold || !out->value || !out->hole ||
+        !out->lastct || !out->count || !out->flags || !out->err_pos)
+        return fail(AGN_EINVAL, "read_cached: null argument");
+    rc = use_device(ctx);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    uint64_t *dkeys = nullptr;  // the kernel's copy of the batch's keys (read batcher's GC list)
+    AGN_HIP(pool_malloc((void **)&dkeys, n_req * sizeof(uint64_t), st));
+    Read6Args a;
+    a.key_off = log->key_off;
+    a.key_len = log->key_len;
+    a.key_id0 = log->key_id0;
+    a.key_type = log->key_type;
+    a.oc = log->oc;
+    a.op_id = log->op_id;
+    a.eff = log->eff;
+    a.log_txid = log->txid;
+    a.n_entries = log->n_entries;
+    a.n_dcs = log->n_dcs;
+    a.req_type = AGN_COUNTER_PN;
+    a.n_req = n_req;
+    a.keys = keys;
+    a.R = R;
+    a.txid = txid;
+    a.gc = should_gc;
+    a.value = out->value;
+    a.hole = out->hole;
+    a.lastct = out->lastct;
+    a.count = out->count;
+    a.flags = out->flags;
+    a.err_pos = out->err_pos;
+    a.status = status;
+    a.prune = prune;
+    a.dkeys = dkeys;
+    a.dprune = prune;
+    a.thr = threshold;
+    rc = launch_read6(*cache, a, st);
+    (void)hipFreeAsync(dkeys, st);
+    return rc;
 }
 
 int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,

@@ -157,6 +157,7 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b) {
         a.op_id = view.op_id;
         a.eff = view.eff;
         a.log_txid = view.txid;
+        a.n_entries = view.n_entries;
         a.n_dcs = D;
         a.req_type = B->crdt;
         a.n_req = n;

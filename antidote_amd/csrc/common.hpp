@@ -60,6 +60,21 @@ __device__ inline int64_t wave_sum_i64(int64_t v) {
 
 __device__ inline uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
+// Bit g of the result = some bit of group g (P consecutive bits) of the wave
+// ballot b, on the scalar unit: the per-op verdict of a ballot whose P lanes
+// per op hold its P 16-byte parts.
+template <int P>
+__device__ __forceinline__ uint64_t group_any(uint64_t b) {
+#pragma unroll
+    for (int sh = 1; sh < P; sh <<= 1) b |= b >> sh;
+    uint64_t m = 0;
+#pragma unroll
+    for (int g = 0; g < AGN_WAVE / P; ++g) m |= ((b >> (g * P)) & 1ull) << g;
+    return m;
+}
+
+__host__ __device__ inline uint64_t low_bits(uint64_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
+
 // Entries of key k: [key_off[k], key_off[k] + key_len[k]) or CSR.
 __host__ __device__ inline uint64_t key_n(const uint64_t *key_off, const uint64_t *key_len,
                                           uint64_t k) {

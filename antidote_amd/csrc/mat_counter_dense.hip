@@ -149,80 +149,6 @@ __device__ __forceinline__ int64_t scan_key_glds(
     return hid;
 }
 
-// Bit q of the result = some bit of nibble q of b (q = 0..15), on the scalar
-// unit: the per-op verdict of a ballot whose 4 lanes per op are its 4 parts.
-__device__ __forceinline__ uint64_t nib_any16(uint64_t b) {
-    b |= b >> 1;
-    b |= b >> 2;
-    b &= 0x1111111111111111ull;
-    b = (b | (b >> 3)) & 0x0303030303030303ull;
-    b = (b | (b >> 6)) & 0x000F000F000F000Full;
-    b = (b | (b >> 12)) & 0x000000FF000000FFull;
-    return (b | (b >> 24)) & 0xFFFFull;
-}
-
-// scan_key for D = 8 with lane-CONTIGUOUS row loads ("quad rows"): load j of a
-// 64-op chunk reads bytes [1 KiB j, 1 KiB (j+1)) of the chunk's rows, so
-// every instruction covers 8 whole 128-byte lines -- the row-per-lane loads
-// of scan_key touch 32 lines per instruction, 32 bytes of each, and request
-// every line four times.  Lane l holds DCs 2p, 2p+1 (p = l & 3) of op
-// 16 j + (l >> 2): the per-op verdicts are nibbles of wave ballots folded on
-// the scalar unit into 64-bit op masks (incl / excl), and the LastOpCt maxima
-// stay per part (ctA, ctB) until one xor-shuffle fold at the end of the key.
-// The effect (and TxId) loads stay lane = op.  Same results as scan_key.
-template <bool WARM, bool NT, bool EFF_NT = false>
-__device__ __forceinline__ void scan_key_q8(
-    const uint64_t *__restrict__ oc, const int64_t *__restrict__ eff,
-    const uint64_t *__restrict__ txid, uint64_t txr, uint64_t off, uint64_t n,
-    uint64_t n_entries, uint64_t rA, uint64_t rB, uint64_t sA, uint64_t sB, uint64_t &ctA,
-    uint64_t &ctB, int64_t &sum, uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
-    const int lane = lane_id();
-    const int q = lane >> 2;
-    const u64x2 *rows = reinterpret_cast<const u64x2 *>(oc);
-    const uint64_t lim = n_entries * 4u - 1u, lim_e = n_entries - 1u;
-    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
-        u64x2 x[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint64_t u = (off + b) * 4u + (uint64_t)(j * AGN_WAVE + lane);
-            u = u < lim ? u : lim;  // past the log's end: clamped, masked below
-            x[j] = ld<NT>(rows + u);
-        }
-        uint64_t e = off + b + (uint64_t)lane;
-        e = e < lim_e ? e : lim_e;
-        const int64_t ev = ld<NT && EFF_NT>(eff + e);
-        // every load of the chunk is in flight before the first verdict (left
-        // alone, the scheduler interleaves the ballots with the loads and
-        // waits for each row load in turn)
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t valid = (n - b >= (uint64_t)AGN_WAVE) ? ~0ull : ((1ull << (n - b)) - 1ull);
-        uint64_t bad = 0, gt = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            bad |= nib_any16(ballot(x[j].x > rA || x[j].y > rB)) << (16 * j);
-            if (WARM) gt |= nib_any16(ballot(x[j].x > sA || x[j].y > sB)) << (16 * j);
-        }
-        uint64_t nip = WARM ? gt : ~0ull;  // belongs_to_snapshot_op: not covered by SCT
-        if (txid != nullptr) nip |= ballot(txid[e] == txr);
-        const uint64_t incl = valid & nip & ~bad, excl = valid & nip & bad;
-        if (first_excl < 0 && excl) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(excl);
-        cnt += (uint32_t)__builtin_popcountll(incl);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool in = ((incl >> (16 * j + q)) & 1ull) != 0ull;
-            ctA = (in && x[j].x > ctA) ? x[j].x : ctA;
-            ctB = (in && x[j].y > ctB) ? x[j].y : ctB;
-        }
-        const bool mine = ((incl >> lane) & 1ull) != 0ull;
-        const bool badv = mine && ev == AGN_EFFECT_INVALID;
-        if (first_err < 0) {
-            const uint64_t be = ballot(badv);
-            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
-        }
-        sum += (mine && !badv) ? ev : 0;
-    }
-}
-
 // Row-load variants of k_counter_key (bit-identical results; agn_tune picks
 // per device): VGPR rows (scan_key), LDS-DMA rows (scan_key_glds, even D),
 // quad rows (scan_key_q8, D = 8, non-temporal).

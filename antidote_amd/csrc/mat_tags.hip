@@ -181,20 +181,6 @@ __device__ __forceinline__ Side load_side(const agn_log &log, uint64_t off, uint
     return s;
 }
 
-// Bit g of the result = some bit of group g (P consecutive bits) of the wave
-// ballot b, on the scalar unit: the per-op verdict of a ballot whose P lanes
-// per op hold its P 16-byte parts.
-template <int P>
-__device__ __forceinline__ uint64_t group_any(uint64_t b) {
-#pragma unroll
-    for (int sh = 1; sh < P; sh <<= 1) b |= b >> sh;
-    uint64_t m = 0;
-#pragma unroll
-    for (int g = 0; g < AGN_WAVE / P; ++g) m |= ((b >> (g * P)) & 1ull) << g;
-    return m;
-}
-
-__device__ __forceinline__ uint64_t low_bits(uint64_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
 
 // CT ("contiguous rows", dense clocks with D = 4 LPO): a sub-iteration's OPI
 // OpSSCommit rows (2 KiB) are read by two lane-contiguous 16-byte loads, 1 KiB

@@ -10,47 +10,142 @@
 //      snapshot_insert_gc (:341-364, 466-563) on the group, LastOpCt from LDS.
 // The three steps are the batched kernels k_ss_lookup -> k_counter_key ->
 // k_ss_store run back to back per request, so a batch costs one launch
-// instead of three kernels and two copies: requests are read from, and
-// results written to, device-visible pinned host memory.
-#include "cache_dev.hpp"
+// instead of three kernels and two copies: for the read batcher requests are
+// read from, and results written to, device-visible pinned host memory;
+// agn_read_cached runs it over device arrays.  D = 8 scans quad rows
+// (counter_scan.hpp scan_key_q8), as the batched counter kernel does.
 #include "counter_scan.hpp"
 #include "serve.hpp"
 
 namespace agn {
 namespace {
 
-template <int D, int G>
+// The key's cache slots in registers, lane l = slot (l / DCP) + SPR r of
+// register r, DC l % DCP: every slot the lookup compares and the store
+// shifts is read by one batch of loads, issued before the log scan, and
+// written back from the lane that read it -- the batched kernels' group loops
+// (cache_dev.hpp) walk the slots one dependent load at a time, which a wave
+// serving one request cannot hide.  A cache written by these entry points
+// holds at most SNAPSHOT_THRESHOLD - 1 entries per key; NSLOT bounds the
+// slots read.
+constexpr uint32_t NSLOT = 16;
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, AGN_WAVE);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, AGN_WAVE);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int D>
 __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
     constexpr int V = DCP;                                          // op slots per lane
-    static_assert(G == DCP, "group = the power of two >= D");
+    constexpr int SPR = AGN_WAVE / DCP;                             // cache slots per register
+    constexpr int NR = (int)((NSLOT + SPR - 1) / SPR);
     __shared__ uint64_t stage[DCP][AGN_WAVE];
-    __shared__ uint64_t sct_row[DCP], ct_row[DCP];
     const uint64_t i = blockIdx.x;
     if (i >= a.n_req) return;
     const int lane = lane_id();
+    const int dl = lane % DCP, jl = lane / DCP;  // this lane's DC and slot
     const uint64_t key = uniform_u64(a.keys[i]);
-
-    // 1. the base snapshot <= R
-    LookupOut lk{0, 0, 0, 0};
-    if (lane < G) {
-        const Grp<G> g;
-        lk = ss_lookup_one<G>(g, c, key, a.R + i * D, nullptr, sct_row, nullptr);
-    }
-    const bool sct_ign = __builtin_amdgcn_readfirstlane(lk.ign) != 0;
-    const uint32_t st = __builtin_amdgcn_readfirstlane(lk.status);
-    const uint32_t is_first = __builtin_amdgcn_readfirstlane(lk.first);
-    const int64_t base = (int64_t)uniform_u64((uint64_t)lk.base);
-    __syncthreads();  // sct_row
-
-    // 2. materialize/4 from the base (k_counter_key's body)
-    uint64_t r[D], s[D], ct[D];
+    const uint32_t S = c.slots;
+    const uint32_t n0 = __builtin_amdgcn_readfirstlane(c.n[key]);
+    uint64_t r[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) r[j] = uniform_u64(a.R[i * D + j]);
     const KeyMeta km = key_meta(key, a.key_off, a.key_len, a.key_id0);
     const uint64_t off = km.off, n = km.n;
-    if (n != 0 && a.key_type != nullptr && byte_of(a.key_type, key) != (a.req_type & 0xffu)) {
-        if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
+    // erlang:error(corrupted_ops_cache) (:190-191), read before any store
+    // (unconditional, from a dummy address when there is no type column: a
+    // conditional scalar load is waited for before the slot loads issue)
+    const uint32_t kty = byte_of(
+        a.key_type ? a.key_type : reinterpret_cast<const uint8_t *>(a.key_off), key);
+    const bool corrupt = n != 0 && a.key_type != nullptr && kty != (a.req_type & 0xffu);
+    const uint32_t nv = n0 < NSLOT ? n0 : NSLOT;
+
+    // the key's cache slots (rows past nv re-read slot 0: same lines, unused)
+    const int dc = dl < D ? dl : D - 1;
+    uint64_t clk[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        const uint32_t j = (uint32_t)(jl + q * SPR);
+        clk[q] = c.clock[(key * S + (j < nv ? j : 0u)) * D + (uint64_t)dc];
+    }
+    const uint32_t ls = (uint32_t)lane < nv ? (uint32_t)lane : 0u;
+    int64_t lop = c.last_op[key * S + ls], val = c.value[key * S + ls];
+    // D = 8: the log's first chunk is in flight with the slots.  Unconditional
+    // (an empty key reads its own slot 0 instead): a load under a branch makes
+    // the wait for the slots at the join wait for the chunk too.
+    Q8Chunk ch0;
+    if constexpr (D == 8) {
+        const bool has = n != 0;
+        ch0 = q8_load<true, false>(has ? a.oc : c.clock + key * S * D,
+                                   has ? a.eff : c.value + key * S, has ? off : 0ull, 0,
+                                   has ? a.n_entries : 1ull);
+    }
+
+    // 1. get_from_snapshot_cache: the first slot <= R (vector_orddict:get_smaller)
+    uint64_t rd = r[0];
+#pragma unroll
+    for (int j = 1; j < D; ++j) rd = dl == j ? r[j] : rd;
+    uint32_t st, is_first;
+    bool sct_ign;
+    int64_t base = 0;
+    uint64_t s[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) s[j] = 0ull;
+    uint32_t n1 = nv;  // the key's entries after the lookup
+    if (n0 == 0) {     // absent: store the empty snapshot at vectorclock:new() (:395-402)
+        if (lane < D) c.clock[(key * S) * D + (uint64_t)lane] = 0ull;
+        if (lane == 0) {
+            c.last_op[key * S] = 0;
+            c.value[key * S] = 0;
+            c.n[key] = 1;
+        }
+        clk[0] = jl == 0 ? 0ull : clk[0];
+        lop = lane == 0 ? 0 : lop;
+        val = lane == 0 ? 0 : val;
+        n1 = 1;
+        st = AGN_SS_NEW;
+        is_first = 1;
+        sct_ign = true;
+    } else {
+        uint64_t ok = 0;  // bit j: slot j <= R
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            const uint64_t gt = group_any<DCP>(ballot(dl < D && clk[q] > rd));
+            ok |= (~gt & low_bits(SPR)) << (q * SPR);
+        }
+        ok &= low_bits(nv);
+        if (ok) {
+            const int f = __builtin_ctzll(ok), q = f / SPR, l0 = (f % SPR) * DCP;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                uint64_t v = readlane_u64(clk[0], l0 + j);
+                if constexpr (NR > 1) v = q ? readlane_u64(clk[1], l0 + j) : v;
+                s[j] = v;
+            }
+            base = (int64_t)readlane_u64((uint64_t)val, f);
+            st = AGN_SS_HIT;
+            is_first = f == 0;
+            sct_ign = false;
+        } else {
+            st = AGN_SS_LOG;
+            is_first = 0;
+            sct_ign = true;
+        }
+    }
+
+    // 2. materialize/4 from the base (k_counter_key's body)
+    uint64_t ct[D];
+    if (corrupt) {
+        if (lane == 0) {
             a.value[i] = 0;
             a.hole[i] = 0;
             a.count[i] = 0;
@@ -65,18 +160,38 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         return;
     }
 #pragma unroll
-    for (int j = 0; j < D; ++j) {
-        s[j] = sct_ign ? 0ull : uniform_u64(sct_row[j]);
-        ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
-    }
+    for (int j = 0; j < D; ++j) ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
     const uint64_t txr = a.txid ? uniform_u64(a.txid[i]) : 0ull;
     const uint64_t *tx = (txr != 0ull) ? a.log_txid : nullptr;
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
-    if (sct_ign)
+    uint64_t ctA = 0, ctB = 0;  // D = 8: quad rows, LastOpCt of DCs 2p, 2p+1 (p = lane & 3)
+    if constexpr (D == 8) {
+        const int p = lane & 3;
+        const uint64_t rA = p == 0 ? r[0] : p == 1 ? r[2 % D] : p == 2 ? r[4 % D] : r[6 % D];
+        const uint64_t rB = p == 0 ? r[1 % D] : p == 1 ? r[3 % D] : p == 2 ? r[5 % D] : r[7 % D];
+        const uint64_t sA = p == 0 ? s[0] : p == 1 ? s[2 % D] : p == 2 ? s[4 % D] : s[6 % D];
+        const uint64_t sB = p == 0 ? s[1 % D] : p == 1 ? s[3 % D] : p == 2 ? s[5 % D] : s[7 % D];
+        ctA = sA;
+        ctB = sB;
+        if (n != 0) {
+#define AGN_R6Q(W)                                                                             \
+    q8_fold<W>(ch0, tx, txr, off, 0, n, a.n_entries, rA, rB, sA, sB, ctA, ctB, sum, cnt,       \
+               first_excl, first_err);                                                         \
+    scan_key_q8<W, true, false, true>(a.oc, a.eff, tx, txr, off, n, a.n_entries, rA, rB, sA, sB, \
+                                      ctA, ctB, sum, cnt, first_excl, first_err)
+            if (sct_ign) {
+                AGN_R6Q(false);
+            } else {
+                AGN_R6Q(true);
+            }
+#undef AGN_R6Q
+        }
+    } else if (sct_ign) {
         scan_key<D, false>(a.oc, a.eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl, first_err);
-    else
+    } else {
         scan_key<D, true>(a.oc, a.eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl, first_err);
+    }
     int64_t hid;
     {
         const uint64_t pos = first_excl >= 0 ? (uint64_t)first_excl : n - 1;
@@ -86,24 +201,39 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             hid = n ? (int64_t)a.op_id[uniform_u64(off + pos)] : 0;
     }
     const int64_t total = wave_sum_dpp(sum);
-    // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots of
-    // one DC -> xor-shuffle across the 64/DCP lanes that share it
-#pragma unroll
-    for (int j = 0; j < D; ++j) stage[j][lane] = ct[j];
-    __syncthreads();
-    const int cd = lane % DCP, grp = lane / DCP;
-    uint64_t m = 0;
-    if (cd < D) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) m = umax64(m, stage[cd][grp * V + v]);
-    }
-#pragma unroll
-    for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
     const bool ct_ign = sct_ign && cnt == 0u;
-    if (grp == 0 && cd < D) {
-        const uint64_t mv = ct_ign ? 0ull : m;
-        a.lastct[i * D + (uint64_t)cd] = mv;
-        ct_row[cd] = mv;
+    uint64_t ctl;  // LastOpCt of DC dl on every lane
+    if constexpr (D == 8) {
+        // the 16 lanes of each part fold by xor-shuffles; lanes 0..3 hold the row
+#pragma unroll
+        for (int x = 4; x < AGN_WAVE; x <<= 1) {
+            ctA = umax64(ctA, shfl_xor_u64(ctA, x));
+            ctB = umax64(ctB, shfl_xor_u64(ctB, x));
+        }
+        if (ct_ign) ctA = ctB = 0ull;
+        if (lane < 4) {
+            u64x2 v;
+            v.x = ctA;
+            v.y = ctB;
+            reinterpret_cast<u64x2 *>(a.lastct + i * D)[lane] = v;
+        }
+        const uint64_t xa = shfl_u64(ctA, dl >> 1), xb = shfl_u64(ctB, dl >> 1);
+        ctl = (dl & 1) ? xb : xa;
+    } else {
+        // LastOpCt: per-lane maxima -> LDS [DCP][64] -> each lane folds V slots
+        // of one DC -> xor-shuffle across the 64/DCP lanes that share it
+#pragma unroll
+        for (int j = 0; j < D; ++j) stage[j][lane] = ct[j];
+        __syncthreads();
+        uint64_t m = 0;
+        if (dl < D) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) m = umax64(m, stage[dl][jl * V + v]);
+        }
+#pragma unroll
+        for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
+        ctl = ct_ign ? 0ull : m;
+        if (jl == 0 && dl < D) a.lastct[i * D + (uint64_t)dl] = ctl;
     }
     // NewLastOp = id(oldest excluded) - 1, else get_first_id (:49-63)
     const int64_t hole = first_excl >= 0 ? hid - 1 : hid;
@@ -112,15 +242,54 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     if (ct_ign) fl |= AGN_F_CT_IGNORE;
     if (first_err >= 0) fl |= AGN_F_ERR_UNEXPECTED;
     const int64_t value = (int64_t)((uint64_t)base + (uint64_t)total);
-    __syncthreads();  // ct_row
 
-    // 3. internal_store_ss / snapshot_insert_gc's policy
+    // 3. internal_store_ss / insert_bigger / snapshot_insert_gc (cache_dev.hpp
+    //    ss_store_one on the register copy of the slots)
+    const bool gc = a.gc != nullptr && a.gc[i] != 0;
     bool pr = false;
-    if (lane < G) {
-        const Grp<G> g;
-        const bool gc = a.gc != nullptr && a.gc[i] != 0;
-        pr = ss_store_one<G>(g, c, key, n, (uint8_t)st, (uint8_t)is_first, gc, ct_row, nullptr,
-                             hole, value, cnt, fl, a.thr, nullptr);
+    const bool refresh = (fl & AGN_F_NEWSS) && is_first && cnt >= AGN_MIN_OP_STORE_SS;
+    const int64_t lop0 = (int64_t)readlane_u64((uint64_t)lop, 0);
+    if (st != AGN_SS_LOG && n != 0 && !(fl & (AGN_F_ERR_UNEXPECTED | AGN_F_CT_IGNORE)) &&
+        (refresh || gc) && (hole - lop0 >= AGN_MIN_OP_STORE_SS || gc)) {
+        // insert_bigger: prepend iff not le(LastOpCt, head clock)
+        const bool prepend = (ballot(jl == 0 && dl < D && ctl > clk[0]) & low_bits(DCP)) != 0ull;
+        const uint32_t size1 = n1 + (prepend ? 1u : 0u);
+        const bool collect = size1 >= AGN_SNAPSHOT_THRESHOLD || gc;
+        uint32_t kept = n1;
+        if (collect) kept = prepend ? (n1 < AGN_SNAPSHOT_MIN - 1 ? n1 : AGN_SNAPSHOT_MIN - 1)
+                                    : (n1 < AGN_SNAPSHOT_MIN ? n1 : AGN_SNAPSHOT_MIN);
+        const uint32_t new_n = kept + (prepend ? 1u : 0u);
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            const uint32_t j = (uint32_t)(jl + q * SPR);
+            if (j < kept) {
+                if (prepend && dl < D) c.clock[(key * S + j + 1) * D + (uint64_t)dl] = clk[q];
+                m = clk[q] < m ? clk[q] : m;
+            }
+        }
+        if (prepend) {
+            if ((uint32_t)lane < kept) {
+                c.last_op[key * S + (uint64_t)lane + 1] = lop;
+                c.value[key * S + (uint64_t)lane + 1] = val;
+            }
+            if (jl == 0 && dl < D) c.clock[(key * S) * D + (uint64_t)dl] = ctl;
+            if (lane == 0) {
+                c.last_op[key * S] = hole;
+                c.value[key * S] = value;
+            }
+            m = ctl < m ? ctl : m;
+        }
+        if (collect) {  // CommitTime = vectorclock:min of the kept clocks (:523-527)
+#pragma unroll
+            for (int x = DCP; x < AGN_WAVE; x <<= 1) {
+                const uint64_t o = shfl_xor_u64(m, x);
+                m = o < m ? o : m;
+            }
+            if (jl == 0 && dl < D) a.thr[key * D + (uint64_t)dl] = m;
+        }
+        if (lane == 0) c.n[key] = new_n;
+        pr = collect;
     }
     if (lane == 0) {
         a.value[i] = value;
@@ -146,14 +315,14 @@ int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     if (a.n_req > 0x7fffffffull) return fail(AGN_ENOTSUP, "read6: batch too large");
     const dim3 grid((unsigned)a.n_req), block(AGN_WAVE);
     switch (a.n_dcs) {
-        case 1: hipLaunchKernelGGL((k_read6<1, 1>), grid, block, 0, st, c, a); break;
-        case 2: hipLaunchKernelGGL((k_read6<2, 2>), grid, block, 0, st, c, a); break;
-        case 3: hipLaunchKernelGGL((k_read6<3, 4>), grid, block, 0, st, c, a); break;
-        case 4: hipLaunchKernelGGL((k_read6<4, 4>), grid, block, 0, st, c, a); break;
-        case 5: hipLaunchKernelGGL((k_read6<5, 8>), grid, block, 0, st, c, a); break;
-        case 6: hipLaunchKernelGGL((k_read6<6, 8>), grid, block, 0, st, c, a); break;
-        case 7: hipLaunchKernelGGL((k_read6<7, 8>), grid, block, 0, st, c, a); break;
-        case 8: hipLaunchKernelGGL((k_read6<8, 8>), grid, block, 0, st, c, a); break;
+        case 1: hipLaunchKernelGGL((k_read6<1>), grid, block, 0, st, c, a); break;
+        case 2: hipLaunchKernelGGL((k_read6<2>), grid, block, 0, st, c, a); break;
+        case 3: hipLaunchKernelGGL((k_read6<3>), grid, block, 0, st, c, a); break;
+        case 4: hipLaunchKernelGGL((k_read6<4>), grid, block, 0, st, c, a); break;
+        case 5: hipLaunchKernelGGL((k_read6<5>), grid, block, 0, st, c, a); break;
+        case 6: hipLaunchKernelGGL((k_read6<6>), grid, block, 0, st, c, a); break;
+        case 7: hipLaunchKernelGGL((k_read6<7>), grid, block, 0, st, c, a); break;
+        case 8: hipLaunchKernelGGL((k_read6<8>), grid, block, 0, st, c, a); break;
         default: return fail(AGN_ENOTSUP, "read6: n_dcs=%u", a.n_dcs);
     }
     AGN_HIP(hipGetLastError());

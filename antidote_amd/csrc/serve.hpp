@@ -47,6 +47,7 @@ struct Read6Args {
     const uint32_t *op_id;
     const int64_t *eff;
     const uint64_t *log_txid;
+    uint64_t n_entries;  // entry slots of the log (quad-row loads are clamped below)
     uint32_t n_dcs, req_type;
     // the batch (device-visible pinned host memory)
     uint64_t n_req;

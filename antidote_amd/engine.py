@@ -157,6 +157,16 @@ class Engine:
                                     first_ptr, status_ptr, gc_ptr, C.byref(rs), handle_ptr,
                                     prune_ptr, thr_ptr, thrm_ptr, stream), "agn_ss_store")
 
+    def read_cached(self, cache, dlog, n_req, keys_ptr, R_ptr, txid_ptr, gc_ptr, dres,
+                    status_ptr, prune_ptr, thr_ptr, stream=None):
+        """agn_read_cached: read/6 for a batch in one kernel (ss_lookup ->
+        materialize -> ss_store), counter_pn with dense clocks, D <= 8."""
+        ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
+        rs = dres.struct if isinstance(dres, DeviceArrays) else dres
+        check(self.lib.agn_read_cached(self.ctx, C.byref(cache), C.byref(ls), n_req, keys_ptr,
+                                       R_ptr, txid_ptr, gc_ptr, C.byref(rs), status_ptr,
+                                       prune_ptr, thr_ptr, stream), "agn_read_cached")
+
     def prune_ops(self, dlog: DeviceArrays, prune_ptr, thr_ptr, thr_mask_ptr, dout: DeviceArrays,
                   flags_ptr=None, totals_ptr=None, stream=None):
         """agn_prune_ops: materializer_vnode GC of the device op log (out of place)."""

@@ -472,6 +472,24 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
                  const uint8_t *should_gc, const agn_result *res, const int64_t *handle,
                  uint8_t *prune, uint64_t *threshold, uint64_t *threshold_mask, void *stream);
 
+/* materializer_vnode:read/6 for a batch (:96-102, 371-509) in ONE kernel:
+ * agn_ss_lookup -> agn_materialize from the cached base -> agn_ss_store, per
+ * request, for counter_pn logs with dense clocks (D <= 8; the read
+ * batcher's fused path over device arrays).  keys[n_req] (distinct, device),
+ * R[n_req][D], txid[n_req] (NULL: ignore), should_gc[n_req] (NULL: none);
+ * results in out (value, hole, lastct, count, flags, err_pos), status[n_req]
+ * (AGN_SS_*), prune[n_req] (per request, unlike agn_ss_store's per key) and
+ * threshold[n_keys][D].  Same results, cache contents and prune flags as the
+ * three calls; AGN_ENOTSUP for another type or shape.  One launch, the key's
+ * cache slots held in registers: 21 us for 10k keys (cfg1, D = 3) where the
+ * three calls take 35 us; a bulk batch is faster as the three calls (10M keys,
+ * cfg2: 11.6 vs 10.1 ms).  Reads at most 16 slots of a key (caches written by
+ * these entry points hold at most SNAPSHOT_THRESHOLD - 1). */
+int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
+                    const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
+                    const uint8_t *should_gc, agn_result *out, uint8_t *status, uint8_t *prune,
+                    uint64_t *threshold, void *stream);
+
 /* ---- log-read fallback and recovery ingest ------------------------------
  * A partition's logging_vnode disk log, decoded into records in log order
  * (#log_record{} -> #log_operation{tx_id, op_type, log_payload},

@@ -14,6 +14,7 @@ import pytest
 
 from antidote_amd import _abi
 from oracle import py_oracle as po
+from synth import random_case
 
 S = 10  # slots
 
@@ -272,3 +273,84 @@ def test_cache_gpu_vs_oracle(eng, oracle_lib, D, sparse, K):
         g = eng.download(dev[name], dt, shape)
         for k in np.nonzero(gn)[0][:5000]:
             assert np.array_equal(g[k, :gn[k]], want_a[name][k, :gn[k]]), (name, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [1, 3, 5, 8])
+def test_read_cached_vs_sequence(eng, D):
+    """agn_read_cached (read/6 in one kernel: lookup -> materialize from the
+    cached base -> store policy) equals agn_ss_lookup -> agn_materialize ->
+    agn_ss_store on two caches that start empty: every result field, the
+    lookup status, the prune flags (per request vs per key), the GC
+    thresholds and the cache contents, over rounds of batches on distinct
+    keys with GC reads mixed in (cold reads, hits, stores, prunes)."""
+    K = 3000
+    log, req, _ = random_case(501 + D, _abi.COUNTER_PN, K, D, 90, txid=0.2, empty=0.05)
+    rng = np.random.default_rng(D)
+    dlog = eng.upload_log(log)
+    dlog.struct.oc_mask = None
+
+    def cache():
+        bufs = {"n": eng.upload(np.zeros(K, np.uint32)),
+                "clock": eng.empty(8 * K * S * D), "last_op": eng.empty(8 * K * S),
+                "value": eng.empty(8 * K * S)}
+        c = _abi.AgnSsCache()
+        c.n_dcs, c.slots, c.n_keys = D, S, K
+        c.n, c.clock, c.last_op, c.value = (bufs[x].ptr for x in ("n", "clock", "last_op", "value"))
+        c.clock_mask = None
+        return c, bufs
+
+    ca, ba = cache()
+    cb, bb = cache()
+    for rnd in range(4):
+        nr = 1500 + 300 * rnd
+        keys = rng.permutation(K)[:nr].astype(np.uint64)
+        R = req.R[keys.astype(np.int64)] + rng.integers(0, 3, (nr, D)).astype(np.uint64)
+        tx = req.txid[keys.astype(np.int64)].copy()
+        gc = (rng.random(nr) < 0.2).astype(np.uint8)
+        dk, dR, dtx, dgc = (eng.upload(x) for x in (keys, np.ascontiguousarray(R), tx, gc))
+        # the sequence
+        o = {"sct": eng.empty(nr * D * 8), "ign": eng.empty(nr), "base": eng.empty(nr * 8),
+             "first": eng.empty(nr), "status": eng.empty(nr), "prune": eng.empty(K),
+             "thr": eng.empty(K * D * 8)}
+        eng.ss_lookup(ca, nr, dk.ptr, dR.ptr, None, o["sct"].ptr, None, o["ign"].ptr,
+                      o["base"].ptr, o["first"].ptr, o["status"].ptr)
+        rs = _abi.AgnRead()
+        rs.n_dcs, rs.req_type, rs.n_req = D, _abi.COUNTER_PN, nr
+        rs.keys, rs.R, rs.txid = dk.ptr, dR.ptr, dtx.ptr
+        rs.sct, rs.sct_ignore, rs.base_value = o["sct"].ptr, o["ign"].ptr, o["base"].ptr
+        res_a = eng.alloc_result(nr, D, sparse=False)
+        eng.materialize(dlog, rs, res_a)
+        eng.ss_store(ca, dlog, nr, dk.ptr, o["first"].ptr, o["status"].ptr, dgc.ptr, res_a, None,
+                     o["prune"].ptr, o["thr"].ptr, None)
+        # fused
+        res_b = eng.alloc_result(nr, D, sparse=False)
+        st_b, pr_b, thr_b = eng.empty(nr), eng.empty(nr), eng.empty(K * D * 8)
+        eng.read_cached(cb, dlog, nr, dk.ptr, dR.ptr, dtx.ptr, dgc.ptr, res_b, st_b.ptr, pr_b.ptr,
+                        thr_b.ptr)
+        eng.sync()
+        ga, gb = eng.fetch_result(res_a), eng.fetch_result(res_b)
+        for f in ("value", "hole", "lastct", "count", "flags", "err_pos"):
+            assert np.array_equal(getattr(ga, f), getattr(gb, f)), (rnd, f)
+        sa = eng.download(o["status"], np.uint8, (nr,))
+        assert np.array_equal(sa, eng.download(st_b, np.uint8, (nr,))), rnd
+        pa = eng.download(o["prune"], np.uint8, (K,))[keys.astype(np.int64)]
+        pb = eng.download(pr_b, np.uint8, (nr,))
+        assert np.array_equal(pa, pb), rnd
+        sel = keys[pa == 1].astype(np.int64)
+        assert np.array_equal(eng.download(o["thr"], np.uint64, (K, D))[sel],
+                              eng.download(thr_b, np.uint64, (K, D))[sel]), rnd
+        na = eng.download(ba["n"], np.uint32, (K,))
+        assert np.array_equal(na, eng.download(bb["n"], np.uint32, (K,))), rnd
+        for name, dt, shape in (("clock", np.uint64, (K, S, D)), ("last_op", np.int64, (K, S)),
+                                ("value", np.int64, (K, S))):
+            xa, xb = eng.download(ba[name], dt, shape), eng.download(bb[name], dt, shape)
+            for k in np.nonzero(na)[0]:
+                assert np.array_equal(xa[k, :na[k]], xb[k, :na[k]]), (rnd, name, k)
+        if rnd == 0:
+            assert (sa == _abi.SS_NEW).all()
+        else:
+            assert (sa == _abi.SS_HIT).any()
+        for b in list(o.values()) + [dk, dR, dtx, dgc, st_b, pr_b, thr_b] + \
+                list(res_a.bufs.values()) + list(res_b.bufs.values()):
+            b.free()
