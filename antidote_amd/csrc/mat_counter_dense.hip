@@ -193,7 +193,10 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
 
     const int lane = lane_id();
     const int w = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
-    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    // unconditional (as the side loads below): a conditional scalar load is
+    // waited for on its own
+    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t blk = a.xcd ? xb : blockIdx.x;
     const uint64_t i = uniform_u64((uint64_t)blk * WPB + (uint64_t)w);
     if (i >= a.n_req) return;
     uint64_t r[D], s[D], ct[D];
@@ -204,20 +207,33 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     const KeyMeta km = key_meta(key, key_off, key_len, key_id0);
     const uint64_t off = km.off, n = km.n;
     const uint32_t id0 = km.id0;  // consecutive-id base (agn_log_index_ids)
-    if (n != 0 && key_type != nullptr && byte_of(key_type, key) != (a.req_type & 0xffu)) {
+    // The side bytes and rows (key_type, sct_ignore, SCT, TxId) load
+    // unconditionally -- from an in-bounds dummy when the column is absent --
+    // so they share the metadata's round trip: a conditional scalar load is
+    // waited for on its own before the row loads issue.
+    const uint32_t kty =
+        byte_of(key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off), key);
+    const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
+    const uint32_t sib =
+        ANY_WARM ? byte_of(sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R), i) : 0u;
+    const uint64_t txv = uniform_u64((req_txid ? req_txid : R)[i]);
+    uint64_t sv[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
+    if (n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu)) {
         if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
             o_flags[i] = AGN_F_ERR_CORRUPTED;
             o_err[i] = 0xffffffffu;
         }
         return;
     }
-    const bool sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && byte_of(sct_ignore, i));
+    const bool sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        s[j] = sct_ign ? 0ull : uniform_u64(sct[i * D + j]);
+        s[j] = sct_ign ? 0ull : sv[j];
         ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
     }
-    const uint64_t txr = req_txid ? uniform_u64(req_txid[i]) : 0ull;
+    const uint64_t txr = req_txid ? txv : 0ull;
     const uint64_t *tx = (txr != 0ull) ? log_txid : nullptr;
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
