@@ -178,3 +178,45 @@ def test_descriptors_validate_without_gpu(lib):
             assert lib.agn_last_error() == b"null context", lib.agn_last_error()
             return 0
         run.run(fn)
+
+
+def test_read_cached_validates_without_gpu(lib):
+    """agn_read_cached's argument checks run before the device is touched:
+    counter_pn with dense clocks and D <= 8 only (ENOTSUP otherwise), the
+    cache and log must agree on keys and DCs, an empty batch is a no-op, and
+    a valid batch then needs the context."""
+    from synth import random_case
+    from antidote_amd.encode import log_struct
+
+    def case(crdt, D, sparse=False):
+        log, _req, _ = random_case(5, crdt, 12, D, 6, sparse=sparse)
+        ls = log_struct(log)
+        if log.oc_mask is None:
+            ls.oc_mask = None
+        c = _abi.AgnSsCache()
+        c.n_dcs, c.slots, c.n_keys = D, _abi.SNAPSHOT_THRESHOLD, 12
+        bufs = [np.zeros(12, np.uint32), np.zeros(12 * 10 * D, np.uint64),
+                np.zeros(12 * 10, np.int64), np.zeros(12 * 10, np.int64)]
+        c.n, c.clock, c.last_op, c.value = (b.ctypes.data for b in bufs)
+        res = alloc_result(4, D, sparse=False)
+        return ls, c, result_struct(res), (log, bufs, res)
+
+    keys = np.arange(4, dtype=np.uint64)
+    R = np.zeros((4, 8), np.uint64)
+    st, pr, thr = np.zeros(4, np.uint8), np.zeros(4, np.uint8), np.zeros(12 * 8, np.uint64)
+
+    def call(ls, c, os_, n=4):
+        return lib.agn_read_cached(None, C.byref(c) if c is not None else None, C.byref(ls), n,
+                                   keys.ctypes.data, R.ctypes.data, None, None, C.byref(os_),
+                                   st.ctypes.data, pr.ctypes.data, thr.ctypes.data, None)
+
+    ls, c, os_, keep = case(_abi.COUNTER_PN, 8)
+    assert call(ls, None, os_) == _abi.EINVAL
+    assert call(ls, c, os_, n=0) == _abi.OK
+    assert call(ls, c, os_) == _abi.EINVAL and lib.agn_last_error() == b"null context"
+    c.n_keys = 11
+    assert call(ls, c, os_) == _abi.EINVAL
+    for crdt, D, sparse in ((_abi.SET_AW, 4, False), (_abi.COUNTER_PN, 9, False),
+                            (_abi.COUNTER_PN, 4, True)):
+        ls, c, os_, keep = case(crdt, D, sparse)
+        assert call(ls, c, os_) == _abi.ENOTSUP, (crdt, D, sparse)
