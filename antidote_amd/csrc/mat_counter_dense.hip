@@ -152,7 +152,7 @@ __device__ __forceinline__ int64_t scan_key_glds(
 // Row-load variants of k_counter_key (bit-identical results; agn_tune picks
 // per device): VGPR rows (scan_key), LDS-DMA rows (scan_key_glds, even D),
 // quad rows (scan_key_q8, D = 8, non-temporal).
-enum { ROWS_VGPR = 0, ROWS_GLDS = 1, ROWS_QUAD = 2 };
+enum { ROWS_VGPR = 0, ROWS_GLDS = 1, ROWS_QUAD = 2, ROWS_QUAD2 = 3 };
 
 // One wave = one request, no loop: the grid is the batch (ceil(n_req / WPB)
 // blocks).  Measured on cfg2 this beats every software-pipelined variant
@@ -348,6 +348,210 @@ inline const uint32_t *id0_index(const agn_log &log) {
     return (v && v[0] == '0') ? nullptr : log.key_id0;
 }
 
+// ROWS_QUAD2 (D = 8): quad rows, TWO requests per wave with both keys'
+// first chunks in flight at once (9 KiB of rows per wave slot instead of 4.5).
+// Same results as k_counter_key.  The default for warm batches (the SCT
+// rows and flags lengthen each request's prologue, which the second key's
+// loads cover); cold batches measured no change (56 VGPRs, 8 waves).
+// AGN_COUNTER_VARIANT=3 forces it, =2 the one-request form.
+struct Q2Key {
+    uint64_t i, key, off, n, txr;
+    uint32_t id0;
+    bool corrupt, sct_ign;
+    uint64_t rA, rB, sA, sB;
+};
+
+template <bool ANY_WARM>
+__device__ __forceinline__ Q2Key q2_prologue(const DenseArgs &a, uint64_t i,
+                                             const uint64_t *__restrict__ keys,
+                                             const uint64_t *__restrict__ key_off,
+                                             const uint64_t *__restrict__ key_len,
+                                             const uint8_t *__restrict__ key_type,
+                                             const uint32_t *__restrict__ key_id0,
+                                             const uint64_t *__restrict__ R,
+                                             const uint64_t *__restrict__ sct,
+                                             const uint8_t *__restrict__ sct_ignore,
+                                             const uint64_t *__restrict__ req_txid) {
+    constexpr int D = 8;
+    Q2Key k;
+    k.i = i;
+    k.key = keys ? uniform_u64(keys[i]) : i;
+    const KeyMeta km = key_meta(k.key, key_off, key_len, key_id0);
+    k.off = km.off;
+    k.n = km.n;
+    k.id0 = km.id0;
+    const uint32_t kty =
+        byte_of(key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off), k.key);
+    k.corrupt = k.n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu);
+    const uint32_t sib =
+        ANY_WARM ? byte_of(sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R), i) : 0u;
+    k.sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
+    const uint64_t txv = uniform_u64((req_txid ? req_txid : R)[i]);
+    k.txr = req_txid ? txv : 0ull;
+    uint64_t r[D], sv[D];
+    const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        r[j] = uniform_u64(R[i * D + j]);
+        sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
+        sv[j] = k.sct_ign ? 0ull : sv[j];
+    }
+    const int p = lane_id() & 3;
+    k.rA = p == 0 ? r[0] : p == 1 ? r[2] : p == 2 ? r[4] : r[6];
+    k.rB = p == 0 ? r[1] : p == 1 ? r[3] : p == 2 ? r[5] : r[7];
+    k.sA = p == 0 ? sv[0] : p == 1 ? sv[2] : p == 2 ? sv[4] : sv[6];
+    k.sB = p == 0 ? sv[1] : p == 1 ? sv[3] : p == 2 ? sv[5] : sv[7];
+    return k;
+}
+
+struct Q2Acc {
+    int64_t sum = 0, first_excl = -1, first_err = -1;
+    uint32_t cnt = 0;
+    uint64_t ctA, ctB;
+};
+
+template <bool ANY_WARM>
+__device__ __forceinline__ void q2_fold(const Q2Key &k, const Q8Chunk &c, uint64_t b,
+                                        const uint64_t *__restrict__ log_txid, uint64_t n_entries,
+                                        Q2Acc &s) {
+    const uint64_t *tx = k.txr ? log_txid : nullptr;
+    if (ANY_WARM && !k.sct_ign)
+        q8_fold<true>(c, tx, k.txr, k.off, b, k.n, n_entries, k.rA, k.rB, k.sA, k.sB, s.ctA, s.ctB,
+                      s.sum, s.cnt, s.first_excl, s.first_err);
+    else
+        q8_fold<false>(c, tx, k.txr, k.off, b, k.n, n_entries, k.rA, k.rB, k.sA, k.sB, s.ctA,
+                       s.ctB, s.sum, s.cnt, s.first_excl, s.first_err);
+}
+
+template <bool ANY_WARM>
+__device__ __forceinline__ void q2_rest(const Q2Key &k, const uint64_t *__restrict__ oc,
+                                        const int64_t *__restrict__ eff,
+                                        const uint64_t *__restrict__ log_txid, uint64_t n_entries,
+                                        Q2Acc &s) {
+    if (k.n <= (uint64_t)AGN_WAVE) return;
+    const uint64_t *tx = k.txr ? log_txid : nullptr;
+    if (ANY_WARM && !k.sct_ign)
+        scan_key_q8<true, true, false, true>(oc, eff, tx, k.txr, k.off, k.n, n_entries, k.rA, k.rB,
+                                             k.sA, k.sB, s.ctA, s.ctB, s.sum, s.cnt, s.first_excl,
+                                             s.first_err);
+    else
+        scan_key_q8<false, true, false, true>(oc, eff, tx, k.txr, k.off, k.n, n_entries, k.rA,
+                                              k.rB, k.sA, k.sB, s.ctA, s.ctB, s.sum, s.cnt,
+                                              s.first_excl, s.first_err);
+}
+
+__device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
+                                            const uint32_t *__restrict__ op_id,
+                                            const int64_t *__restrict__ base_value,
+                                            int64_t *__restrict__ o_value,
+                                            int64_t *__restrict__ o_hole,
+                                            uint64_t *__restrict__ o_lastct,
+                                            uint32_t *__restrict__ o_count,
+                                            uint32_t *__restrict__ o_flags,
+                                            uint32_t *__restrict__ o_err) {
+    constexpr int D = 8;
+    const int lane = lane_id();
+    const uint64_t i = k.i;
+    if (k.corrupt) {
+        if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
+            o_flags[i] = AGN_F_ERR_CORRUPTED;
+            o_err[i] = 0xffffffffu;
+        }
+        return;
+    }
+    int64_t hid;
+    const uint64_t pos = s.first_excl >= 0 ? (uint64_t)s.first_excl : k.n - 1;
+    if (k.id0 != AGN_ID0_NONE)
+        hid = k.n ? (int64_t)((uint64_t)k.id0 + pos) : 0;
+    else
+        hid = k.n ? (int64_t)op_id[uniform_u64(k.off + pos)] : 0;
+    const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)base_value[i]) : 0;
+    const int64_t total = wave_sum_dpp(s.sum);
+    const bool ct_ign = k.sct_ign && s.cnt == 0u;
+#pragma unroll
+    for (int x = 4; x < AGN_WAVE; x <<= 1) {
+        s.ctA = umax64(s.ctA, shfl_xor_u64(s.ctA, x));
+        s.ctB = umax64(s.ctB, shfl_xor_u64(s.ctB, x));
+    }
+    if (lane < 4) {
+        u64x2 v;
+        v.x = ct_ign ? 0ull : s.ctA;
+        v.y = ct_ign ? 0ull : s.ctB;
+        reinterpret_cast<u64x2 *>(o_lastct + i * D)[lane] = v;
+    }
+    if (lane == 0) {
+        const int64_t hole = s.first_excl >= 0 ? hid - 1 : hid;
+        uint32_t fl = 0;
+        if (s.cnt) fl |= AGN_F_NEWSS;
+        if (ct_ign) fl |= AGN_F_CT_IGNORE;
+        if (s.first_err >= 0) fl |= AGN_F_ERR_UNEXPECTED;
+        o_value[i] = (int64_t)((uint64_t)base + (uint64_t)total);
+        o_hole[i] = hole;
+        o_count[i] = s.cnt;
+        o_flags[i] = fl;
+        o_err[i] = s.first_err >= 0 ? (uint32_t)(k.off + (uint64_t)s.first_err) : 0xffffffffu;
+    }
+}
+
+template <bool ANY_WARM>
+__global__ __launch_bounds__(64) void k_counter_quad2(
+    DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
+    const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
+    const uint32_t *__restrict__ key_id0, const uint64_t *__restrict__ oc,
+    const uint32_t *__restrict__ op_id, const int64_t *__restrict__ eff,
+    const uint64_t *__restrict__ log_txid, const uint64_t *__restrict__ R,
+    const uint64_t *__restrict__ sct, const uint8_t *__restrict__ sct_ignore,
+    const uint64_t *__restrict__ req_txid, const int64_t *__restrict__ base_value,
+    int64_t *__restrict__ o_value, int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
+    uint32_t *__restrict__ o_err) {
+    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint64_t i0 = uniform_u64((uint64_t)blk * 2u);
+    if (i0 >= a.n_req) return;
+    const bool two = i0 + 1u < a.n_req;
+    const uint64_t i1 = two ? i0 + 1u : i0;
+    const Q2Key k0 = q2_prologue<ANY_WARM>(a, i0, keys, key_off, key_len, key_type, key_id0, R,
+                                           sct, sct_ignore, req_txid);
+    const Q2Key k1 = q2_prologue<ANY_WARM>(a, i1, keys, key_off, key_len, key_type, key_id0, R,
+                                           sct, sct_ignore, req_txid);
+    Q2Acc s0, s1;
+    s0.ctA = k0.sA;
+    s0.ctB = k0.sB;
+    s1.ctA = k1.sA;
+    s1.ctB = k1.sB;
+    if (a.n_entries != 0) {
+        const Q8Chunk c0 = q8_load<true, false>(oc, eff, k0.off, 0, a.n_entries);
+        const Q8Chunk c1 = q8_load<true, false>(oc, eff, k1.off, 0, a.n_entries);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!k0.corrupt) q2_fold<ANY_WARM>(k0, c0, 0, log_txid, a.n_entries, s0);
+        if (!k1.corrupt) q2_fold<ANY_WARM>(k1, c1, 0, log_txid, a.n_entries, s1);
+        if (!k0.corrupt) q2_rest<ANY_WARM>(k0, oc, eff, log_txid, a.n_entries, s0);
+        if (!k1.corrupt) q2_rest<ANY_WARM>(k1, oc, eff, log_txid, a.n_entries, s1);
+    }
+    q2_epilogue(k0, s0, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err);
+    if (two)
+        q2_epilogue(k1, s1, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err);
+}
+
+int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u};
+    const uint64_t nb = (req.n_req + 1) / 2;
+    if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
+                                        (unsigned long long)req.n_req);
+#define AGN_Q2L(W)                                                                              \
+    hipLaunchKernelGGL((k_counter_quad2<W>), dim3((unsigned)nb), dim3(64), 0, st, a, req.keys, \
+                       log.key_off, log.key_len, log.key_type, id0_index(log), log.oc,         \
+                       log.op_id, log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid, \
+                       req.base_value, out.value, out.hole, out.lastct, out.count, out.flags,  \
+                       out.err_pos)
+    if (req.sct) AGN_Q2L(true);
+    else AGN_Q2L(false);
+#undef AGN_Q2L
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
 // Two chunks per step for D <= 4 (scan_key PAIR), unless AGN_COUNTER_PAIR=0
 // (A/B knob).
 inline uint32_t pair_chunks() {
@@ -382,7 +586,7 @@ inline int cur_dev() {
 
 inline int forced_variant() {
     const char *v = getenv("AGN_COUNTER_VARIANT");
-    if (v && v[0] >= '0' && v[0] <= '2') return v[0] - '0';
+    if (v && v[0] >= '0' && v[0] <= '3') return v[0] - '0';
     v = getenv("AGN_COUNTER_GLDS");
     if (v && (v[0] == '0' || v[0] == '1')) return v[0] - '0';
     return -1;
@@ -449,7 +653,14 @@ int launch_var(int v, const agn_log &log, const agn_read &req, const agn_result 
 
 template <int D, int WPB>
 int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    return launch_var<D, WPB>(counter_variant<D>(), log, req, out, st);
+    const int v = counter_variant<D>();
+    // quad rows, warm batch (SCT given), not forced: two requests per wave
+    // (warm cfg2 8.37-8.45 vs 8.83-9.02 ms; cold no change,
+    // profiles/r02/ab_counter_quad2.log)
+    if constexpr (D == 8)
+        if (v == ROWS_QUAD2 || (v == ROWS_QUAD && req.sct && forced_variant() < 0))
+            return launch_quad2(log, req, out, st);
+    return launch_var<D, WPB>(v == ROWS_QUAD2 ? default_variant<D>() : v, log, req, out, st);
 }
 
 // Waves (= requests) per block: 1 measured 1.4-3.4 % faster than 2 and

@@ -71,7 +71,7 @@ def test_kat_system_txn_gpu(eng, oracle_lib, c):
 # ------------------------------------------------------------------ randomised differential
 # counter_pn runs through every counter kernel: the dense fast path (auto),
 # its opt-in LDS-DMA row path (glds, even D only) and the general kernel
-COUNTER_IMPLS = ("auto", "glds", "quad", "general")
+COUNTER_IMPLS = ("auto", "glds", "quad", "quad2", "general")
 DIFF = []
 for crdt in (_abi.COUNTER_PN, _abi.SET_AW, _abi.REGISTER_MV):
     for D in (1, 2, 3, 5, 8, 12, 16, 17, 33, 64, 100, 256):
@@ -85,9 +85,11 @@ def _set_impl(monkeypatch, impl):
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     # "auto" = the VGPR-row dense kernel whatever agn_tune selected in this
-    # process; "glds" / "quad" = the LDS-DMA / quad-row variants where the
-    # shape has them (even D / D = 8), else VGPR rows
-    monkeypatch.setenv("AGN_COUNTER_VARIANT", {"glds": "1", "quad": "2"}.get(impl, "0"))
+    # process; "glds" / "quad" / "quad2" = the LDS-DMA / quad-row / two-
+    # requests-per-wave quad-row variants where the shape has them (even D /
+    # D = 8), else VGPR rows
+    monkeypatch.setenv("AGN_COUNTER_VARIANT",
+                       {"glds": "1", "quad": "2", "quad2": "3"}.get(impl, "0"))
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
 
@@ -148,6 +150,24 @@ def test_long_keys_vs_oracle(eng, oracle_lib, counter_impl):
         ls.oc_mask = None
         oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4)
         assert not compare(crdt, 8, res_g, res_o, False, req.n_req)
+
+
+@pytest.mark.parametrize("variant", [None, "2", "3"])
+@pytest.mark.parametrize("K", [1, 2, 301])
+def test_quad_pairs_vs_oracle(eng, oracle_lib, monkeypatch, variant, K):
+    """D = 8 quad rows with a request keys array and odd / tiny batches: the
+    two-requests-per-wave kernel's last wave has one request; cold and warm
+    requests mixed (variant None = the default choice: quad2 for a warm batch)."""
+    monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    if variant is None:
+        monkeypatch.delenv("AGN_COUNTER_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("AGN_COUNTER_VARIANT", variant)
+    log, req, cap = random_case(6151 + K, _abi.COUNTER_PN, K, 8, 200, warm=0.5, txid=0.3,
+                                invalid=0.02, corrupt=0.05, base=0.4, identity=False)
+    _, _, bad = _oracle_vs_gpu(eng, oracle_lib, _abi.COUNTER_PN, 8, log, req)
+    assert not bad, bad[:10]
 
 
 def _oracle_vs_gpu(eng, oracle_lib, crdt, D, log, req, sparse=False):
