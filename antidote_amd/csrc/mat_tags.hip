@@ -212,10 +212,25 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     for (uint64_t it = (uint64_t)blk * WPB + (uint64_t)w; it < n_items; it += nw) {
         const uint64_t i = SLOW ? (uint64_t)__builtin_amdgcn_readfirstlane(wl[it]) : it;
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
+        // The key's and the request's side values load together and
+        // unconditionally (in-bounds dummies for absent columns): each
+        // conditional load was waited for on its own before the next issued.
+        const uint64_t *lenp = log.key_len ? log.key_len + key : log.key_off + key + 1;
         const uint64_t off = uniform_u64(log.key_off[key]);
-        const uint64_t n = uniform_u64(key_n(log.key_off, log.key_len, key));
+        const uint64_t lv = uniform_u64(*lenp);
+        const uint32_t kt = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(log.key_type ? log.key_type
+                                    : reinterpret_cast<const uint8_t *>(log.key_off))[key]);
+        const uint32_t si = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(req.sct_ignore ? req.sct_ignore
+                                      : reinterpret_cast<const uint8_t *>(req.R))[i]);
+        const uint64_t txv = uniform_u64((req.txid ? req.txid : req.R)[i]);
+        const uint64_t *bop = req.base_off ? req.base_off + i : req.R + i;
+        const uint64_t b0v = uniform_u64(bop[0]);
+        const uint64_t b1v = uniform_u64((req.base_off ? bop + 1 : bop)[0]);
+        const uint64_t n = log.key_len ? lv : lv - off;
 
-        if (n != 0 && log.key_type != nullptr && log.key_type[key] != (uint8_t)req.req_type) {
+        if (n != 0 && log.key_type != nullptr && kt != (uint32_t)(uint8_t)req.req_type) {
             if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
                 out.flags[i] = AGN_F_ERR_CORRUPTED;
                 out.err_pos[i] = 0xffffffffu;
@@ -225,20 +240,24 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         }
 
         // ---- read snapshot R, base snapshot time SCT, LastOpCt seed
-        const bool sct_ign = !WARM || req.sct == nullptr || (req.sct_ignore && req.sct_ignore[i]);
+        const bool sct_ign = !WARM || req.sct == nullptr || (req.sct_ignore && si != 0u);
+        const uint64_t *sctp = req.sct ? req.sct : req.R;
         const uint32_t rbits = chunk_bits<DPL, SPARSE>(req.R_mask, i, W, d0, D);
         const uint32_t sbits = sct_ign ? 0u : chunk_bits<DPL, SPARSE>(req.sct_mask, i, W, d0, D);
         uint64_t r[DPL], s[DPL], ct[DPL];
 #pragma unroll
         for (int j = 0; j < DPL; ++j) {
             const uint32_t d = (uint32_t)(d0 + j);
-            r[j] = (d < D) ? req.R[i * D + d] : 0ull;
-            s[j] = ((sbits >> j) & 1u) ? req.sct[i * D + d] : 0ull;
+            const uint32_t dd = d < D ? d : D - 1u;
+            const uint64_t rv = req.R[i * D + dd];
+            const uint64_t sv = WARM ? sctp[i * D + dd] : 0ull;
+            r[j] = (d < D) ? rv : 0ull;
+            s[j] = ((sbits >> j) & 1u) ? sv : 0ull;
             // LastOpCt starts as SnapshotCommitTime (materialize/4 :94-95);
             // "+1 encoded" in sparse mode (0 = DC absent from the dict)
             ct[j] = ((sbits >> j) & 1u) ? (SPARSE ? s[j] + 1ull : s[j]) : 0ull;
         }
-        const uint64_t txr = req.txid ? uniform_u64(req.txid[i]) : 0ull;
+        const uint64_t txr = req.txid ? txv : 0ull;
         const bool use_tx = txr != 0ull && log.txid != nullptr;
         // CT: this lane's parts of R / SCT / LastOpCt (DCs dp, dp + 1)
         uint64_t rA = 0, rB = 0, sA = 0, sB = 0, ctA = 0, ctB = 0;
@@ -246,9 +265,10 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             const uint32_t dp = 2u * (uint32_t)(lane % P);
             rA = req.R[i * D + dp];
             rB = req.R[i * D + dp + 1];
-            if (!sct_ign) {
-                sA = req.sct[i * D + dp];
-                sB = req.sct[i * D + dp + 1];
+            if constexpr (WARM) {
+                const uint64_t xa = sctp[i * D + dp], xb = sctp[i * D + dp + 1];
+                sA = sct_ign ? 0ull : xa;
+                sB = sct_ign ? 0ull : xb;
             }
             ctA = sA;
             ctB = sB;
@@ -256,8 +276,8 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 
         // ---- base snapshot state: candidates with ord = index (< B)
         heads_clear<CAP>(L);
-        const uint64_t b0 = req.base_off ? req.base_off[i] : 0ull;
-        const uint32_t B = req.base_off ? (uint32_t)(req.base_off[i + 1] - b0) : 0u;
+        const uint64_t b0 = req.base_off ? b0v : 0ull;
+        const uint32_t B = req.base_off ? (uint32_t)(b1v - b0v) : 0u;
         bool overflow = B > (uint32_t)(CAP - AGN_WAVE);
         uint32_t used = 0;
         if (!overflow) {
