@@ -653,6 +653,57 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
                            handle, prune, threshold, threshold_mask, (hipStream_t)stream);
 }
 
+// agn_read_cached's batch size from which it runs the three batched kernels
+// (k_ss_lookup -> the counter kernel -> k_ss_store, per-request prune flags)
+// instead of the fused one: same results; the batched kernels serve 8
+// requests per wave in the cache steps and two per wave in a warm scan, so a
+// bulk batch is faster that way (10M keys: 10.2 against 11.6 ms), while the
+// fused kernel's single launch wins for serving-sized batches (10k keys: 21
+// against 35 us).  AGN_READ_CACHED_SPLIT=<n> moves the switch (0: never).
+static uint64_t read_cached_split() {
+    const char *v = getenv("AGN_READ_CACHED_SPLIT");
+    if (v && v[0]) {
+        const uint64_t n = strtoull(v, nullptr, 10);
+        return n ? n : ~0ull;
+    }
+    return 1ull << 20;
+}
+
+static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
+                           const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
+                           const uint8_t *should_gc, agn_result *out, uint8_t *status,
+                           uint8_t *prune, uint64_t *threshold, hipStream_t st) {
+    const uint32_t D = log->n_dcs;
+    uint8_t *tmp = nullptr;  // sct [n][D] u64 | base [n] i64 | ign [n] | first [n]
+    const size_t sz = n_req * (8ull * D + 8ull + 2ull);
+    AGN_HIP(pool_malloc((void **)&tmp, sz, st));
+    uint64_t *sct = reinterpret_cast<uint64_t *>(tmp);
+    int64_t *base = reinterpret_cast<int64_t *>(sct + n_req * D);
+    uint8_t *ign = reinterpret_cast<uint8_t *>(base + n_req);
+    uint8_t *first = ign + n_req;
+    int rc = launch_ss_lookup(*cache, n_req, keys, R, nullptr, sct, nullptr, ign, base, first,
+                              status, st);
+    if (rc == AGN_OK) {
+        agn_read rq{};
+        rq.n_req = n_req;
+        rq.keys = keys;
+        rq.R = R;
+        rq.sct = sct;
+        rq.sct_ignore = ign;
+        rq.txid = txid;
+        rq.req_type = AGN_COUNTER_PN;
+        rq.base_value = base;
+        agn_result o = *out;
+        o.lastct_mask = nullptr;
+        rc = launch_counter(*log, rq, o, st);
+    }
+    if (rc == AGN_OK)
+        rc = launch_ss_store_req(*cache, log->key_off, log->key_len, n_req, keys, first, status,
+                                 should_gc, *out, prune, threshold, nullptr, st);
+    (void)hipFreeAsync(tmp, st);
+    return rc;
+}
+
 int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
                     const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
                     const uint8_t *should_gc, agn_result *out, uint8_t *status, uint8_t *prune,
@@ -671,6 +722,9 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
     rc = use_device(ctx);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
+    if (n_req >= read_cached_split()) return read_cached_seq(cache, log, n_req, keys, R, txid,
+                                                             should_gc, out, status, prune,
+                                                             threshold, st);
     uint64_t *dkeys = nullptr;  // the kernel's copy of the batch's keys (read batcher's GC list)
     AGN_HIP(pool_malloc((void **)&dkeys, n_req * sizeof(uint64_t), st));
     Read6Args a;

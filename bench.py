@@ -606,23 +606,38 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
     ms = (t_lookup + t_mat + t_store) / steps
     flags = eng.download(res.bufs["flags"], np.uint32, (n_keys,))
     cnt = eng.download(res.bufs["count"], np.uint32, (n_keys,))
-    # the same warm step as one kernel (agn_read_cached) on the same cache
+    # the same warm step through agn_read_cached on the same cache: its
+    # default dispatch (the batched kernels from 1M requests) and the fused
+    # kernel forced at this size (AGN_READ_CACHED_SPLIT=0)
     dkeys = eng.upload(np.arange(n_keys, dtype=np.uint64))
-    t_fused = 0.0
-    for i in range(steps + 1):
-        ev[0].record()
-        eng.read_cached(c, dl, n_keys, dkeys.ptr, dr.R, dr.txid, None, res, bufs["status"].ptr,
-                        bufs["prune"].ptr, bufs["thr"].ptr, sp)
-        ev[1].record()
-        torch.cuda.synchronize()
-        if i:
-            t_fused += ev[0].elapsed_time(ev[1])
+    t_rc = {}
+    old_split = os.environ.get("AGN_READ_CACHED_SPLIT")
+    for form, split in (("default", old_split), ("fused", "0")):
+        if split is None:
+            os.environ.pop("AGN_READ_CACHED_SPLIT", None)
+        else:
+            os.environ["AGN_READ_CACHED_SPLIT"] = split
+        t_rc[form] = 0.0
+        for i in range(steps + 1):
+            ev[0].record()
+            eng.read_cached(c, dl, n_keys, dkeys.ptr, dr.R, dr.txid, None, res,
+                            bufs["status"].ptr, bufs["prune"].ptr, bufs["thr"].ptr, sp)
+            ev[1].record()
+            torch.cuda.synchronize()
+            if i:
+                t_rc[form] += ev[0].elapsed_time(ev[1])
+    if old_split is None:
+        os.environ.pop("AGN_READ_CACHED_SPLIT", None)
+    else:
+        os.environ["AGN_READ_CACHED_SPLIT"] = old_split
+    t_fused = t_rc["fused"]
     hits_f = eng.download(bufs["status"], np.uint8, (n_keys,))
     for b in list(bufs.values()) + list(res.bufs.values()) + [dkeys]:
         b.free()
     ops = n_keys * cfg["ops_per_key"]
     return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
             "store_ms": t_store / steps, "ops_per_s": ops / (ms * 1e-3),
+            "read_cached_ms": t_rc["default"] / steps,
             "fused_ms": t_fused / steps, "fused_ops_per_s": ops / (t_fused / steps * 1e-3),
             "fused_hit_frac": float((hits_f == _abi.SS_HIT).mean()),
             "vc_compares_per_s": 2 * ops / (ms * 1e-3),

@@ -480,11 +480,13 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
  * results in out (value, hole, lastct, count, flags, err_pos), status[n_req]
  * (AGN_SS_*), prune[n_req] (per request, unlike agn_ss_store's per key) and
  * threshold[n_keys][D].  Same results, cache contents and prune flags as the
- * three calls; AGN_ENOTSUP for another type or shape.  One launch, the key's
- * cache slots held in registers: 21 us for 10k keys (cfg1, D = 3) where the
- * three calls take 35 us; a bulk batch is faster as the three calls (10M keys,
- * cfg2: 11.6 vs 10.1 ms).  Reads at most 16 slots of a key (caches written by
- * these entry points hold at most SNAPSHOT_THRESHOLD - 1). */
+ * three calls; AGN_ENOTSUP for another type or shape.  Below 2^20 requests
+ * one launch, the key's cache slots held in registers (21 us for 10k keys,
+ * cfg1, D = 3, where the three calls take 35 us); from 2^20 requests the
+ * batched kernels, which are faster in bulk (10M keys: 10.2 vs 11.6 ms);
+ * AGN_READ_CACHED_SPLIT=<n> moves the switch (0: always one launch).  Reads
+ * at most 16 slots of a key (caches written by these entry points hold at
+ * most SNAPSHOT_THRESHOLD - 1). */
 int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
                     const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
                     const uint8_t *should_gc, agn_result *out, uint8_t *status, uint8_t *prune,
