@@ -656,17 +656,19 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
 // agn_read_cached's batch size from which it runs the three batched kernels
 // (k_ss_lookup -> the counter kernel -> k_ss_store, per-request prune flags)
 // instead of the fused one: same results; the batched kernels serve 8
-// requests per wave in the cache steps and two per wave in a warm scan, so a
-// bulk batch is faster that way (10M keys: 10.2 against 11.6 ms), while the
-// fused kernel's single launch wins for serving-sized batches (10k keys: 21
-// against 35 us).  AGN_READ_CACHED_SPLIT=<n> moves the switch (0: never).
+// requests per wave in the cache steps and two per wave in a warm scan, so
+// they win from ~32k requests (warm cfg2 keys, batched vs fused: 10k 28 vs
+// 24 us, 30k 48.6 vs 48.5, 100k 116 vs 125, 300k 309 vs 354, 1M 1.05 vs
+// 1.17 ms, 10M 10.2 vs 11.6 ms; profiles/r02/read_cached_split.log), while
+// the fused kernel's single launch wins below.  AGN_READ_CACHED_SPLIT=<n>
+// moves the switch (0: never).
 static uint64_t read_cached_split() {
     const char *v = getenv("AGN_READ_CACHED_SPLIT");
     if (v && v[0]) {
         const uint64_t n = strtoull(v, nullptr, 10);
         return n ? n : ~0ull;
     }
-    return 1ull << 20;
+    return 1ull << 15;
 }
 
 static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_req,

@@ -480,9 +480,9 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
  * results in out (value, hole, lastct, count, flags, err_pos), status[n_req]
  * (AGN_SS_*), prune[n_req] (per request, unlike agn_ss_store's per key) and
  * threshold[n_keys][D].  Same results, cache contents and prune flags as the
- * three calls; AGN_ENOTSUP for another type or shape.  Below 2^20 requests
+ * three calls; AGN_ENOTSUP for another type or shape.  Below 2^15 requests
  * one launch, the key's cache slots held in registers (21 us for 10k keys,
- * cfg1, D = 3, where the three calls take 35 us); from 2^20 requests the
+ * cfg1, D = 3, where the three calls take 35 us); from 2^15 requests the
  * batched kernels, which are faster in bulk (10M keys: 10.2 vs 11.6 ms);
  * AGN_READ_CACHED_SPLIT=<n> moves the switch (0: always one launch).  Reads
  * at most 16 slots of a key (caches written by these entry points hold at
