@@ -1,19 +1,21 @@
 // read6.hip — materializer_vnode:read/6 for a batch of distinct keys in ONE
 // kernel (the cached read batcher's path for counter_pn, dense clocks,
-// D <= 8).  One wave per request:
+// D <= 8).  One wave per request, the key's cache slots in registers:
 //   1. get_from_snapshot_cache (src/materializer_vnode.erl:384-413,
-//      vector_orddict:get_smaller src/vector_orddict.erl:74-87) on the
-//      request's group of G lanes (cache_dev.hpp), the SCT row into LDS;
+//      vector_orddict:get_smaller src/vector_orddict.erl:74-87): a ballot of
+//      "slot > R" folded per slot on the scalar unit, SCT and the base value
+//      read out of the slot registers;
 //   2. materialize/4 from that base (src/clocksi_materializer.erl:82-268):
-//      the dense counter scan (counter_scan.hpp), SCT and R in SGPRs;
+//      the dense counter scan (counter_scan.hpp), SCT and R in SGPRs; D = 8
+//      scans quad rows with the first chunk issued with the slot loads;
 //   3. the cache half of materialize_snapshot / internal_store_ss /
-//      snapshot_insert_gc (:341-364, 466-563) on the group, LastOpCt from LDS.
-// The three steps are the batched kernels k_ss_lookup -> k_counter_key ->
-// k_ss_store run back to back per request, so a batch costs one launch
-// instead of three kernels and two copies: for the read batcher requests are
-// read from, and results written to, device-visible pinned host memory;
-// agn_read_cached runs it over device arrays.  D = 8 scans quad rows
-// (counter_scan.hpp scan_key_q8), as the batched counter kernel does.
+//      insert_bigger / snapshot_insert_gc (:341-364, 466-563): the shift and
+//      the GC threshold from the slot registers.
+// Same results as the batched kernels k_ss_lookup -> k_counter_key ->
+// k_ss_store (cache_dev.hpp, per-request prune flags), in one launch instead
+// of three kernels and two copies: for the read batcher requests are read
+// from, and results written to, device-visible pinned host memory;
+// agn_read_cached runs it over device arrays below 2^15 requests.
 #include "counter_scan.hpp"
 #include "serve.hpp"
 
