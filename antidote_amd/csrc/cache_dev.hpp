@@ -65,6 +65,14 @@ __device__ __forceinline__ LookupOut ss_lookup_one(const Grp<G> &g, const agn_ss
                                                    const uint64_t *Rm_row, uint64_t *sct_row,
                                                    uint64_t *sctm_row) {
     const uint32_t D = c.n_dcs, W = n_words(D), S = c.slots;
+    // Dense rows with D <= G: slot 0 (always in bounds), its value and R are
+    // loaded with the entry count, so a hit on the newest snapshot -- the
+    // common warm read -- costs no round trip after it.
+    const bool dense1 = D <= (uint32_t)G && c.clock_mask == nullptr && Rm_row == nullptr;
+    const uint32_t dd = g.sub < D ? g.sub : D - 1u;
+    const uint64_t c0 = c.clock[(k * S) * D + dd];
+    const uint64_t r0 = R_row[dd];
+    const int64_t v0 = c.value[k * S];
     const uint32_t n = c.n[k];
     if (n == 0) {
         for (uint32_t d = g.sub; d < D; d += G) {
@@ -83,7 +91,12 @@ __device__ __forceinline__ LookupOut ss_lookup_one(const Grp<G> &g, const agn_ss
         return LookupOut{1, 1, AGN_SS_NEW, 0};  // base {ignore, Type:new()} (:395-396)
     }
     int found = -1;
-    for (uint32_t j = 0; j < n; ++j) {
+    uint32_t j0 = 0;
+    if (dense1) {
+        if (g.all(g.sub >= D || c0 <= r0)) found = 0;
+        else j0 = 1;
+    }
+    for (uint32_t j = j0; found < 0 && j < n; ++j) {
         if (grp_le<G>(g, c.clock, c.clock_mask, k * S + j, R_row, Rm_row, 0, D, W)) {
             found = (int)j;
             break;
@@ -91,7 +104,11 @@ __device__ __forceinline__ LookupOut ss_lookup_one(const Grp<G> &g, const agn_ss
     }
     if (found >= 0) {
         const uint64_t row = k * S + (uint64_t)found;
-        copy_row<G>(g, sct_row, 0, c.clock, row, D);
+        if (dense1 && found == 0) {
+            if (g.sub < D) sct_row[g.sub] = c0;
+        } else {
+            copy_row<G>(g, sct_row, 0, c.clock, row, D);
+        }
         if (sctm_row) {
             if (c.clock_mask) copy_row<G>(g, sctm_row, 0, c.clock_mask, row, W);
             else for (uint32_t x = g.sub; x < W; x += G) sctm_row[x] = full_word(x, W, D);
@@ -99,7 +116,9 @@ __device__ __forceinline__ LookupOut ss_lookup_one(const Grp<G> &g, const agn_ss
     }
     return LookupOut{(uint8_t)(found >= 0 ? 0 : 1), (uint8_t)(found == 0 ? 1 : 0),
                      (uint8_t)(found >= 0 ? AGN_SS_HIT : AGN_SS_LOG),
-                     found >= 0 ? c.value[k * S + (uint64_t)found] : 0};
+                     found == 0 && dense1 ? v0
+                     : found >= 0         ? c.value[k * S + (uint64_t)found]
+                                          : 0};
 }
 
 // The cache half of materialize_snapshot for one request on its group
