@@ -342,10 +342,16 @@ FULL = [
     # BASELINE cfg4 (one GPU's shard at G=8): register_mv 125k keys x 100 ops, D=64
     dict(crdt_type=3, n_dcs=64, n_keys=125_000, ops_per_key=100, n_elems=16, seed=20250115,
          key_stride=8),
+    # cfg3 / cfg4 warm (SCT rows: the tags kernels' warm filter at full size)
+    dict(crdt_type=2, n_dcs=16, n_keys=1_000_000, ops_per_key=256, n_elems=32, seed=20250114,
+         warm=1),
+    dict(crdt_type=3, n_dcs=64, n_keys=125_000, ops_per_key=100, n_elems=16, seed=20250115,
+         key_stride=8, warm=1),
 ]
 
 
-@pytest.mark.parametrize("spec", FULL, ids=["cfg2_counter", "cfg2_counter_warm", "cfg3_set_aw", "cfg4_register_mv"])
+@pytest.mark.parametrize("spec", FULL, ids=["cfg2_counter", "cfg2_counter_warm", "cfg3_set_aw", "cfg4_register_mv",
+                              "cfg3_set_aw_warm", "cfg4_register_mv_warm"])
 def test_full_size_sampled_parity(eng, oracle_lib, spec):
     cfg = _abi.AgnGenCfg(**{"key_base": 0, "key_stride": 1, "warm": 0, **spec})
     dl, dr, res = _run_dev(eng, cfg)
