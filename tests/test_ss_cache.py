@@ -358,3 +358,74 @@ def test_read_cached_vs_sequence(eng, monkeypatch, D, split):
         for b in list(o.values()) + [dk, dR, dtx, dgc, st_b, pr_b, thr_b] + \
                 list(res_a.bufs.values()) + list(res_b.bufs.values()):
             b.free()
+
+
+@pytest.mark.gpu
+def test_read_cached_default_dispatch(eng, monkeypatch):
+    """A batch above the fused/batched switch (2^15 requests) through
+    agn_read_cached's default dispatch equals the fused kernel forced on it
+    (AGN_READ_CACHED_SPLIT=0): outputs, status, prune flags, thresholds and
+    the caches, over a cold round and a warm round with GC reads."""
+    K, D = 40_000, 8
+    log, req, _ = random_case(977, _abi.COUNTER_PN, K, D, 12, txid=0.2, empty=0.05)
+    dlog = eng.upload_log(log)
+    dlog.struct.oc_mask = None
+    rng = np.random.default_rng(5)
+
+    def cache():
+        bufs = {"n": eng.upload(np.zeros(K, np.uint32)),
+                "clock": eng.empty(8 * K * S * D), "last_op": eng.empty(8 * K * S),
+                "value": eng.empty(8 * K * S)}
+        c = _abi.AgnSsCache()
+        c.n_dcs, c.slots, c.n_keys = D, S, K
+        c.n, c.clock, c.last_op, c.value = (bufs[x].ptr for x in ("n", "clock", "last_op", "value"))
+        c.clock_mask = None
+        return c, bufs
+
+    caches = [cache(), cache()]
+    nr = 36_000
+    try:
+        for rnd in range(2):
+            keys = rng.permutation(K)[:nr].astype(np.uint64)
+            R = req.R[keys.astype(np.int64)] + rng.integers(0, 3, (nr, D)).astype(np.uint64)
+            tx = req.txid[keys.astype(np.int64)].copy()
+            gc = (rng.random(nr) < 0.2).astype(np.uint8)
+            dk, dR, dtx, dgc = (eng.upload(x) for x in (keys, np.ascontiguousarray(R), tx, gc))
+            got = []
+            for (c, _b), split in zip(caches, (None, "0")):
+                if split is None:
+                    monkeypatch.delenv("AGN_READ_CACHED_SPLIT", raising=False)
+                else:
+                    monkeypatch.setenv("AGN_READ_CACHED_SPLIT", split)
+                res = eng.alloc_result(nr, D, sparse=False)
+                st, pr, thr = eng.empty(nr), eng.empty(nr), eng.empty(K * D * 8)
+                eng.lib.agn_memset_d(eng.ctx, thr.ptr, 0, K * D * 8, None)
+                eng.read_cached(c, dlog, nr, dk.ptr, dR.ptr, dtx.ptr, dgc.ptr, res, st.ptr, pr.ptr,
+                                thr.ptr)
+                eng.sync()
+                got.append((eng.fetch_result(res), eng.download(st, np.uint8, (nr,)),
+                            eng.download(pr, np.uint8, (nr,)),
+                            eng.download(thr, np.uint64, (K, D))))
+                for b in [st, pr, thr] + list(res.bufs.values()):
+                    b.free()
+            (ra, sa, pa, ta), (rb, sb, pb, tb) = got
+            for f in ("value", "hole", "lastct", "count", "flags", "err_pos"):
+                assert np.array_equal(getattr(ra, f), getattr(rb, f)), (rnd, f)
+            assert np.array_equal(sa, sb) and np.array_equal(pa, pb), rnd
+            assert np.array_equal(ta, tb), rnd
+            na = eng.download(caches[0][1]["n"], np.uint32, (K,))
+            assert np.array_equal(na, eng.download(caches[1][1]["n"], np.uint32, (K,))), rnd
+            for name, dt, shape in (("clock", np.uint64, (K, S, D)), ("last_op", np.int64, (K, S)),
+                                    ("value", np.int64, (K, S))):
+                xa = eng.download(caches[0][1][name], dt, shape)
+                xb = eng.download(caches[1][1][name], dt, shape)
+                live = np.arange(S)[None, :] < na[:, None]
+                assert np.array_equal(xa[live], xb[live]), (rnd, name)
+            if rnd == 1:
+                assert (sa == _abi.SS_HIT).any() and pa.any()
+            for b in (dk, dR, dtx, dgc):
+                b.free()
+    finally:
+        for _c, bufs in caches:
+            for b in bufs.values():
+                b.free()
