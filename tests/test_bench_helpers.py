@@ -1,0 +1,62 @@
+"""bench.py's measurement plumbing on the CPU: the PMC traffic attached to a
+bench line is the file measured on exactly the kernel's current sources and
+units per launch (scripts/pmc_traffic.py output), never a stale one, and the
+algorithmic byte counts follow DESIGN.md §4 / SURVEY.md §8(d)."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_kernel_sha_covers_sources_and_header(tmp_path, monkeypatch):
+    base = bench.kernel_src_sha16(2)
+    assert len(base) == 16 and base == bench.kernel_src_sha16(2)
+    # configs built from the same sources share the hash; others differ
+    assert bench.kernel_src_sha16(1) == base
+    assert bench.kernel_src_sha16(3) != base and bench.kernel_src_sha16(5) != base
+    # any change to one of the sources (or the ABI header) changes it
+    fake = tmp_path / "antidote_amd" / "csrc"
+    fake.mkdir(parents=True)
+    (tmp_path / "include").mkdir()
+    for f in bench.KERNEL_SOURCES[2]:
+        (fake / f).write_bytes(open(os.path.join(ROOT, "antidote_amd", "csrc", f), "rb").read())
+    hdr = open(os.path.join(ROOT, "include", "antidote_gpu.h"), "rb").read()
+    (tmp_path / "include" / "antidote_gpu.h").write_bytes(hdr)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.kernel_src_sha16(2) == base
+    (tmp_path / "include" / "antidote_gpu.h").write_bytes(hdr + b"\n")
+    assert bench.kernel_src_sha16(2) != base
+
+
+def test_pmc_traffic_only_on_matching_build(tmp_path, monkeypatch):
+    sha = bench.kernel_src_sha16(2)
+    pmc = tmp_path / "profiles" / "pmc"
+    pmc.mkdir(parents=True)
+    # the hash of the real sources; the PMC directory is a scratch one
+    monkeypatch.setattr(bench, "kernel_src_sha16", lambda c: sha)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    v, why = bench.pmc_traffic(2, 10_000_000)
+    assert v is None and "no PMC pass" in why
+    rec = {"kernel": "k_counter_key", "n_keys": 10_000_000, "hbm_bytes_per_launch": 4.85e10,
+           "kernel_src_sha16": sha, "measured": "test"}
+    (pmc / "cfg2.json").write_text(json.dumps(rec))
+    v, why = bench.pmc_traffic(2, 10_000_000)
+    assert v == 4.85e10 and sha in why
+    v, why = bench.pmc_traffic(2, 5_000_000)  # other units per launch
+    assert v is None and "5000000 units" in why
+    (pmc / "cfg2.json").write_text(json.dumps({**rec, "kernel_src_sha16": "0" * 16}))
+    v, why = bench.pmc_traffic(2, 10_000_000)
+    assert v is None and "0" * 16 in why
+
+
+@pytest.mark.parametrize("config", [1, 2, 3, 4, 5])
+def test_committed_pmc_files_are_well_formed(config):
+    p = os.path.join(ROOT, "profiles", "pmc", f"cfg{config}.json")
+    d = json.load(open(p))
+    assert d["hbm_bytes_per_launch"] > 0 and len(d["kernel_src_sha16"]) == 16
+    assert d["n_keys"] == {1: 10_000, 2: 10_000_000, 3: 1_000_000, 4: 1_000_000, 5: 4096}[config]
