@@ -60,3 +60,18 @@ def test_committed_pmc_files_are_well_formed(config):
     d = json.load(open(p))
     assert d["hbm_bytes_per_launch"] > 0 and len(d["kernel_src_sha16"]) == 16
     assert d["n_keys"] == {1: 10_000, 2: 10_000_000, 3: 1_000_000, 4: 1_000_000, 5: 4096}[config]
+
+
+def test_algorithmic_bytes_match_design():
+    """cfg2's per-launch bytes (47.76 GB; SURVEY.md §8(d):
+    50.24 GB) and the per-op / per-key terms of the counter formula."""
+    c2 = bench.CONFIGS[2]
+    assert bench.algorithmic_bytes(c2, 10_000_000) == 47_760_000_000
+    assert bench.algorithmic_bytes_survey(c2, 10_000_000) == 50_240_000_000
+    c1 = bench.CONFIGS[1]
+    D, N, K = c1["n_dcs"], c1["ops_per_key"], c1["n_keys"]
+    assert bench.algorithmic_bytes(c1, K) == K * N * (8 * D + 8) + K * (8 + 16 * D + 32)
+    # set/register terms grow with removed tokens and live output pairs
+    c3 = bench.CONFIGS[3]
+    b0 = bench.algorithmic_bytes(c3, 1000)
+    assert bench.algorithmic_bytes(c3, 1000, n_rem=10, n_live=5) == b0 + 80 + 60
