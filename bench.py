@@ -635,7 +635,12 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
     for b in list(bufs.values()) + list(res.bufs.values()) + [dkeys]:
         b.free()
     ops = n_keys * cfg["ops_per_key"]
+    # the warm materialize's bytes: the cold kernel's plus the SCT row, its
+    # ignore flag and the base value per request
+    wbytes = algorithmic_bytes(cfg, n_keys) + n_keys * (8 * D + 1 + 8)
     return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
+            "materialize_algorithmic_bytes": wbytes,
+            "materialize_frac": wbytes / (t_mat / steps * 1e-3) / 8e12,
             "store_ms": t_store / steps, "ops_per_s": ops / (ms * 1e-3),
             "read_cached_ms": t_rc["default"] / steps,
             "fused_ms": t_fused / steps, "fused_ops_per_s": ops / (t_fused / steps * 1e-3),
