@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK = 0
 EINVAL, EHIP, ENOMEM, ECAPACITY, ENOTSUP, ERCCL, ENODEV = -1, -2, -3, -4, -5, -6, -7
@@ -41,7 +41,7 @@ class AgnLog(C.Structure):
         ("key_off", P), ("key_len", P), ("key_type", P), ("oc", P), ("oc_mask", P),
         ("op_id", P), ("txid", P), ("eff", P),
         ("tag", P), ("add_tok", P), ("rem_off", P), ("rem_tok", P),
-        ("key_id0", P),
+        ("key_id0", P), ("key_mask", P),
     ]
 
 
@@ -133,6 +133,7 @@ PROTOTYPES = {
                                        C.POINTER(AgnResult)]),
     "agn_state_capacity": (C.c_int, [C.POINTER(AgnLog), C.POINTER(AgnRead), P]),
     "agn_log_index_ids": (C.c_int, [P, C.POINTER(AgnLog), P, P]),
+    "agn_log_index_masks": (C.c_int, [P, C.POINTER(AgnLog), P, P]),
     "agn_tune": (C.c_int, [P, C.POINTER(AgnLog), C.POINTER(AgnRead), C.POINTER(AgnResult), P,
                            C.c_int, C.POINTER(C.c_int), P]),
     "agn_select_base": (C.c_int, [P, C.c_uint32, C.c_uint64, P, P, P, P, P, P, P, P]),

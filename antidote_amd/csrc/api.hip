@@ -330,6 +330,16 @@ int agn_log_index_ids(agn_ctx *ctx, const agn_log *log, uint32_t *out, void *str
     return launch_index_ids(*log, out, (hipStream_t)stream);
 }
 
+int agn_log_index_masks(agn_ctx *ctx, const agn_log *log, uint64_t *out, void *stream) {
+    if (!log || !out) return fail(AGN_EINVAL, "index_masks: null argument");
+    if (log->n_keys && !log->key_off) return fail(AGN_EINVAL, "index_masks: key_off required");
+    if (log->n_dcs == 0 || log->n_dcs > 64)
+        return fail(AGN_EINVAL, "index_masks: n_dcs=%u not in [1,64]", log->n_dcs);
+    int rc = use_device(ctx);
+    if (rc) return rc;
+    return launch_index_masks(*log, out, (hipStream_t)stream);
+}
+
 int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_off) {
     if (!log || !req || !cap_off) return fail(AGN_EINVAL, "null argument");
     cap_off[0] = 0;
@@ -441,6 +451,24 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
         for (uint64_t e = 0; e <= E; ++e) n_rem = std::max<uint64_t>(n_rem, log->rem_off[e]);
     const uint64_t n_base = req->base_off ? req->base_off[Q] : 0;
     const uint64_t n_out = out->out_off ? out->out_off[Q] : 0;
+    // a sparse log without agn_log.key_mask: build it here (one pass over the
+    // masks already in host memory), so keys whose entries share one DC set
+    // take the dense row scan (D <= 8)
+    std::vector<uint64_t> hkm;
+    const uint64_t *kmask = log->key_mask;
+    if (log->oc_mask && !kmask && D <= 8 && log->crdt_type == AGN_COUNTER_PN) {
+        const uint64_t full = low_bits(D);
+        hkm.assign(K, 0);
+        for (uint64_t k = 0; k < K; ++k) {
+            const uint64_t o = log->key_off[k], n = key_n(log->key_off, log->key_len, k);
+            if (n == 0) continue;
+            uint64_t m0 = log->oc_mask[o] & full;
+            for (uint64_t x = 1; x < n && m0; ++x)
+                if ((log->oc_mask[o + x] & full) != m0) m0 = 0;
+            hkm[k] = m0;
+        }
+        kmask = hkm.data();
+    }
     Pack p;
     const size_t l_koff = p.in(log->key_off, K + 1), l_klen = p.in(log->key_len, K),
                  l_ktype = p.in(log->key_type, K), l_oc = p.in(log->oc, E * D),
@@ -448,7 +476,8 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
                  l_tx = p.in(log->txid, E), l_eff = p.in(log->eff, E), l_tag = p.in(log->tag, E),
                  l_add = p.in(log->add_tok, E),
                  l_roff = p.in(log->rem_off, log->rem_off ? E + 1 : 0),
-                 l_rtok = p.in(log->rem_tok, n_rem), l_id0 = p.in(log->key_id0, K);
+                 l_rtok = p.in(log->rem_tok, n_rem), l_id0 = p.in(log->key_id0, K),
+                 l_kmask = p.in(kmask, (log->oc_mask && D <= 64) ? K : 0);
     const size_t q_keys = p.in(req->keys, Q), q_R = p.in(req->R, Q * D),
                  q_Rm = p.in(req->R_mask, Q * W), q_sct = p.in(req->sct, Q * D),
                  q_sctm = p.in(req->sct_mask, Q * W), q_sign = p.in(req->sct_ignore, Q),
@@ -484,6 +513,7 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     dl.rem_off = at<const uint32_t>(S, l_roff);
     dl.rem_tok = at<const uint64_t>(S, l_rtok);
     dl.key_id0 = at<const uint32_t>(S, l_id0);
+    dl.key_mask = at<const uint64_t>(S, l_kmask);
     agn_read dr = *req;
     dr.keys = at<const uint64_t>(S, q_keys);
     dr.R = at<const uint64_t>(S, q_R);
@@ -683,6 +713,8 @@ static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_r
     int64_t *base = reinterpret_cast<int64_t *>(sct + n_req * D);
     uint8_t *ign = reinterpret_cast<uint8_t *>(base + n_req);
     uint8_t *first = ign + n_req;
+    agn_result o = *out;
+    o.lastct_mask = nullptr;
     int rc = launch_ss_lookup(*cache, n_req, keys, R, nullptr, sct, nullptr, ign, base, first,
                               status, st);
     if (rc == AGN_OK) {
@@ -695,13 +727,13 @@ static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_r
         rq.txid = txid;
         rq.req_type = AGN_COUNTER_PN;
         rq.base_value = base;
-        agn_result o = *out;
-        o.lastct_mask = nullptr;
         rc = launch_counter(*log, rq, o, st);
     }
     if (rc == AGN_OK)
+        // the store reads LastOpCt as the counter kernel wrote it: dense, so
+        // with the (unwritten) caller mask nulled as in the kernel's copy
         rc = launch_ss_store_req(*cache, log->key_off, log->key_len, n_req, keys, first, status,
-                                 should_gc, *out, prune, threshold, nullptr, st);
+                                 should_gc, o, prune, threshold, nullptr, st);
     (void)hipFreeAsync(tmp, st);
     return rc;
 }

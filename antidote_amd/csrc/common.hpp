@@ -150,6 +150,7 @@ agn_ctx *oplog_ctx(const agn_oplog *L);
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t s);
 int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st);
+int launch_index_masks(const agn_log &log, uint64_t *out, hipStream_t st);
 int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                          hipStream_t s);
 int tune_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,

@@ -208,6 +208,72 @@ __device__ __forceinline__ void scan_key(const uint64_t *__restrict__ oc,
     }
 }
 
+// ---- presence masks (D <= 8, one mask word per clock) ---------------------
+// A sparse log's key whose entries do not all carry the same DC set, or whose
+// DCs are not all in R (agn_log.key_mask), is scanned with its per-entry
+// masks: lane = op, the row and its mask word loaded together, and the dict
+// fold of is_op_in_snapshot (src/clocksi_materializer.erl:236-258): a DC of
+// the op missing from R excludes the op (:245-247), a DC missing from SCT
+// reads 0 (vectorclock:le), LastOpCt takes the max over each included op's
+// own DCs and unites their DC sets (um, per lane).  s[] is SCT with its
+// missing DCs already 0.  Same outputs as scan_key otherwise.
+template <int D, bool WARM>
+__device__ __forceinline__ void scan_key_msk(const uint64_t *__restrict__ oc,
+                                             const uint64_t *__restrict__ oc_mask,
+                                             const int64_t *__restrict__ eff,
+                                             const uint64_t *__restrict__ txid, uint64_t txr,
+                                             uint64_t off, uint64_t n, const uint64_t (&r)[D],
+                                             const uint64_t (&s)[D], uint64_t rm, uint64_t (&ct)[D],
+                                             uint64_t &um, int64_t &sum, uint32_t &cnt,
+                                             int64_t &first_excl, int64_t &first_err) {
+    constexpr uint64_t FULL = (1ull << D) - 1ull;
+    const int lane = lane_id();
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        const uint64_t pos = b + (uint64_t)lane;
+        const bool valid = pos < n;
+        const uint64_t e = off + (valid ? pos : 0ull);
+        uint64_t o[D];
+        load_row<D, false>(oc + e * D, o);
+        const uint64_t m = (oc_mask ? oc_mask[e] : FULL) & FULL;
+        const int64_t ev = eff[e];
+        bool okR = (m & ~rm) == 0ull, leS = true;  // a DC of the op missing from R: false
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const bool p = ((m >> j) & 1ull) != 0ull;
+            okR = okR && (!p || o[j] <= r[j]);
+            if (WARM) leS = leS && (!p || o[j] <= s[j]);
+        }
+        bool nip = WARM ? !leS : true;
+        if (txid != nullptr) nip = nip || (txid[e] == txr);
+        const bool incl = valid && nip && okR;
+        const bool excl = valid && nip && !okR;
+        if (first_excl < 0) {
+            const uint64_t bx = ballot(excl);
+            if (bx) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(bx);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+            ct[j] = (incl && ((m >> j) & 1ull) && o[j] > ct[j]) ? o[j] : ct[j];
+        um |= incl ? m : 0ull;
+        const bool bad = incl && ev == AGN_EFFECT_INVALID;
+        cnt += (uint32_t)__builtin_popcountll(ballot(incl));
+        if (first_err < 0) {
+            const uint64_t be = ballot(bad);
+            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+        }
+        sum += (incl && !bad) ? ev : 0;
+    }
+}
+
+// OR of a per-lane DC set over the wave (D <= 8 bits), as a scalar.
+template <int D>
+__device__ __forceinline__ uint64_t wave_or_bits(uint64_t um) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) r |= (ballot(((um >> j) & 1ull) != 0ull) != 0ull) ? (1ull << j) : 0ull;
+    return r;
+}
+
 // Bit q of the result = some bit of nibble q of b (q = 0..15), on the scalar
 // unit: the per-op verdict of a ballot whose 4 lanes per op are its 4 parts.
 __device__ __forceinline__ uint64_t nib_any16(uint64_t b) {

@@ -45,6 +45,45 @@ struct DenseArgs {
     uint32_t qnt;  // quad rows, non-temporal loads: bit 0 rows, bit 1 effects (AGN_COUNTER_QUAD_NT)
 };
 
+// Presence masks of a sparse batch (the MSK instantiations; one word per
+// clock, D <= 8): agn_log.key_mask / oc_mask, agn_read.R_mask / sct_mask and
+// agn_result.lastct_mask.  Any may be null (= every DC present).
+struct MaskArgs {
+    const uint64_t *key_mask, *oc_mask, *R_mask, *sct_mask;
+    uint64_t *o_mask;
+};
+
+// A request of a sparse batch: the DC set U every op of its key carries (0 =
+// the entries differ or it is unknown), R's and SCT's DC sets, and whether
+// the dense scan serves it exactly (uni: no ops, or U is known and inside R:
+// then every compare of is_op_in_snapshot's dict fold is a compare of U's
+// columns, src/clocksi_materializer.erl:236-258, and the columns outside U
+// are neutralised -- R and SCT read as +inf there, so they never exclude an
+// op nor keep it out of the snapshot; LastOpCt keeps SCT's value there).
+template <int D>
+struct Presence {
+    uint64_t U, Rm, Sm;
+    bool uni;
+};
+
+template <int D, bool MSK>
+__device__ __forceinline__ Presence<D> presence(const MaskArgs &m, uint64_t kmw, uint64_t rmw,
+                                                uint64_t smw, uint64_t n) {
+    constexpr uint64_t FULL = (1ull << D) - 1ull;
+    Presence<D> p;
+    if constexpr (!MSK) {
+        p.U = p.Rm = p.Sm = FULL;
+        p.uni = true;
+    } else {
+        // a log without masks: every entry carries every DC
+        p.U = m.oc_mask ? (m.key_mask ? (kmw & FULL) : 0ull) : FULL;
+        p.Rm = m.R_mask ? (rmw & FULL) : FULL;
+        p.Sm = m.sct_mask ? (smw & FULL) : FULL;
+        p.uni = n == 0 || (p.U != 0ull && (p.U & ~p.Rm) == 0ull);
+    }
+    return p;
+}
+
 typedef __attribute__((address_space(3))) void *lds_ptr;
 
 // LDS words per wave of the LDS-DMA path: rows (DCP*64 u64, reused as the
@@ -172,22 +211,24 @@ enum { ROWS_VGPR = 0, ROWS_GLDS = 1, ROWS_QUAD = 2, ROWS_QUAD2 = 3 };
 // (writing 16 B instead: 8.33 -> 7.57 ms), full 128 B record lines 1 %,
 // non-temporal stores +7 % worse.  The HBM read/write turnaround, not the
 // instruction stream, is the remaining bound.
-template <int D, bool ANY_WARM, int WPB, int VAR, bool KEYS>
+template <int D, bool ANY_WARM, int WPB, int VAR, bool KEYS, bool MSK>
 __global__ __launch_bounds__(64 * WPB) void k_counter_key(
-    DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
-    const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
-    const uint32_t *__restrict__ key_id0, const uint64_t *__restrict__ oc,
-    const uint32_t *__restrict__ op_id, const int64_t *__restrict__ eff,
-    const uint64_t *__restrict__ log_txid, const uint64_t *__restrict__ R,
-    const uint64_t *__restrict__ sct, const uint8_t *__restrict__ sct_ignore,
-    const uint64_t *__restrict__ req_txid, const int64_t *__restrict__ base_value,
-    int64_t *__restrict__ o_value, int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
+    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
+    const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
+    const uint64_t *__restrict__ oc, const uint32_t *__restrict__ op_id,
+    const int64_t *__restrict__ eff, const uint64_t *__restrict__ log_txid,
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ sct,
+    const uint8_t *__restrict__ sct_ignore, const uint64_t *__restrict__ req_txid,
+    const int64_t *__restrict__ base_value, int64_t *__restrict__ o_value,
+    int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
     uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
     uint32_t *__restrict__ o_err) {
     constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
     constexpr int V = DCP;                                          // op slots per lane
     constexpr bool GLDS = VAR == ROWS_GLDS;
     constexpr bool QUAD = VAR == ROWS_QUAD && D == 8;
+    static_assert(!(MSK && GLDS), "sparse batches use VGPR or quad rows");
     constexpr int LW = GLDS ? GldsLds<D>::WORDS : QUAD ? 1 : DCP * AGN_WAVE;
     __shared__ uint64_t lds_all[WPB][LW];  // GLDS: chunk rows/effects/ids; then the ct stage
 
@@ -199,7 +240,7 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     const uint32_t blk = a.xcd ? xb : blockIdx.x;
     const uint64_t i = uniform_u64((uint64_t)blk * WPB + (uint64_t)w);
     if (i >= a.n_req) return;
-    uint64_t r[D], s[D], ct[D];
+    uint64_t r[D], s[D], e[D], ct[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) r[j] = uniform_u64(R[i * D + j]);  // issued with the key's metadata
     // KEYS = false (identity key map): R and the key's metadata in one round trip
@@ -220,6 +261,13 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     uint64_t sv[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
+    // sparse batch: the key's DC set and R's / SCT's mask words, same round trip
+    uint64_t kmw = 0, rmw = 0, smw = 0;
+    if constexpr (MSK) {
+        kmw = uniform_u64(*(mk.key_mask ? mk.key_mask + key : R));
+        rmw = uniform_u64(*(mk.R_mask ? mk.R_mask + i : R));
+        smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
+    }
     if (n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu)) {
         if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
             o_flags[i] = AGN_F_ERR_CORRUPTED;
@@ -228,37 +276,70 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
         return;
     }
     const bool sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
+    const Presence<D> pr = presence<D, MSK>(mk, kmw, rmw, smw, n);
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        s[j] = sct_ign ? 0ull : sv[j];
-        ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
+        // e = SCT as a dict read (missing DC = 0); LastOpCt starts as it
+        // (materialize/4 :94-95).  s = the compare value: +inf outside U on
+        // the dense scan of a sparse key.
+        const bool inU = ((pr.U >> j) & 1ull) != 0ull;
+        e[j] = (sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : sv[j];
+        s[j] = (MSK && pr.uni && !inU) ? ~0ull : e[j];
+        r[j] = (MSK && pr.uni && !inU) ? ~0ull : r[j];
+        ct[j] = e[j];
     }
     const uint64_t txr = req_txid ? txv : 0ull;
     const uint64_t *tx = (txr != 0ull) ? log_txid : nullptr;
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
     int64_t hid = -1;
+    uint64_t um = 0;            // MSK, mixed key: DCs of the included ops (per lane)
     uint64_t ctA = 0, ctB = 0;  // QUAD: LastOpCt of DCs 2p, 2p+1 (p = lane & 3)
+    const bool warm = ANY_WARM && !sct_ign;
+#define AGN_MSK_SCAN()                                                                         \
+    do {                                                                                       \
+        if (!warm)                                                                             \
+            scan_key_msk<D, false>(oc, mk.oc_mask, eff, tx, txr, off, n, r, s, pr.Rm, ct, um,  \
+                                   sum, cnt, first_excl, first_err);                           \
+        else                                                                                   \
+            scan_key_msk<D, ANY_WARM>(oc, mk.oc_mask, eff, tx, txr, off, n, r, s, pr.Rm, ct,   \
+                                      um, sum, cnt, first_excl, first_err);                    \
+    } while (0)
     if constexpr (QUAD) {
         const int p = lane & 3;
         const uint64_t rA = p == 0 ? r[0] : p == 1 ? r[2 % D] : p == 2 ? r[4 % D] : r[6 % D];
         const uint64_t rB = p == 0 ? r[1 % D] : p == 1 ? r[3 % D] : p == 2 ? r[5 % D] : r[7 % D];
         const uint64_t sA = p == 0 ? s[0] : p == 1 ? s[2 % D] : p == 2 ? s[4 % D] : s[6 % D];
         const uint64_t sB = p == 0 ? s[1 % D] : p == 1 ? s[3 % D] : p == 2 ? s[5 % D] : s[7 % D];
-        ctA = sA;
-        ctB = sB;
+        const uint64_t eA = p == 0 ? e[0] : p == 1 ? e[2 % D] : p == 2 ? e[4 % D] : e[6 % D];
+        const uint64_t eB = p == 0 ? e[1 % D] : p == 1 ? e[3 % D] : p == 2 ? e[5 % D] : e[7 % D];
+        ctA = eA;
+        ctB = eB;
 #define AGN_Q8(W, NT, ENT)                                                                     \
     scan_key_q8<W, NT, ENT>(oc, eff, tx, txr, off, n, a.n_entries, rA, rB, sA, sB, ctA, ctB, sum, \
                             cnt, first_excl, first_err)
-        const bool warm = ANY_WARM && !sct_ign;
-        if (!warm) {
-            if (a.qnt & 2u) AGN_Q8(false, true, true);
-            else if (a.qnt & 1u) AGN_Q8(false, true, false);
-            else AGN_Q8(false, false, false);
-        } else {
-            if (a.qnt & 2u) AGN_Q8(ANY_WARM, true, true);
-            else if (a.qnt & 1u) AGN_Q8(ANY_WARM, true, false);
-            else AGN_Q8(ANY_WARM, false, false);
+        if (!MSK || pr.uni) {
+            if (!warm) {
+                if (a.qnt & 2u) AGN_Q8(false, true, true);
+                else if (a.qnt & 1u) AGN_Q8(false, true, false);
+                else AGN_Q8(false, false, false);
+            } else {
+                if (a.qnt & 2u) AGN_Q8(ANY_WARM, true, true);
+                else if (a.qnt & 1u) AGN_Q8(ANY_WARM, true, false);
+                else AGN_Q8(ANY_WARM, false, false);
+            }
+            if (MSK) {  // outside U: SCT's value (an op's row there is not in its dict)
+                ctA = ((pr.U >> (2 * p)) & 1ull) ? ctA : eA;
+                ctB = ((pr.U >> (2 * p + 1)) & 1ull) ? ctB : eB;
+            }
+        } else if constexpr (MSK) {
+            AGN_MSK_SCAN();
+#pragma unroll
+            for (int j = 0; j < D; ++j)
+#pragma unroll
+                for (int x = 1; x < AGN_WAVE; x <<= 1) ct[j] = umax64(ct[j], shfl_xor_u64(ct[j], x));
+            ctA = p == 0 ? ct[0] : p == 1 ? ct[2 % D] : p == 2 ? ct[4 % D] : ct[6 % D];
+            ctB = p == 0 ? ct[1 % D] : p == 1 ? ct[3 % D] : p == 2 ? ct[5 % D] : ct[7 % D];
         }
 #undef AGN_Q8
     } else if constexpr (GLDS && D % 2 == 0) {
@@ -268,21 +349,30 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
         else
             hid = scan_key_glds<D, ANY_WARM>(oc, eff, op_id, tx, txr, off, n, a.n_entries, r, s,
                                              ct, sum, cnt, first_excl, first_err, lds_all[w]);
-    } else if (D <= 4 && a.pair) {
-        if (!ANY_WARM || sct_ign)
-            scan_key<D, false, true>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                                     first_err);
-        else
-            scan_key<D, ANY_WARM, true>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt,
-                                        first_excl, first_err);
     } else {
-        if (!ANY_WARM || sct_ign)
-            scan_key<D, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                               first_err);
-        else
-            scan_key<D, ANY_WARM>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
-                                  first_err);
+        if (MSK && !pr.uni) {
+            if constexpr (MSK) AGN_MSK_SCAN();
+        } else if (D <= 4 && a.pair) {
+            if (!warm)
+                scan_key<D, false, true>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                         first_err);
+            else
+                scan_key<D, ANY_WARM, true>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt,
+                                            first_excl, first_err);
+        } else {
+            if (!warm)
+                scan_key<D, false>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                   first_err);
+            else
+                scan_key<D, ANY_WARM>(oc, eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl,
+                                      first_err);
+        }
+        if (MSK && pr.uni) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) ct[j] = ((pr.U >> j) & 1ull) ? ct[j] : e[j];
+        }
     }
+#undef AGN_MSK_SCAN
     // NewLastOp id and base value: scalar loads, issued before the reductions
     if (hid < 0) {
         const uint64_t pos = first_excl >= 0 ? (uint64_t)first_excl : n - 1;
@@ -327,6 +417,13 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
         for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
         if (g == 0 && c < D) o_lastct[i * D + (uint64_t)c] = ct_ign ? 0ull : m;
     }
+    // LastOpCt's DC set: SCT's united with the included ops' (U, or the
+    // per-lane sets of a mixed key)
+    uint64_t mo = 0;
+    if constexpr (MSK) {
+        const uint64_t un = pr.uni ? (cnt ? pr.U : 0ull) : wave_or_bits<D>(um);
+        mo = ct_ign ? 0ull : ((sct_ign ? 0ull : pr.Sm) | un);
+    }
     if (lane == 0) {
         // NewLastOp = id(oldest excluded) - 1, else get_first_id (:49-63)
         const int64_t hole = first_excl >= 0 ? hid - 1 : hid;
@@ -339,6 +436,7 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
         o_count[i] = cnt;
         o_flags[i] = fl;
         o_err[i] = first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
+        if (MSK && mk.o_mask) mk.o_mask[i] = mo;
     }
 }
 
@@ -357,12 +455,13 @@ inline const uint32_t *id0_index(const agn_log &log) {
 struct Q2Key {
     uint64_t i, key, off, n, txr;
     uint32_t id0;
-    bool corrupt, sct_ign;
-    uint64_t rA, rB, sA, sB;
+    bool corrupt, sct_ign, uni;
+    uint64_t rA, rB, sA, sB, eA, eB;  // per lane: DCs 2p, 2p+1 (p = lane & 3)
+    uint64_t U, Sm, Rm;               // MSK (Presence)
 };
 
-template <bool ANY_WARM>
-__device__ __forceinline__ Q2Key q2_prologue(const DenseArgs &a, uint64_t i,
+template <bool ANY_WARM, bool MSK>
+__device__ __forceinline__ Q2Key q2_prologue(const DenseArgs &a, const MaskArgs &mk, uint64_t i,
                                              const uint64_t *__restrict__ keys,
                                              const uint64_t *__restrict__ key_off,
                                              const uint64_t *__restrict__ key_len,
@@ -388,19 +487,35 @@ __device__ __forceinline__ Q2Key q2_prologue(const DenseArgs &a, uint64_t i,
     k.sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
     const uint64_t txv = uniform_u64((req_txid ? req_txid : R)[i]);
     k.txr = req_txid ? txv : 0ull;
-    uint64_t r[D], sv[D];
+    uint64_t kmw = 0, rmw = 0, smw = 0;
+    if constexpr (MSK) {
+        kmw = uniform_u64(*(mk.key_mask ? mk.key_mask + k.key : R));
+        rmw = uniform_u64(*(mk.R_mask ? mk.R_mask + i : R));
+        smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
+    }
+    const Presence<D> pr = presence<D, MSK>(mk, kmw, rmw, smw, k.n);
+    k.U = pr.U;
+    k.Rm = pr.Rm;
+    k.Sm = pr.Sm;
+    k.uni = pr.uni;
+    uint64_t r[D], sv[D], ev[D];
     const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
+        const bool inU = ((pr.U >> j) & 1ull) != 0ull;
         r[j] = uniform_u64(R[i * D + j]);
         sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
-        sv[j] = k.sct_ign ? 0ull : sv[j];
+        ev[j] = (k.sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : sv[j];  // dict read of SCT
+        sv[j] = (MSK && pr.uni && !inU) ? ~0ull : ev[j];              // compare value
+        r[j] = (MSK && pr.uni && !inU) ? ~0ull : r[j];
     }
     const int p = lane_id() & 3;
     k.rA = p == 0 ? r[0] : p == 1 ? r[2] : p == 2 ? r[4] : r[6];
     k.rB = p == 0 ? r[1] : p == 1 ? r[3] : p == 2 ? r[5] : r[7];
     k.sA = p == 0 ? sv[0] : p == 1 ? sv[2] : p == 2 ? sv[4] : sv[6];
     k.sB = p == 0 ? sv[1] : p == 1 ? sv[3] : p == 2 ? sv[5] : sv[7];
+    k.eA = p == 0 ? ev[0] : p == 1 ? ev[2] : p == 2 ? ev[4] : ev[6];
+    k.eB = p == 0 ? ev[1] : p == 1 ? ev[3] : p == 2 ? ev[5] : ev[7];
     return k;
 }
 
@@ -408,6 +523,7 @@ struct Q2Acc {
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
     uint64_t ctA, ctB;
+    uint64_t um = 0;  // MSK, mixed key: the included ops' DC set
 };
 
 template <bool ANY_WARM>
@@ -440,6 +556,45 @@ __device__ __forceinline__ void q2_rest(const Q2Key &k, const uint64_t *__restri
                                               s.first_excl, s.first_err);
 }
 
+// A mixed key of a sparse batch (MSK, !uni): the per-entry-mask scan, lane =
+// op, with R / SCT / the LastOpCt seed gathered back from the quad lanes
+// (lane p < 4 holds DCs 2p, 2p+1).
+template <bool ANY_WARM>
+__device__ __forceinline__ void q2_msk(const Q2Key &k, const uint64_t *__restrict__ oc,
+                                       const uint64_t *__restrict__ oc_mask,
+                                       const int64_t *__restrict__ eff,
+                                       const uint64_t *__restrict__ log_txid, Q2Acc &s) {
+    constexpr int D = 8;
+    uint64_t r[D], sv[D], ct[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const int p = j >> 1;
+        const uint64_t vr = (j & 1) ? k.rB : k.rA, vs = (j & 1) ? k.sB : k.sA,
+                       ve = (j & 1) ? k.eB : k.eA;
+        r[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vr >> 32), p) << 32) |
+               __builtin_amdgcn_readlane((uint32_t)vr, p);
+        sv[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vs >> 32), p) << 32) |
+                __builtin_amdgcn_readlane((uint32_t)vs, p);
+        ct[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ve >> 32), p) << 32) |
+                __builtin_amdgcn_readlane((uint32_t)ve, p);
+    }
+    const uint64_t *tx = k.txr ? log_txid : nullptr;
+    if (ANY_WARM && !k.sct_ign)
+        scan_key_msk<D, true>(oc, oc_mask, eff, tx, k.txr, k.off, k.n, r, sv, k.Rm, ct, s.um,
+                              s.sum, s.cnt, s.first_excl, s.first_err);
+    else
+        scan_key_msk<D, false>(oc, oc_mask, eff, tx, k.txr, k.off, k.n, r, sv, k.Rm, ct, s.um,
+                               s.sum, s.cnt, s.first_excl, s.first_err);
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+        for (int x = 1; x < AGN_WAVE; x <<= 1) ct[j] = umax64(ct[j], shfl_xor_u64(ct[j], x));
+    const int p = lane_id() & 3;
+    s.ctA = p == 0 ? ct[0] : p == 1 ? ct[2] : p == 2 ? ct[4] : ct[6];
+    s.ctB = p == 0 ? ct[1] : p == 1 ? ct[3] : p == 2 ? ct[5] : ct[7];
+}
+
+template <bool MSK>
 __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
                                             const uint32_t *__restrict__ op_id,
                                             const int64_t *__restrict__ base_value,
@@ -448,7 +603,8 @@ __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
                                             uint64_t *__restrict__ o_lastct,
                                             uint32_t *__restrict__ o_count,
                                             uint32_t *__restrict__ o_flags,
-                                            uint32_t *__restrict__ o_err) {
+                                            uint32_t *__restrict__ o_err,
+                                            uint64_t *__restrict__ o_mask) {
     constexpr int D = 8;
     const int lane = lane_id();
     const uint64_t i = k.i;
@@ -468,6 +624,16 @@ __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
     const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)base_value[i]) : 0;
     const int64_t total = wave_sum_dpp(s.sum);
     const bool ct_ign = k.sct_ign && s.cnt == 0u;
+    uint64_t mo = 0;
+    if constexpr (MSK) {
+        if (k.uni) {  // outside U: SCT's value (an op's row there is not in its dict)
+            const int p = lane & 3;
+            s.ctA = ((k.U >> (2 * p)) & 1ull) ? s.ctA : k.eA;
+            s.ctB = ((k.U >> (2 * p + 1)) & 1ull) ? s.ctB : k.eB;
+        }
+        const uint64_t un = k.uni ? (s.cnt ? k.U : 0ull) : wave_or_bits<D>(s.um);
+        mo = ct_ign ? 0ull : ((k.sct_ign ? 0ull : k.Sm) | un);
+    }
 #pragma unroll
     for (int x = 4; x < AGN_WAVE; x <<= 1) {
         s.ctA = umax64(s.ctA, shfl_xor_u64(s.ctA, x));
@@ -490,19 +656,21 @@ __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
         o_count[i] = s.cnt;
         o_flags[i] = fl;
         o_err[i] = s.first_err >= 0 ? (uint32_t)(k.off + (uint64_t)s.first_err) : 0xffffffffu;
+        if (MSK && o_mask) o_mask[i] = mo;
     }
 }
 
-template <bool ANY_WARM>
+template <bool ANY_WARM, bool MSK>
 __global__ __launch_bounds__(64) void k_counter_quad2(
-    DenseArgs a, const uint64_t *__restrict__ keys, const uint64_t *__restrict__ key_off,
-    const uint64_t *__restrict__ key_len, const uint8_t *__restrict__ key_type,
-    const uint32_t *__restrict__ key_id0, const uint64_t *__restrict__ oc,
-    const uint32_t *__restrict__ op_id, const int64_t *__restrict__ eff,
-    const uint64_t *__restrict__ log_txid, const uint64_t *__restrict__ R,
-    const uint64_t *__restrict__ sct, const uint8_t *__restrict__ sct_ignore,
-    const uint64_t *__restrict__ req_txid, const int64_t *__restrict__ base_value,
-    int64_t *__restrict__ o_value, int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
+    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
+    const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
+    const uint64_t *__restrict__ oc, const uint32_t *__restrict__ op_id,
+    const int64_t *__restrict__ eff, const uint64_t *__restrict__ log_txid,
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ sct,
+    const uint8_t *__restrict__ sct_ignore, const uint64_t *__restrict__ req_txid,
+    const int64_t *__restrict__ base_value, int64_t *__restrict__ o_value,
+    int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
     uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
     uint32_t *__restrict__ o_err) {
     const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
@@ -511,42 +679,70 @@ __global__ __launch_bounds__(64) void k_counter_quad2(
     if (i0 >= a.n_req) return;
     const bool two = i0 + 1u < a.n_req;
     const uint64_t i1 = two ? i0 + 1u : i0;
-    const Q2Key k0 = q2_prologue<ANY_WARM>(a, i0, keys, key_off, key_len, key_type, key_id0, R,
-                                           sct, sct_ignore, req_txid);
-    const Q2Key k1 = q2_prologue<ANY_WARM>(a, i1, keys, key_off, key_len, key_type, key_id0, R,
-                                           sct, sct_ignore, req_txid);
+    const Q2Key k0 = q2_prologue<ANY_WARM, MSK>(a, mk, i0, keys, key_off, key_len, key_type,
+                                                key_id0, R, sct, sct_ignore, req_txid);
+    const Q2Key k1 = q2_prologue<ANY_WARM, MSK>(a, mk, i1, keys, key_off, key_len, key_type,
+                                                key_id0, R, sct, sct_ignore, req_txid);
     Q2Acc s0, s1;
-    s0.ctA = k0.sA;
-    s0.ctB = k0.sB;
-    s1.ctA = k1.sA;
-    s1.ctB = k1.sB;
+    s0.ctA = k0.eA;
+    s0.ctB = k0.eB;
+    s1.ctA = k1.eA;
+    s1.ctB = k1.eB;
     if (a.n_entries != 0) {
         const Q8Chunk c0 = q8_load<true, false>(oc, eff, k0.off, 0, a.n_entries);
         const Q8Chunk c1 = q8_load<true, false>(oc, eff, k1.off, 0, a.n_entries);
         __builtin_amdgcn_sched_barrier(0);
-        if (!k0.corrupt) q2_fold<ANY_WARM>(k0, c0, 0, log_txid, a.n_entries, s0);
-        if (!k1.corrupt) q2_fold<ANY_WARM>(k1, c1, 0, log_txid, a.n_entries, s1);
-        if (!k0.corrupt) q2_rest<ANY_WARM>(k0, oc, eff, log_txid, a.n_entries, s0);
-        if (!k1.corrupt) q2_rest<ANY_WARM>(k1, oc, eff, log_txid, a.n_entries, s1);
+        const bool d0 = !k0.corrupt && (!MSK || k0.uni), d1 = !k1.corrupt && (!MSK || k1.uni);
+        if (d0) q2_fold<ANY_WARM>(k0, c0, 0, log_txid, a.n_entries, s0);
+        if (d1) q2_fold<ANY_WARM>(k1, c1, 0, log_txid, a.n_entries, s1);
+        if (d0) q2_rest<ANY_WARM>(k0, oc, eff, log_txid, a.n_entries, s0);
+        if (d1) q2_rest<ANY_WARM>(k1, oc, eff, log_txid, a.n_entries, s1);
+        if constexpr (MSK) {
+            if (!k0.corrupt && !k0.uni) q2_msk<ANY_WARM>(k0, oc, mk.oc_mask, eff, log_txid, s0);
+            if (!k1.corrupt && !k1.uni) q2_msk<ANY_WARM>(k1, oc, mk.oc_mask, eff, log_txid, s1);
+        }
     }
-    q2_epilogue(k0, s0, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err);
+    q2_epilogue<MSK>(k0, s0, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err,
+                     mk.o_mask);
     if (two)
-        q2_epilogue(k1, s1, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err);
+        q2_epilogue<MSK>(k1, s1, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags,
+                         o_err, mk.o_mask);
+}
+
+MaskArgs mask_args(const agn_log &log, const agn_read &req, const agn_result &out) {
+    MaskArgs m;
+    m.key_mask = log.oc_mask ? log.key_mask : nullptr;
+    m.oc_mask = log.oc_mask;
+    m.R_mask = req.R_mask;
+    m.sct_mask = req.sct ? req.sct_mask : nullptr;
+    m.o_mask = out.lastct_mask;
+    return m;
+}
+
+inline bool sparse_batch(const agn_log &log, const agn_read &req, const agn_result &out) {
+    return log.oc_mask || req.R_mask || (req.sct && req.sct_mask) || out.lastct_mask;
 }
 
 int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u};
+    const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + 1) / 2;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);
-#define AGN_Q2L(W)                                                                              \
-    hipLaunchKernelGGL((k_counter_quad2<W>), dim3((unsigned)nb), dim3(64), 0, st, a, req.keys, \
-                       log.key_off, log.key_len, log.key_type, id0_index(log), log.oc,         \
-                       log.op_id, log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid, \
-                       req.base_value, out.value, out.hole, out.lastct, out.count, out.flags,  \
+#define AGN_Q2L(W, M)                                                                           \
+    hipLaunchKernelGGL((k_counter_quad2<W, M>), dim3((unsigned)nb), dim3(64), 0, st, a, mk,     \
+                       req.keys, log.key_off, log.key_len, log.key_type, id0_index(log), log.oc, \
+                       log.op_id, log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,  \
+                       req.base_value, out.value, out.hole, out.lastct, out.count, out.flags,   \
                        out.err_pos)
-    if (req.sct) AGN_Q2L(true);
-    else AGN_Q2L(false);
+    const bool msk = sparse_batch(log, req, out);
+    if (req.sct) {
+        if (msk) AGN_Q2L(true, true);
+        else AGN_Q2L(true, false);
+    } else {
+        if (msk) AGN_Q2L(false, true);
+        else AGN_Q2L(false, false);
+    }
 #undef AGN_Q2L
     AGN_HIP(hipGetLastError());
     return AGN_OK;
@@ -604,23 +800,24 @@ int counter_variant() {
     return t >= 0 ? t : default_variant<D>();
 }
 
-template <int D, int WPB, int VAR, bool KEYS>
+template <int D, int WPB, int VAR, bool KEYS, bool MSK>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     const char *qv = getenv("AGN_COUNTER_QUAD_NT");
     DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, pair_chunks(),
                 (qv && qv[0] >= '0' && qv[0] <= '3') ? (uint32_t)(qv[0] - '0') : 1u};
+    const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);
     if (req.sct)
-        hipLaunchKernelGGL((k_counter_key<D, true, WPB, VAR, KEYS>), dim3((unsigned)nb),
-                           dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
+        hipLaunchKernelGGL((k_counter_key<D, true, WPB, VAR, KEYS, MSK>), dim3((unsigned)nb),
+                           dim3(64 * WPB), 0, st, a, mk, req.keys, log.key_off, log.key_len,
                            log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
                            req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
                            out.hole, out.lastct, out.count, out.flags, out.err_pos);
     else
-        hipLaunchKernelGGL((k_counter_key<D, false, WPB, VAR, KEYS>), dim3((unsigned)nb),
-                           dim3(64 * WPB), 0, st, a, req.keys, log.key_off, log.key_len,
+        hipLaunchKernelGGL((k_counter_key<D, false, WPB, VAR, KEYS, MSK>), dim3((unsigned)nb),
+                           dim3(64 * WPB), 0, st, a, mk, req.keys, log.key_off, log.key_len,
                            log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
                            req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
                            out.hole, out.lastct, out.count, out.flags, out.err_pos);
@@ -628,10 +825,10 @@ int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out,
     return AGN_OK;
 }
 
-template <int D, int WPB, int VAR>
+template <int D, int WPB, int VAR, bool MSK>
 int launch_key_g(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    return req.keys ? launch_key_k<D, WPB, VAR, true>(log, req, out, st)
-                    : launch_key_k<D, WPB, VAR, false>(log, req, out, st);
+    return req.keys ? launch_key_k<D, WPB, VAR, true, MSK>(log, req, out, st)
+                    : launch_key_k<D, WPB, VAR, false, MSK>(log, req, out, st);
 }
 
 // The variants this D has: VGPR rows always, LDS-DMA rows for even D, quad
@@ -641,14 +838,17 @@ constexpr bool has_variant(int v) {
     return v == ROWS_VGPR || (v == ROWS_GLDS && D % 2 == 0) || (v == ROWS_QUAD && D == 8);
 }
 
-template <int D, int WPB>
+// A sparse batch (presence masks, MSK) runs VGPR or quad rows: the LDS-DMA
+// variant has no per-entry-mask scan for its mixed keys.
+template <int D, int WPB, bool MSK>
 int launch_var(int v, const agn_log &log, const agn_read &req, const agn_result &out,
                hipStream_t st) {
-    if constexpr (D % 2 == 0)
-        if (v == ROWS_GLDS) return launch_key_g<D, WPB, ROWS_GLDS>(log, req, out, st);
+    if constexpr (D % 2 == 0 && !MSK)
+        if (v == ROWS_GLDS) return launch_key_g<D, WPB, ROWS_GLDS, false>(log, req, out, st);
     if constexpr (D == 8)
-        if (v == ROWS_QUAD) return launch_key_g<D, WPB, ROWS_QUAD>(log, req, out, st);
-    return launch_key_g<D, WPB, ROWS_VGPR>(log, req, out, st);
+        if (v == ROWS_QUAD || (MSK && v == ROWS_GLDS))
+            return launch_key_g<D, WPB, ROWS_QUAD, MSK>(log, req, out, st);
+    return launch_key_g<D, WPB, ROWS_VGPR, MSK>(log, req, out, st);
 }
 
 template <int D, int WPB>
@@ -660,7 +860,9 @@ int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, h
     if constexpr (D == 8)
         if (v == ROWS_QUAD2 || (v == ROWS_QUAD && req.sct && forced_variant() < 0))
             return launch_quad2(log, req, out, st);
-    return launch_var<D, WPB>(v == ROWS_QUAD2 ? default_variant<D>() : v, log, req, out, st);
+    const int v2 = v == ROWS_QUAD2 ? default_variant<D>() : v;
+    return sparse_batch(log, req, out) ? launch_var<D, WPB, true>(v2, log, req, out, st)
+                                       : launch_var<D, WPB, false>(v2, log, req, out, st);
 }
 
 // Waves (= requests) per block: 1 measured 1.4-3.4 % faster than 2 and
@@ -670,6 +872,32 @@ template <int D>
 int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
     return launch_key<D, 1>(log, req, out, st);
+}
+
+// agn_log_index_masks: one wave per key; out[k] = the mask word every entry
+// of the segment carries (low D bits), 0 when they differ or the key is empty.
+__global__ __launch_bounds__(256) void k_index_masks(const uint64_t *__restrict__ key_off,
+                                                    const uint64_t *__restrict__ key_len,
+                                                    const uint64_t *__restrict__ oc_mask,
+                                                    uint64_t full, uint64_t n_keys,
+                                                    uint64_t *__restrict__ out) {
+    const uint64_t k = uniform_u64((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (k >= n_keys) return;
+    const int lane = lane_id();
+    const uint64_t off = key_off[k];
+    const uint64_t n = key_len ? key_len[k] : key_off[k + 1] - off;
+    if (n == 0 || oc_mask == nullptr) {
+        if (lane == 0) out[k] = n ? full : 0ull;
+        return;
+    }
+    const uint64_t m0 = uniform_u64(oc_mask[off]) & full;
+    bool ok = true;
+    for (uint64_t b = 0; ok && b < n; b += AGN_WAVE) {
+        const uint64_t p = b + (uint64_t)lane;
+        const bool bad = p < n && (oc_mask[off + p] & full) != m0;
+        ok = ballot(bad) == 0;
+    }
+    if (lane == 0) out[k] = ok ? m0 : 0ull;
 }
 
 // agn_log_index_ids: one wave per key, lanes over the segment's positions.
@@ -697,6 +925,17 @@ __global__ __launch_bounds__(256) void k_index_ids(const uint64_t *__restrict__ 
 }
 
 }  // namespace
+
+int launch_index_masks(const agn_log &log, uint64_t *out, hipStream_t st) {
+    const uint64_t nb = (log.n_keys + 3) / 4;
+    if (nb == 0) return AGN_OK;
+    if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "index_masks: too many keys");
+    if (log.n_dcs > 64) return fail(AGN_ENOTSUP, "index_masks: n_dcs %u > 64", log.n_dcs);
+    hipLaunchKernelGGL(k_index_masks, dim3((unsigned)nb), dim3(256), 0, st, log.key_off,
+                       log.key_len, log.oc_mask, low_bits(log.n_dcs), log.n_keys, out);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
 
 int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st) {
     const uint64_t nb = (log.n_keys + 3) / 4;
@@ -731,7 +970,7 @@ int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, h
             const int var = (r & 1) ? NV - 1 - k : k;  // alternate which variant goes first
             if (!has_variant<D>(var)) continue;
             if (hipEventRecord(e0, st) != hipSuccess) { rc = fail(AGN_EHIP, "tune: record"); break; }
-            rc = launch_var<D, 1>(var, log, req, out, st);
+            rc = launch_var<D, 1, false>(var, log, req, out, st);
             if (rc) break;
             float t = 0.f;
             if (hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
@@ -760,7 +999,7 @@ int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, h
 // AGN_ENOTSUP otherwise so the caller uses the general kernel.
 int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                          hipStream_t st) {
-    if (log.oc_mask || req.R_mask || req.sct_mask || out.lastct_mask) return AGN_ENOTSUP;
+    // presence masks (D <= 8: one word per clock) run the MSK instantiations
     switch (log.n_dcs) {
         case 1: return launch_dense<1>(log, req, out, st);
         case 2: return launch_dense<2>(log, req, out, st);

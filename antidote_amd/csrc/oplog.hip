@@ -149,11 +149,12 @@ __global__ void __launch_bounds__(256) k_scatter_rows(uint64_t *__restrict__ oc,
     oc[dst[i] * D + (j - i * D)] = rows[j];
 }
 
-constexpr int KV = 5;  // k_keys record: key, start, len, id0, ListLen
+constexpr int KV = 6;  // k_keys record: key, start, len, id0, ListLen, DC set (key_mask)
 __global__ void __launch_bounds__(256) k_keys(uint64_t *__restrict__ key_off,
                                               uint64_t *__restrict__ key_len,
                                               uint32_t *__restrict__ key_id0,
-                                              uint32_t *__restrict__ key_lcap, uint64_t n,
+                                              uint32_t *__restrict__ key_lcap,
+                                              uint64_t *__restrict__ key_mask, uint64_t n,
                                               const uint64_t *__restrict__ kv) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -162,6 +163,7 @@ __global__ void __launch_bounds__(256) k_keys(uint64_t *__restrict__ key_off,
     key_len[k] = kv[KV * i + 2];
     key_id0[k] = (uint32_t)kv[KV * i + 3];
     key_lcap[k] = (uint32_t)kv[KV * i + 4];
+    if (key_mask) key_mask[k] = kv[KV * i + 5];
 }
 
 // relayout: every key's segment from arena a into fresh arena b (one wave per key)
@@ -267,6 +269,11 @@ struct agn_oplog {
     std::vector<uint64_t> start, tstart;     // physical segments
     std::vector<uint32_t> cap, tcap, counter;
     std::vector<uint32_t> s_cnt, s_tcnt;     // staged (not yet flushed) entries / tokens
+    // sparse logs with D <= 64: the DC set every entry of the key carries, 0
+    // when they differ (agn_log.key_mask; set by the first append to an empty
+    // key, cleared by an entry with another set; a GC only removes entries,
+    // so a shared set stays shared)
+    std::vector<uint64_t> umask;
     // pinned [6][K]: length (staged included), token length, ListLen, key_id0,
     // live range start (entry slot, token slot); a prune's D2H lands here
     // directly (settled by the next host call), then [3] u64 totals
@@ -290,6 +297,7 @@ struct agn_oplog {
     uint64_t *key_off = nullptr, *key_len = nullptr;
     uint32_t *key_id0 = nullptr;   // consecutive-id index, kept with key_off / key_len
     uint32_t *key_lcap = nullptr;  // ListLen (the in-place prune applies the resize policy)
+    uint64_t *key_mask = nullptr;  // sparse, D <= 64: umask on the device (agn_log.key_mask)
     uint32_t *d_meta = nullptr;    // [6][K] prune output, copied into `meta`
     hipEvent_t up_done = nullptr, gc_done = nullptr;
     bool up_pending = false, gc_pending = false;
@@ -474,6 +482,7 @@ void fill_view(const agn_oplog *L, agn_log *v) {
     v->rem_off = L->a.rem_off;
     v->rem_tok = L->a.tok;
     v->key_id0 = L->key_id0;
+    v->key_mask = L->key_mask;
 }
 
 int do_flush(agn_oplog *L, hipStream_t st) {
@@ -532,6 +541,7 @@ int do_flush(agn_oplog *L, hipStream_t st) {
             kv[KV * j + 2] = L->len[k];
             kv[KV * j + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
             kv[KV * j + 4] = L->lcap[k];
+            kv[KV * j + 5] = L->umask.empty() ? 0ull : L->umask[k];
         }
     }
     char *d = nullptr;
@@ -554,7 +564,7 @@ int do_flush(agn_oplog *L, hipStream_t st) {
     }
     if (nk)
         k_keys<<<(unsigned)((nk + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, L->key_id0,
-                                                              L->key_lcap, nk,
+                                                              L->key_lcap, L->key_mask, nk,
                                                               (const uint64_t *)(d + o_keys));
     AGN_HIP(hipGetLastError());
     AGN_HIP(hipFreeAsync(d, st));
@@ -632,6 +642,7 @@ int relayout(agn_oplog *L, hipStream_t st) {
         kv[KV * k + 2] = L->len[k];
         kv[KV * k + 3] = L->len[k] ? L->id0[k] : AGN_ID0_NONE;
         kv[KV * k + 4] = L->lcap[k];
+        kv[KV * k + 5] = L->umask.empty() ? 0ull : L->umask[k];
     }
     e = hipMemcpyAsync(d_mv, h, mv.size() * sizeof(Move), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) e = hipMemcpyAsync(d_kv, kv, K * KV * 8, hipMemcpyHostToDevice, st);
@@ -646,7 +657,7 @@ int relayout(agn_oplog *L, hipStream_t st) {
     // commit: the new key_off (the copy above read the old arena first)
     if (K)
         k_keys<<<(unsigned)((K + 255) / 256), 256, 0, st>>>(L->key_off, L->key_len, L->key_id0,
-                                                             L->key_lcap, K, d_kv);
+                                                             L->key_lcap, L->key_mask, K, d_kv);
     (void)hipEventRecord(L->up_done, st);
     L->up_pending = true;
     (void)hipFreeAsync(d_mv, st);
@@ -702,6 +713,7 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
         for (auto *v : {&L->cap, &L->tcap, &L->counter, &L->s_cnt, &L->s_tcnt}) v->assign(n_keys, 0);
         L->dirty.assign(n_keys, 0);
         L->move_of.assign(n_keys, -1);
+        if (L->sparse && n_dcs <= 64) L->umask.assign(n_keys, 0);
     } catch (...) {
         delete L;
         return fail(AGN_ENOMEM, "oplog_create: host metadata for %llu keys",
@@ -729,6 +741,8 @@ int agn_oplog_create(agn_ctx *ctx, uint32_t crdt_type, uint32_t n_dcs, uint64_t 
     if (e == hipSuccess) e = hipMemset(L->key_id0, 0xff, K1 * 4);
     if (e == hipSuccess) e = hipMalloc((void **)&L->key_lcap, K1 * 4);
     if (e == hipSuccess) e = hipMemset(L->key_lcap, 0, K1 * 4);
+    if (e == hipSuccess && !L->umask.empty()) e = hipMalloc((void **)&L->key_mask, K1 * 8);
+    if (e == hipSuccess && L->key_mask) e = hipMemset(L->key_mask, 0, K1 * 8);
     if (e == hipSuccess) e = hipMalloc((void **)&L->d_meta, 6 * K1 * 4 + 3 * 8);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L->up_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L->gc_done, hipEventDisableTiming);
@@ -748,7 +762,8 @@ int agn_oplog_destroy(agn_oplog *L) {
     for (void *p : {(void *)a.oc, (void *)a.mask, (void *)a.txid, (void *)a.add, (void *)a.op_id,
                     (void *)a.tag, (void *)a.rem_off, (void *)a.eff, (void *)a.tok,
                     (void *)L->key_off, (void *)L->key_len, (void *)L->key_id0,
-                    (void *)L->key_lcap, (void *)L->d_meta, (void *)L->d_lmeta})
+                    (void *)L->key_lcap, (void *)L->key_mask, (void *)L->d_meta,
+                    (void *)L->d_lmeta})
         if (p) (void)hipFree(p);
     if (L->pinned) (void)hipHostFree(L->pinned);
     if (L->meta) (void)hipHostFree(L->meta);
@@ -839,6 +854,10 @@ static int oplog_append_locked(agn_oplog *L, uint64_t n, const uint64_t *keys,
         // consecutive ids (op_id[p] == id0 + p) survive appends until a
         // same_op entry or a gap; AGN_ID0_NONE itself is never an id base
         const uint32_t p = L->len[k];
+        if (!L->umask.empty()) {
+            const uint64_t m = oc_mask[i * W] & low_bits(D);
+            L->umask[k] = (p == 0) ? m : (L->umask[k] == m ? m : 0ull);
+        }
         if (p == 0) L->id0[k] = id;
         else if (L->id0[k] != AGN_ID0_NONE && (uint64_t)id != (uint64_t)L->id0[k] + p)
             L->id0[k] = AGN_ID0_NONE;

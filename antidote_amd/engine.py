@@ -125,6 +125,18 @@ class Engine:
             dlog.bufs["key_id0"] = b
         return b
 
+    def index_masks(self, dlog, stream=None) -> DevBuf:
+        """Build agn_log.key_mask (the DC set every entry of a key carries, 0
+        when they differ; agn_log_index_masks) for a device log and attach it."""
+        ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
+        b = self.empty(max(1, int(ls.n_keys)) * 8)
+        check(self.lib.agn_log_index_masks(self.ctx, C.byref(ls), b.ptr, stream),
+              "agn_log_index_masks")
+        ls.key_mask = b.ptr
+        if isinstance(dlog, DeviceArrays):
+            dlog.bufs["key_mask"] = b
+        return b
+
     def alloc_log_like(self, log: EncodedLog) -> DeviceArrays:
         """Device arrays with the sizes (and presence) of `log`'s (agn_prune_ops output)."""
         s = _abi.AgnLog()

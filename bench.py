@@ -79,6 +79,11 @@ def parse():
                          "synthetic partition log")
     ap.add_argument("--gc", action="store_true",
                     help="also time the op-log GC (agn_prune_ops) over the whole log")
+    ap.add_argument("--sparse", default="",
+                    help="presence masks on every clock (the log the Erlang NIF builds): "
+                         "'full' = every DC in every clock, 'subsetN' = the first N DCs in every "
+                         "clock (a partition of width D with N interned DCs), 'mixed' = 1 op in 8 "
+                         "lacks one random DC (genuinely sparse clocks); counter_pn configs")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-staged read path (keys + R from pinned host "
                          "memory, results back to pinned host memory; PCIe-inclusive)")
@@ -136,20 +141,48 @@ def algorithmic_bytes_survey(cfg, n_keys, n_rem=0, n_live=0):
     return ops * (8 * D + 20) + 8 * n_rem + 12 * n_live + n_keys * (32 + 16 * D)
 
 
-def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0):
-    """HBM bytes one materialize launch must move."""
+def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0, mask_keys=0, mask_ops=0):
+    """HBM bytes one materialize launch must move.
+    Presence masks (--sparse) add per request its key's DC set, R's mask word
+    and the LastOpCt mask word (mask_keys requests), and the per-entry mask
+    word of the keys whose entries differ (mask_ops entries)."""
     D, N = cfg["n_dcs"], cfg["ops_per_key"]
     ops = n_keys * N
     if cfg["crdt_type"] == 1:
         per_op = 8 * D + 8                    # OpSSCommit row + effect
         per_key = 8 + 8 * D + 8 * D + 32      # key_off, R, LastOpCt, value/hole/count/flags/err/op_id
-        return ops * per_op + n_keys * per_key
+        return ops * per_op + n_keys * per_key + 24 * mask_keys + 8 * mask_ops
     per_op = 8 * D + 4 + 4 + 8 + 4            # oc, op_id, tag, add_tok, rem_off
     per_key = 8 + 8 * D + 8 * D + 24 + 8 + 4  # key_off, R, LastOpCt, hole/count/flags/err, out_off, out_n
     return ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key
 
 
-def cpu_baseline(cfg, n_keys, threads, target_s=10.0):
+def presence_masks(mode, D, n_ops, n_keys, rng=None, torch=None):
+    """The --sparse masks: (oc_mask[n_ops], R_mask[n_keys]) as int64 words,
+    torch tensors on the device (torch given) or numpy arrays."""
+    full = (1 << D) - 1
+    if mode.startswith("subset"):
+        full = (1 << int(mode[6:])) - 1
+    elif mode not in ("full", "mixed"):
+        raise SystemExit(f"--sparse {mode}: want full, mixed or subsetN")
+    if torch is not None:
+        ocm = torch.full((n_ops,), full, dtype=torch.int64, device="cuda")
+        if mode == "mixed":
+            g = torch.Generator(device="cuda").manual_seed(20250112)
+            drop = torch.rand(n_ops, device="cuda", generator=g) < 0.125
+            d = torch.randint(0, D, (n_ops,), device="cuda", generator=g)
+            ocm = torch.where(drop, ocm & ~torch.bitwise_left_shift(torch.ones_like(d), d), ocm)
+        rm = torch.full((n_keys,), full, dtype=torch.int64, device="cuda")
+        return ocm, rm
+    ocm = np.full(n_ops, full, np.uint64)
+    if mode == "mixed":
+        drop = rng.random(n_ops) < 0.125
+        d = rng.integers(0, D, n_ops).astype(np.uint64)
+        ocm[drop] &= ~(np.uint64(1) << d[drop])
+    return ocm.reshape(n_ops, 1), np.full((n_keys, 1), full, np.uint64)
+
+
+def cpu_baseline(cfg, n_keys, threads, target_s=10.0, sparse=""):
     """The C oracle (oracle/liboracle.so, a restatement of the Erlang path) on a
     bounded host-generated sample of the same workload.  Each chunk of the
     sample is materialized `reps` times so that the timed CPU work is about
@@ -173,7 +206,11 @@ def cpu_baseline(cfg, n_keys, threads, target_s=10.0):
         hl, hr = gen_host(g)
         cap = (np.arange(k + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
                if cfg["crdt_type"] != 1 else None)
-        res = alloc_result(k, cfg["n_dcs"], sparse=False, cap_off=cap)
+        res = alloc_result(k, cfg["n_dcs"], sparse=bool(sparse), cap_off=cap)
+        if sparse:  # the same mask mode on the host sample (library arrays stay the library's)
+            ocm, rm = presence_masks(sparse, cfg["n_dcs"], int(hl.n_entries), k,
+                                     rng=np.random.default_rng(done))
+            hl.oc_mask, hr.R_mask = ocm.ctypes.data, rm.ctypes.data
         os_ = result_struct(res)
         for nt in tcounts:
             r = 0
@@ -188,6 +225,8 @@ def cpu_baseline(cfg, n_keys, threads, target_s=10.0):
                     reps[nt] = max(1, int(np.ceil(target_s / (secs[nt] * n_chunks))))
                 if r >= reps[nt]:
                     break
+        if sparse:
+            hl.oc_mask = hr.R_mask = None
         free_gen_host(hl, hr)
         done += k
     return {nt: work[nt] / secs[nt] for nt in tcounts}, {nt: secs[nt] for nt in tcounts}, reps
@@ -256,7 +295,22 @@ def main():
     cap = None
     if cfg["crdt_type"] != 1:
         cap = np.arange(n_keys + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
-    res = eng.alloc_result(n_keys, cfg["n_dcs"], sparse=False, cap_off=cap)
+    presence = None
+    if a.sparse:
+        # presence masks on every clock, as the Erlang NIF's partition logs
+        # carry them; agn_log.key_mask as the engine-owned op log maintains it
+        if cfg["crdt_type"] != 1:
+            raise SystemExit("--sparse: counter_pn configs (1, 2)")
+        ocm_t, rm_t = presence_masks(a.sparse, cfg["n_dcs"], int(dl.n_entries), n_keys,
+                                     torch=torch)
+        dl.oc_mask, dr.R_mask = ocm_t.data_ptr(), rm_t.data_ptr()
+        kmask = eng.index_masks(dl, sp)
+        km = eng.download(kmask, np.uint64, (n_keys,), stream=sp)
+        mixed = int((km == 0).sum())
+        presence = {"mode": a.sparse, "key_mask": "agn_log_index_masks",
+                    "uniform_keys": n_keys - mixed, "mixed_keys": mixed,
+                    "mask_ops": mixed * cfg["ops_per_key"]}
+    res = eng.alloc_result(n_keys, cfg["n_dcs"], sparse=bool(a.sparse), cap_off=cap)
 
     def barrier():
         if world > 1:
@@ -314,7 +368,9 @@ def main():
 
     ops_step = n_keys * cfg["ops_per_key"] * world
     value = ops_step * a.steps / elapsed
-    bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live)
+    bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live,
+                                     n_keys if presence else 0,
+                                     presence["mask_ops"] if presence else 0)
     bytes_survey = algorithmic_bytes_survey(cfg, n_keys, n_rem, n_live)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
 
@@ -338,7 +394,7 @@ def main():
         n_cpu = a.cpu_keys if a.cpu_keys >= 0 else 64_000_000 // cfg["ops_per_key"]
         if world == 1 and n_cpu > 0:
             thr = a.cpu_threads or min(16, os.cpu_count() or 1)
-            rates, secs, reps = cpu_baseline(cfg, min(n_cpu, n_keys), thr)
+            rates, secs, reps = cpu_baseline(cfg, min(n_cpu, n_keys), thr, sparse=a.sparse)
             cpu = {"value": rates[1], "unit": "ops/s", "cores": 1, "kind": "port",
                    "sample": f"{min(n_cpu, n_keys)} keys x {cfg['ops_per_key']} ops of the same "
                              f"workload (host-generated, same SplitMix64 streams), "
@@ -346,8 +402,11 @@ def main():
                              f"{secs[1]:.1f} s of CPU time",
                    "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
-        traffic, traffic_src = pmc_traffic(a.config, n_keys)
+        traffic, traffic_src = pmc_traffic(a.config, n_keys,
+                                           f"cfg{a.config}_sparse_{a.sparse}" if a.sparse else None)
         workload = cfg["name"].format(keys=fmt_keys(n_keys))
+        if a.sparse:
+            workload += f", presence masks on every clock ({a.sparse})"
         line = {
             "metric": "materialized ops/sec + VC compares/sec (1/2/4/8 GPU), % of HBM roofline",
             "value": value, "unit": "ops/s", "n_gpus": world, "steps": a.steps,
@@ -376,6 +435,8 @@ def main():
             "error_keys": err_keys, "mean_included_ops": float(count.mean()),
             "gen_s": t_gen,
         }
+        if presence:
+            line["presence"] = presence
         if gst:
             line["gst"] = gst
         if post_gc:
@@ -390,6 +451,8 @@ def main():
             line["e2e"] = e2e
         print(json.dumps(line), flush=True)
 
+    if presence:  # the masks are torch's, not the generator's
+        dl.oc_mask = dr.R_mask = dl.key_mask = None
     eng.free_gen(dl, dr)
     eng.close()
     if world > 1:

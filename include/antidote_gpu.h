@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AGN_ABI_VERSION 3
+#define AGN_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define AGN_OK 0
@@ -104,6 +104,19 @@ typedef struct agn_log {
      * a GC prune leaves gaps (:576-585); built by agn_log_index_ids.  Lets the
      * counter kernel derive NewLastOp without a dependent op_id load. */
     const uint32_t *key_id0;
+    /* ABI v4, optional (NULL = look at the per-entry masks only; D <= 64): per
+     * key, the presence word that EVERY entry of its segment carries
+     * (oc_mask[e] & low D bits, the same for all e of the key), or 0 when the
+     * key's entries differ (or it is not known).  A dict clock carries the
+     * DCs the DC knew of when it was taken (include/antidote.hrl:188), so in a
+     * steady deployment every op of a key has the same DC set U.  When U is a
+     * subset of the read snapshot's DCs, is_op_in_snapshot's dict fold
+     * (src/clocksi_materializer.erl:236-258) is a plain element-wise compare
+     * over U's columns, and LastOpCt's DC set is SCT's united with U when
+     * any op was included -- so the dense row-scan kernels serve the key
+     * exactly, without reading a mask per op.  Built by agn_log_index_masks;
+     * maintained by the engine-owned agn_oplog. */
+    const uint64_t *key_mask;
 } agn_log;
 
 #define AGN_ID0_NONE 0xFFFFFFFFu
@@ -209,6 +222,13 @@ int agn_tune(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_result *
  * The caller owns out ([n_keys] u32, device) and sets log.key_id0 = out; the
  * index must be rebuilt whenever op ids change (append past a gap, prune). */
 int agn_log_index_ids(agn_ctx *ctx, const agn_log *log, uint32_t *out, void *stream);
+
+/* agn_log.key_mask for a device log with presence masks and D <= 64:
+ * out[k] = the presence word all of key k's entries share (low D bits), or 0
+ * when they differ or the key is empty.  The caller owns out ([n_keys] u64,
+ * device) and sets log.key_mask = out; rebuild it when entries change.  A
+ * log without oc_mask gets every key's full word (all D DCs present). */
+int agn_log_index_masks(agn_ctx *ctx, const agn_log *log, uint64_t *out, void *stream);
 
 /* Upper bound of live pairs per request for set/register types:
  * writes cap_off[n_req+1] (host pointers): cap = #adding entries of the key

@@ -51,7 +51,8 @@ def test_struct_layout_matches_c():
 int main(void) {
   printf("agn_log %zu\nagn_read %zu\nagn_result %zu\nagn_gen_cfg %zu\n", sizeof(agn_log),
          sizeof(agn_read), sizeof(agn_result), sizeof(agn_gen_cfg));
-  F(agn_log, rem_tok) F(agn_log, eff) F(agn_read, req_type) F(agn_read, base_tok)
+  F(agn_log, rem_tok) F(agn_log, eff) F(agn_log, key_id0) F(agn_log, key_mask)
+  F(agn_read, req_type) F(agn_read, base_tok)
   F(agn_result, out_tok) F(agn_result, err_pos) F(agn_gen_cfg, warm) F(agn_gen_cfg, key_stride)
   return 0; }
 '''

@@ -1,0 +1,274 @@
+"""Presence masks on the dense counter kernels (ABI v4, agn_log.key_mask).
+
+The reference's clocks are dicts (include/antidote.hrl:188): a DC missing
+from an op's OpSSCommit is not compared, a DC of the op missing from the read
+snapshot excludes it (src/clocksi_materializer.erl:245-247), a DC missing
+from SCT reads 0, and LastOpCt's DC set is SCT's united with the included
+ops' (:249-256).  The Erlang NIF builds every partition log with presence
+masks (nif_part_open, sparse = 1), so these are the semantics the drop-in
+runs.  Covered here, each against the C oracle (or the reference's ETS
+transcription) bit for bit:
+
+  * keys whose entries all carry one DC set U (the steady state: the dense
+    row scan with U's columns only) and keys whose entries differ (the
+    per-entry-mask scan), mixed in one batch, cold and warm, through every
+    counter kernel (VGPR rows, quad rows, two requests per wave, general);
+    absent columns hold garbage, present ones sometimes 0;
+  * agn_log_index_masks against numpy;
+  * a log whose masks are all full equals the dense log;
+  * the NIF's call sequence on a sparse engine-owned log (one DC joining
+    halfway) equals the same sequence on a dense log and the reference's
+    transcription.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from antidote_amd import _abi
+from antidote_amd.encode import alloc_result, log_struct, read_struct, result_struct
+from antidote_amd.engine import Batcher, OpLog
+from oracle import py_oracle as po
+from synth import compare, random_case
+
+pytestmark = pytest.mark.gpu
+
+
+def presence_case(seed, K, D, nmax, *, p_uniform=0.7, p_cover=0.85, garbage=True, warm=0.4,
+                  **kw):
+    """random_case with per-key DC sets: a fraction p_uniform of the keys have
+    one DC set U on every entry; R covers U for a fraction p_cover of the
+    reads; absent columns of op rows, R and SCT hold garbage."""
+    log, req, cap = random_case(seed, _abi.COUNTER_PN, K, D, nmax, sparse=True, warm=warm, **kw)
+    rng = np.random.default_rng(seed + 1)
+    full = (1 << D) - 1
+    keys = req.keys
+    inv = np.empty(K, np.int64)
+    inv[keys.astype(np.int64)] = np.arange(K)
+    for k in range(K):
+        a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+        i = inv[k]
+        if rng.random() < p_uniform:
+            U = int(rng.integers(1, full + 1))
+            log.oc_mask[a:b, 0] = np.uint64(U)
+        else:
+            U = int(np.bitwise_or.reduce(log.oc_mask[a:b, 0])) if b > a else full
+        if rng.random() < p_cover:
+            req.R_mask[i, 0] = np.uint64(U | int(rng.integers(0, full + 1)))
+        # a few present values are 0 (a DC at time 0 is still present)
+        z = rng.random((b - a, D)) < 0.02
+        log.oc[a:b][z] = 0
+    if garbage:
+        big = lambda shape: rng.integers(1 << 40, 1 << 62, shape, dtype=np.int64).astype(np.uint64)  # noqa: E731
+        bits = ((log.oc_mask[:, :1] >> np.arange(D, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+        log.oc[~bits] = big(int((~bits).sum()))
+        rb = ((req.R_mask[:, :1] >> np.arange(D, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+        req.R[~rb] = big(int((~rb).sum()))
+        sb = ((req.sct_mask[:, :1] >> np.arange(D, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+        req.sct[~sb] = big(int((~sb).sum()))
+    return log, req
+
+
+def oracle_result(oracle_lib, log, req):
+    res = alloc_result(req.n_req, log.n_dcs, sparse=True)
+    ls, rs, os_ = log_struct(log), read_struct(req, sparse=True), result_struct(res)
+    assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
+    return res
+
+
+def device_result(eng, log, req, index):
+    dl, dr = eng.upload_log(log), eng.upload_read(req, sparse=True)
+    if index:
+        eng.index_masks(dl)
+    dres = eng.alloc_result(req.n_req, log.n_dcs, sparse=True)
+    eng.materialize(dl, dr, dres)
+    return eng.fetch_result(dres)
+
+
+IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3"}
+
+
+@pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
+@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general"])
+@pytest.mark.parametrize("D", [1, 3, 5, 8])
+def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
+    monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
+    monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
+    if impl == "general":
+        monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
+    else:
+        monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    log, req = presence_case(1000 * D + len(impl) + len(path), 260, D, 150, txid=0.3,
+                             invalid=0.02, corrupt=0.03, identity=(D % 2 == 0))
+    want = oracle_result(oracle_lib, log, req)
+    if path == "host":
+        got = eng.materialize_host(log, req, sparse=True)
+    else:
+        got = device_result(eng, log, req, index=(path == "device_indexed"))
+    bad = compare(_abi.COUNTER_PN, D, got, want, True, req.n_req)
+    assert not bad, bad[:10]
+    # absent LastOpCt columns are 0, as the oracle writes them
+    m = got.lastct_mask[:, 0]
+    for d in range(D):
+        absent = ((m >> np.uint64(d)) & np.uint64(1)) == 0
+        assert not got.lastct[absent, d].any()
+
+
+@pytest.mark.parametrize("D", [3, 8, 40, 64])
+def test_index_masks_vs_numpy(eng, D):
+    log, req, _ = random_case(77 + D, _abi.COUNTER_PN, 500, D, 90, sparse=True)
+    rng = np.random.default_rng(D)
+    full = (1 << D) - 1 if D < 64 else (1 << 64) - 1
+    for k in range(500):
+        a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+        if rng.random() < 0.6:
+            log.oc_mask[a:b, 0] = np.uint64(int(rng.integers(1, 1 << 62)) | (1 << 63))
+    dl = eng.upload_log(log)
+    buf = eng.index_masks(dl)
+    got = eng.download(buf, np.uint64, (500,))
+    want = np.zeros(500, np.uint64)
+    for k in range(500):
+        a, b = int(log.key_off[k]), int(log.key_off[k + 1])
+        if b == a:
+            continue
+        ms = log.oc_mask[a:b, 0] & np.uint64(full)
+        if (ms == ms[0]).all():
+            want[k] = ms[0]
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2"])
+@pytest.mark.parametrize("D", [3, 8])
+def test_full_masks_equal_dense(eng, monkeypatch, D, impl):
+    """Every DC present everywhere: the masked batch equals the dense one, and
+    LastOpCt's DC set is all of them (or empty when LastOpCt is ignore)."""
+    monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS[impl])
+    log, req, _ = random_case(515 + D, _abi.COUNTER_PN, 400, D, 200, sparse=True, warm=0.5,
+                              txid=0.3, invalid=0.02, corrupt=0.03)
+    full = np.uint64((1 << D) - 1)
+    log.oc_mask[:] = full
+    req.R_mask[:] = full
+    req.sct_mask[:] = full
+    dense = eng.materialize_host(log, req, sparse=False)
+    masked = eng.materialize_host(log, req, sparse=True)
+    assert not compare(_abi.COUNTER_PN, D, masked, dense, False, req.n_req)
+    ign = (masked.flags & _abi.F_CT_IGNORE) != 0
+    corrupt = (masked.flags & _abi.F_ERR_CORRUPTED) != 0
+    ok = ~corrupt
+    assert (masked.lastct_mask[ok & ~ign, 0] == full).all()
+    assert (masked.lastct_mask[ok & ign, 0] == 0).all()
+
+
+# ---------------------------------------------------------------- the NIF's sequence
+DCAP = 8      # columns of the partition (nif_part_open's D)
+JOIN = 1500   # step at which a fourth DC joins
+
+
+class DictWorkload:
+    """Dict clocks over interned DC columns, as nif clock_row builds them:
+    DCs 0..2 from the start, DC 3 from step JOIN on."""
+
+    def __init__(self, seed, K):
+        self.rng = np.random.default_rng(seed)
+        self.clk = np.zeros(DCAP, np.int64)
+        self.clk[:3] = 1000
+        self.n_dc = 3
+        self.K = K
+
+    def join(self):
+        self.clk[3] = 1000
+        self.n_dc = 4
+
+    def mask(self, n=None):
+        return np.uint64((1 << (self.n_dc if n is None else n)) - 1)
+
+    def op(self):
+        n = self.n_dc
+        c = int(self.rng.integers(0, n))
+        ss = np.zeros(DCAP, np.int64)
+        ss[:n] = np.maximum(self.clk[:n] - self.rng.integers(0, 40, n), 0)
+        self.clk[c] += int(self.rng.integers(1, 30))
+        oc = ss.copy()
+        oc[c] = self.clk[c]
+        return c, ss, int(self.clk[c]), oc, int(self.rng.integers(-50, 51))
+
+    def read(self):
+        lag = 400 if self.rng.random() < 0.85 else 20000
+        n = self.n_dc
+        if n == 4 and self.rng.random() < 0.1:
+            n = 3   # a reader whose snapshot predates the new DC
+        R = np.zeros(DCAP, np.int64)
+        R[:n] = np.maximum(self.clk[:n] - self.rng.integers(0, lag, n), 0)
+        return R, self.mask(n)
+
+
+def dvc(row, n):
+    return {d: int(row[d]) for d in range(n)}
+
+
+@pytest.mark.parametrize("read6", ["1", "0"])
+def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6):
+    """update/2 + read/6 as nif/antidote_gpu_nif.c issues them, on a sparse
+    log (presence masks; the NIF's configuration) and on a dense log: every
+    read bit-identical between the two (value, NewLastOp, LastOpCt, Count,
+    flags, cache status), LastOpCt's DC set inside the DCs known at the read,
+    and every served value equal to the reference's ETS transcription."""
+    monkeypatch.setenv("AGN_READ6", read6)
+    K, steps = 24, 3500
+    w = DictWorkload(23, K)
+    vn = po.MaterializerVnode()
+    quirk, served, n_cmp = set(), 0, 0
+    with OpLog(eng, _abi.COUNTER_PN, DCAP, K, sparse=True) as ls, \
+            OpLog(eng, _abi.COUNTER_PN, DCAP, K, sparse=False) as ld, \
+            Batcher(ls, max_batch=8, cached=True) as bs, \
+            Batcher(ld, max_batch=8, cached=True) as bd:
+        for s in range(steps):
+            if s == JOIN:
+                w.join()
+            key = int(w.rng.integers(0, K))
+            if w.rng.random() < 0.7:
+                n = w.n_dc
+                c, ss, ct, oc, eff = w.op()
+                pay = po.Payload(key, po.COUNTER_PN, eff, dvc(ss, n), (c, ct), s + 1)
+                try:
+                    vn.update(key, pay)
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                for ol, bt, sparse in ((ls, bs, True), (ld, bd, False)):
+                    if ol.gc_due(key)[0]:
+                        bt.read(key, R=ss.astype(np.uint64),
+                                R_mask=np.array([w.mask()]) if sparse else None, gc=True)
+                    ol.append(np.array([key], np.uint64), oc.reshape(1, DCAP).astype(np.uint64),
+                              oc_mask=np.array([[w.mask()]]) if sparse else None,
+                              eff=np.array([eff], np.int64), txid=np.array([s + 1], np.uint64))
+                if vn.ops_cache.get(key) and any(vn.ops_cache[key][po.FIRST_OP - 1 + i] == 0
+                                                 for i in range(vn.ops_cache[key][1][0])):
+                    quirk.add(key)
+            else:
+                R, Rm = w.read()
+                gs = bs.read(key, R=R.astype(np.uint64), R_mask=np.array([Rm]))
+                gd = bd.read(key, R=R.astype(np.uint64))
+                for f in ("status", "value", "hole", "count", "flags"):
+                    assert gs[f] == gd[f], (s, key, f, gs[f], gd[f])
+                if gs["status"] != _abi.SS_LOG:
+                    assert np.array_equal(gs["lastct"], gd["lastct"]), (s, key)
+                    assert (int(gs["lastct_mask"][0]) & ~int(w.mask())) == 0, (s, key)
+                    n_cmp += 1
+                if key in quirk:
+                    continue
+                try:
+                    want = vn.read(key, po.COUNTER_PN, dvc(R, int(Rm).bit_length()), po.IGNORE)
+                except NotImplementedError:
+                    assert gs["status"] == _abi.SS_LOG, (s, key)
+                    continue
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                    continue
+                assert gs["status"] in (_abi.SS_HIT, _abi.SS_NEW), (s, key, gs["status"])
+                assert want == ("ok", gs["value"]), (s, key, want, gs["value"])
+                served += 1
+        lns, lls, cts = ls.key_meta()
+        lnd, lld, ctd = ld.key_meta()
+    assert served > 600 and n_cmp > 800, (served, n_cmp)
+    assert np.array_equal(lns, lnd) and np.array_equal(lls, lld) and np.array_equal(cts, ctd)

@@ -16,8 +16,13 @@
 // partitions, per-read latency percentiles, mean batch size and read
 // statuses as one JSON line.
 //
-//   serve_bench [keys=N] [ops=N] [dcs=N] [parts=N] [threads=N] [reads=N]
-//               [batch=N] [wait=US] [wps=N] [hot=N]
+// sparse=1 builds the logs the way the Erlang NIF does (nif_part_open,
+// nif/antidote_gpu_nif.c): presence masks on every clock (the op rows, the
+// reads' R, LastOpCt), `dcs` columns of which the first `present` are
+// interned DCs (the rest absent from every dict clock).
+//
+//   serve_bench [keys=N] [ops=N] [dcs=N] [present=N] [sparse=0|1] [parts=N]
+//               [threads=N] [reads=N] [batch=N] [wait=US] [wps=N] [hot=N]
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -61,6 +66,7 @@ struct Partition {
 
 int main(int argc, char **argv) {
     uint64_t K = 250000, N = 64, D = 8, P = 1, T = 20, M = 5000, batch = 1024, wait = 0, hot = 0;
+    uint64_t sparse = 0, present = 0;
     double wps = 0;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -81,12 +87,18 @@ int main(int argc, char **argv) {
         else if (k == "wait") wait = std::strtoull(v, nullptr, 10);
         else if (k == "wps") wps = std::atof(v);
         else if (k == "hot") hot = std::strtoull(v, nullptr, 10);
+        else if (k == "sparse") sparse = std::strtoull(v, nullptr, 10);
+        else if (k == "present") present = std::strtoull(v, nullptr, 10);
         else {
             std::fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 2;
         }
     }
-    if (K == 0 || D == 0 || D > 64 || P == 0 || P > 64 || T == 0 || T * P > 1024) return 2;
+    if (present == 0) present = D;
+    if (K == 0 || D == 0 || D > 64 || P == 0 || P > 64 || T == 0 || T * P > 1024 || present > D)
+        return 2;
+    // the interned DCs' presence word (sparse logs)
+    const uint64_t pmask = present >= 64 ? ~0ull : ((1ull << present) - 1ull);
     const uint64_t H = (hot == 0 || hot > K) ? K : hot;  // keys read / written
 
     agn_ctx *ctx = nullptr;
@@ -96,33 +108,34 @@ int main(int argc, char **argv) {
     double t_load = now_s();
     for (uint64_t p = 0; p < P; ++p) {
         Partition &pt = parts[p];
-        if ((rc = agn_oplog_create(ctx, AGN_COUNTER_PN, (uint32_t)D, K, 0, 0, &pt.log)))
+        if ((rc = agn_oplog_create(ctx, AGN_COUNTER_PN, (uint32_t)D, K, (int)sparse, 0, &pt.log)))
             die("agn_oplog_create", rc);
         // the partition's history: N ops per key, commit clocks increasing per DC
         pt.clock.assign(D, 1700000000000000ull);
         uint64_t seed = 20250112ull + p;
         const uint64_t chunk = 1u << 20;
-        std::vector<uint64_t> keys, oc;
+        std::vector<uint64_t> keys, oc, ocm;
         std::vector<int64_t> eff;
         for (uint64_t done = 0; done < K * N;) {
             const uint64_t n = std::min(chunk, K * N - done);
             keys.resize(n);
             oc.resize(n * D);
             eff.resize(n);
+            ocm.assign(sparse ? n : 0, pmask);
             for (uint64_t i = 0; i < n; ++i) {
                 keys[i] = (done + i) % K;  // ops of keys interleave, as updates do
-                const uint32_t dc = (uint32_t)(splitmix(seed) % D);
+                const uint32_t dc = (uint32_t)(splitmix(seed) % present);
                 pt.clock[dc] += 1 + splitmix(seed) % 1000;
                 for (uint32_t d = 0; d < D; ++d) {
                     const uint64_t lag = splitmix(seed) % 5000;
                     const uint64_t c = pt.clock[d];
-                    oc[i * D + d] = d == dc ? c : (c > lag ? c - lag : 0);
+                    oc[i * D + d] = d >= present ? 0 : d == dc ? c : (c > lag ? c - lag : 0);
                 }
                 eff[i] = (int64_t)(splitmix(seed) % 2001) - 1000;
             }
-            if ((rc = agn_oplog_append(pt.log, n, keys.data(), nullptr, oc.data(), nullptr,
-                                       nullptr, eff.data(), nullptr, nullptr, nullptr, nullptr,
-                                       nullptr, nullptr)))
+            if ((rc = agn_oplog_append(pt.log, n, keys.data(), nullptr, oc.data(),
+                                       sparse ? ocm.data() : nullptr, nullptr, eff.data(),
+                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr)))
                 die("agn_oplog_append", rc);
             done += n;
         }
@@ -143,11 +156,14 @@ int main(int argc, char **argv) {
     // warm-up: the first 4096 keys of every partition once
     for (auto &pt : parts) {
         std::vector<uint64_t> R, ct(D);
+        uint64_t ctm = 0;
         snapshot_clock(pt, R);
         agn_key_read rd{};
         agn_key_result o{};
         rd.R = R.data();
+        rd.R_mask = sparse ? &pmask : nullptr;
         o.lastct = ct.data();
+        o.lastct_mask = sparse ? &ctm : nullptr;
         for (uint64_t k = 0; k < std::min<uint64_t>(H, 4096); ++k) {
             rd.key = k;
             if ((rc = agn_batcher_read(pt.b, &rd, &o))) die("agn_batcher_read (warm-up)", rc);
@@ -169,12 +185,13 @@ int main(int argc, char **argv) {
                 std::vector<uint64_t> row(D);
                 while (!stop.load(std::memory_order_relaxed)) {
                     const uint64_t key = splitmix(ws) % H;
-                    const uint32_t dc = (uint32_t)(splitmix(ws) % D);
+                    const uint32_t dc = (uint32_t)(splitmix(ws) % present);
                     pt.clock[dc] += 1 + splitmix(ws) % 1000;
-                    for (uint64_t d = 0; d < D; ++d) row[d] = pt.clock[d];
+                    for (uint64_t d = 0; d < D; ++d) row[d] = d < present ? pt.clock[d] : 0;
                     const int64_t e = (int64_t)(splitmix(ws) % 2001) - 1000;
-                    if (agn_oplog_append(pt.log, 1, &key, nullptr, row.data(), nullptr, nullptr,
-                                         &e, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr))
+                    if (agn_oplog_append(pt.log, 1, &key, nullptr, row.data(),
+                                         sparse ? &pmask : nullptr, nullptr, &e, nullptr, nullptr,
+                                         nullptr, nullptr, nullptr, nullptr))
                         die("agn_oplog_append (writer)", -1);
                     // published after the append: a read at the new clock sees the op
                     pt.pub[dc].store(pt.clock[dc], std::memory_order_release);
@@ -197,9 +214,12 @@ int main(int argc, char **argv) {
             Partition &pt = parts[t % P];
             uint64_t s = 1000 + t;
             std::vector<uint64_t> R, ct(D);
+            uint64_t ctm = 0;
             agn_key_read rd{};
             agn_key_result o{};
             o.lastct = ct.data();
+            o.lastct_mask = sparse ? &ctm : nullptr;
+            rd.R_mask = sparse ? &pmask : nullptr;
             lat[t].reserve(M);
             for (uint64_t i = 0; i < M; ++i) {
                 snapshot_clock(pt, R);
@@ -243,13 +263,15 @@ int main(int argc, char **argv) {
     }
     const uint64_t reads = NT * M;
     std::printf(
-        "{\"tool\": \"serve_bench\", \"parts\": %llu, \"keys_per_part\": %llu, \"hot_keys\": %llu, "
+        "{\"tool\": \"serve_bench\", \"log\": \"%s\", \"dcs_present\": %llu, "
+        "\"parts\": %llu, \"keys_per_part\": %llu, \"hot_keys\": %llu, "
         "\"ops_per_key\": %llu, \"n_dcs\": %llu, \"threads_per_part\": %llu, \"reads\": %llu, "
         "\"max_batch\": %llu, \"max_wait_us\": %llu, \"writes_per_s_per_part\": %.0f, "
         "\"writes\": %llu, \"load_s\": %.3f, \"elapsed_s\": %.4f, \"reads_per_s\": %.1f, "
         "\"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
         "\"batches\": %llu, \"mean_batch\": %.2f, \"status\": {\"hit\": %llu, \"new\": %llu, "
         "\"log\": %llu}, \"errors\": %llu}\n",
+        sparse ? "sparse (presence masks, as the NIF builds it)" : "dense", (unsigned long long)present,
         (unsigned long long)P, (unsigned long long)K, (unsigned long long)H, (unsigned long long)N,
         (unsigned long long)D, (unsigned long long)T, (unsigned long long)reads,
         (unsigned long long)batch, (unsigned long long)wait, wps,
