@@ -69,7 +69,18 @@ class AgnSsCache(C.Structure):
     _fields_ = [
         ("n_dcs", C.c_uint32), ("slots", C.c_uint32), ("n_keys", C.c_uint64),
         ("n", P), ("clock", P), ("clock_mask", P), ("last_op", P), ("value", P),
+        ("state_tag", P), ("state_tok", P), ("state_cap", C.c_uint64), ("state_ctl", P),
     ]
+
+
+def ss_state(start, pairs):
+    """AGN_SS_STATE(start, pairs): a snapshot state in a cache's arena."""
+    return (start << 24) | pairs
+
+
+def ss_state_unpack(v):
+    v &= (1 << 64) - 1
+    return v >> 24, v & 0xFFFFFF
 
 
 class AgnKeyRead(C.Structure):
@@ -146,6 +157,7 @@ PROTOTYPES = {
                                 P, P]),
     "agn_ss_store": (C.c_int, [P, C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P, P,
                                P, C.POINTER(AgnResult), P, P, P, P, P]),
+    "agn_ss_state_compact": (C.c_int, [P, C.POINTER(AgnSsCache), P, P, C.c_uint64, P]),
     "agn_read_cached": (C.c_int, [P, C.POINTER(AgnSsCache), C.POINTER(AgnLog), C.c_uint64, P, P,
                                   P, P, C.POINTER(AgnResult), P, P, P, P]),
     "agn_prune_ops": (C.c_int, [P, C.POINTER(AgnLog), P, P, P, C.POINTER(AgnLog), P, P, P]),

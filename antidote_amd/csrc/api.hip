@@ -350,6 +350,8 @@ int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_of
             for (uint64_t e = log->key_off[k]; e < log->key_off[k] + key_n(log->key_off, log->key_len, k); ++e)
                 c += log->add_tok[e] != 0;
         if (req->base_off) c += req->base_off[i + 1] - req->base_off[i];
+        else if (req->base_value && is_tag_type(log->crdt_type))
+            c += AGN_SS_STATE_PAIRS(req->base_value[i]);
         cap_off[i + 1] = cap_off[i] + c;
     }
     return AGN_OK;
@@ -449,7 +451,11 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     uint64_t n_rem = log->rem_off ? log->rem_off[E] : 0;
     if (log->rem_off && log->key_len)  // segmented log: the token arena's high-water mark
         for (uint64_t e = 0; e <= E; ++e) n_rem = std::max<uint64_t>(n_rem, log->rem_off[e]);
-    const uint64_t n_base = req->base_off ? req->base_off[Q] : 0;
+    uint64_t n_base = req->base_off ? req->base_off[Q] : 0;
+    if (!req->base_off && req->base_value && is_tag_type(log->crdt_type))  // arena references
+        for (uint64_t i = 0; i < Q; ++i)
+            n_base = std::max<uint64_t>(n_base, AGN_SS_STATE_START(req->base_value[i]) +
+                                                    AGN_SS_STATE_PAIRS(req->base_value[i]));
     const uint64_t n_out = out->out_off ? out->out_off[Q] : 0;
     // a sparse log without agn_log.key_mask: build it here (one pass over the
     // masks already in host memory), so keys whose entries share one DC set
@@ -643,6 +649,9 @@ static int check_cache(const agn_ss_cache *c) {
         return fail(AGN_EINVAL, "ss cache: slots=%u < %d", c->slots, AGN_SNAPSHOT_THRESHOLD - 1);
     if (c->n_keys && (!c->n || !c->clock || !c->last_op || !c->value))
         return fail(AGN_EINVAL, "ss cache: null array");
+    if ((c->state_tag || c->state_tok || c->state_ctl) &&
+        !(c->state_tag && c->state_tok && c->state_ctl))
+        return fail(AGN_EINVAL, "ss cache: state arena needs state_tag, state_tok and state_ctl");
     return AGN_OK;
 }
 
@@ -672,8 +681,10 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
         return fail(AGN_EINVAL, "ss_store: null argument");
     if (log->n_keys != cache->n_keys || log->n_dcs != cache->n_dcs)
         return fail(AGN_EINVAL, "ss_store: log and cache disagree on keys / DCs");
+    const bool arena = cache->state_tag != nullptr && is_tag_type(log->crdt_type);
     if (n_req && (!is_first || !status || !res->hole || !res->lastct || !res->count ||
-                  !res->flags || (!handle && !res->value)))
+                  !res->flags || (!arena && !handle && !res->value) ||
+                  (arena && (!res->out_off || !res->out_n || !res->out_tag || !res->out_tok))))
         return fail(AGN_EINVAL, "ss_store: null argument");
     if (!keys && n_req != cache->n_keys)
         return fail(AGN_EINVAL, "ss_store: keys == NULL needs n_req == n_keys");
@@ -738,6 +749,72 @@ static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_r
     return rc;
 }
 
+// read/6 of a set_aw / register_mv batch over a cache with a state arena:
+// lookup (the hit slot's AGN_SS_STATE as the base) -> the tags kernel reading
+// the base state from the arena -> the store appending the new state to it.
+static int read_cached_tags(agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
+                            const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
+                            const uint8_t *should_gc, agn_result *out, uint8_t *status,
+                            uint8_t *prune, uint64_t *threshold, hipStream_t st) {
+    const uint32_t D = log->n_dcs;
+    uint8_t *tmp = nullptr;  // sct [n][D] u64 | base [n] i64 | ign [n] | first [n]
+    AGN_HIP(pool_malloc((void **)&tmp, n_req * (8ull * D + 8ull + 2ull), st));
+    uint64_t *sct = reinterpret_cast<uint64_t *>(tmp);
+    int64_t *base = reinterpret_cast<int64_t *>(sct + n_req * D);
+    uint8_t *ign = reinterpret_cast<uint8_t *>(base + n_req);
+    uint8_t *first = ign + n_req;
+    agn_result o = *out;
+    o.lastct_mask = nullptr;
+    o.value = nullptr;
+    int rc = launch_ss_lookup(*cache, n_req, keys, R, nullptr, sct, nullptr, ign, base, first,
+                              status, st);
+    if (rc == AGN_OK) {
+        agn_read rq{};
+        rq.n_req = n_req;
+        rq.keys = keys;
+        rq.R = R;
+        rq.sct = sct;
+        rq.sct_ignore = ign;
+        rq.txid = txid;
+        rq.req_type = log->crdt_type;
+        rq.base_value = base;  // AGN_SS_STATE references into the arena
+        rq.base_tag = cache->state_tag;
+        rq.base_tok = cache->state_tok;
+        rc = launch_tags(*log, rq, o, st);
+    }
+    if (rc == AGN_OK)
+        rc = launch_ss_store_req(*cache, log->key_off, log->key_len, n_req, keys, first, status,
+                                 should_gc, o, prune, threshold, nullptr, st);
+    (void)hipFreeAsync(tmp, st);
+    return rc;
+}
+
+int agn_ss_state_compact(agn_ctx *ctx, agn_ss_cache *cache, uint32_t *new_tag, uint64_t *new_tok,
+                         uint64_t new_cap, void *stream) {
+    int rc = check_cache(cache);
+    if (rc) return rc;
+    if (!cache->state_tag || !cache->state_tok || !cache->state_ctl)
+        return fail(AGN_EINVAL, "ss_state_compact: the cache has no state arena");
+    if ((!new_tag || !new_tok) && new_cap)
+        return fail(AGN_EINVAL, "ss_state_compact: null arena");
+    rc = use_device(ctx);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    uint64_t ctl[4];
+    AGN_HIP(hipMemcpyAsync(ctl, cache->state_ctl, sizeof ctl, hipMemcpyDeviceToHost, st));
+    AGN_HIP(hipStreamSynchronize(st));
+    const uint64_t live = ctl[0] - ctl[1];
+    if (live > new_cap)
+        return fail(AGN_ECAPACITY, "ss_state_compact: %llu live pairs > %llu",
+                    (unsigned long long)live, (unsigned long long)new_cap);
+    rc = launch_ss_compact(*cache, new_tag, new_tok, new_cap, cache->state_ctl + 2, st);
+    if (rc) return rc;
+    cache->state_tag = new_tag;
+    cache->state_tok = new_tok;
+    cache->state_cap = new_cap;
+    return AGN_OK;
+}
+
 int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
                     const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
                     const uint8_t *should_gc, agn_result *out, uint8_t *status, uint8_t *prune,
@@ -747,6 +824,20 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
     if (!log || !out || !log->key_off) return fail(AGN_EINVAL, "read_cached: null argument");
     if (log->n_keys != cache->n_keys || log->n_dcs != cache->n_dcs)
         return fail(AGN_EINVAL, "read_cached: log and cache disagree on keys / DCs");
+    if (is_tag_type(log->crdt_type)) {
+        if (!cache->state_tag || !cache->state_tok || !cache->state_ctl || cache->clock_mask)
+            return fail(AGN_ENOTSUP, "read_cached: set/register needs a cache with a state "
+                                     "arena and dense clocks");
+        if (n_req == 0) return AGN_OK;
+        if (!keys || !R || !status || !prune || !threshold || !out->hole || !out->lastct ||
+            !out->count || !out->flags || !out->err_pos || !out->out_off || !out->out_n ||
+            !out->out_tag || !out->out_tok)
+            return fail(AGN_EINVAL, "read_cached: null argument");
+        rc = use_device(ctx);
+        if (rc) return rc;
+        return read_cached_tags(cache, log, n_req, keys, R, txid, should_gc, out, status, prune,
+                                threshold, (hipStream_t)stream);
+    }
     if (!read6_supported(*log, log->n_dcs) || cache->clock_mask)
         return fail(AGN_ENOTSUP, "read_cached: counter_pn with dense clocks, D <= 8");
     if (n_req == 0) return AGN_OK;

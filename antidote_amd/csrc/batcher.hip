@@ -84,6 +84,12 @@ struct agn_batcher {
     agn_ss_cache ss{};
     uint64_t *thr = nullptr;    // [K][D] prune thresholds
     uint64_t *thrm = nullptr;   // [K][W] (sparse logs)
+    // set_aw / register_mv: the cache's state arena (ss.state_*), the host's
+    // copy of its state_ctl after the last batch, and per key an upper bound
+    // of the pairs of any state the cache holds for it (the largest result
+    // seen: every cached state is a result's), which sizes a batch's output
+    uint64_t *ctl_h = nullptr;  // pinned [4]
+    std::vector<uint32_t> kbound;
 };
 
 namespace {
@@ -203,10 +209,186 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b) {
                             (const uint8_t *)(B->dbuf + d_pr), B->thr, B->thrm, B->stream);
 }
 
+// The state arena must hold `need` more pairs: re-pack the live states into a
+// fresh arena of max(capacity, 2 x (live + need)) pairs (agn_ss_state_compact's
+// kernel) and free the old one.  Between batches, on the batcher's stream.
+int ensure_state_room(agn_batcher *B, uint64_t need) {
+    if (B->ss.state_cap - B->ctl_h[0] >= need) return AGN_OK;
+    AGN_HIP(hipStreamSynchronize(B->stream));
+    const uint64_t live = B->ctl_h[0] - B->ctl_h[1];
+    const uint64_t cap = std::max<uint64_t>(B->ss.state_cap, 2 * (live + need));
+    uint32_t *nt = nullptr;
+    uint64_t *nk = nullptr;
+    if (hipMalloc((void **)&nt, cap * 4) != hipSuccess || hipMalloc((void **)&nk, cap * 8) != hipSuccess) {
+        if (nt) (void)hipFree(nt);
+        return fail(AGN_ENOMEM, "batcher: state arena of %llu pairs", (unsigned long long)cap);
+    }
+    int rc = launch_ss_compact(B->ss, nt, nk, cap, B->ss.state_ctl + 2, B->stream);
+    if (rc == AGN_OK && hipMemcpyAsync(B->ctl_h, B->ss.state_ctl, 4 * 8, hipMemcpyDeviceToHost,
+                                       B->stream) != hipSuccess)
+        rc = fail(AGN_EHIP, "batcher: state_ctl copy");
+    if (rc == AGN_OK && hipStreamSynchronize(B->stream) != hipSuccess)
+        rc = fail(AGN_EHIP, "batcher: state compaction");
+    if (rc) {
+        (void)hipFree(nt);
+        (void)hipFree(nk);
+        return rc;
+    }
+    (void)hipFree(B->ss.state_tag);
+    (void)hipFree(B->ss.state_tok);
+    B->ss.state_tag = nt;
+    B->ss.state_tok = nk;
+    B->ss.state_cap = cap;
+    return AGN_OK;
+}
+
+// Cached mode, set_aw / register_mv: read/6 for a batch with the snapshot
+// states on the device.  get_from_snapshot_cache's base is the hit slot's
+// state in the arena (agn_ss_lookup writes its AGN_SS_STATE reference), the
+// tags kernel folds the key's ops onto it in place of a host-shipped base,
+// and materialize_snapshot's store appends the result's state to the arena:
+// no state crosses PCIe except the caller's result.
+int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
+    const uint64_t n = b.size();
+    const uint32_t D = B->D, W = B->W;
+    bool sparse = B->sparse_log != 0;
+    for (Pending *p : b) sparse = sparse || p->rd->R_mask;
+    std::vector<uint64_t> keys(n);
+    std::vector<uint32_t> lens(n);
+    for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
+    size_t o_keys_saved = 0, o_pr_saved = 0;
+    {
+        std::shared_lock<std::shared_mutex> hold;
+        int rc = oplog_begin_read(B->log, B->stream, n, keys.data(), lens.data(), hold);
+        if (rc) return rc;
+        // result capacity per request: the key's entries (each adds at most
+        // one pair) + the bound of its cached states
+        std::vector<uint64_t> co(n + 1);
+        co[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + B->kbound[keys[i]];
+        const uint64_t ncap = co[n];
+        rc = ensure_state_room(B, ncap);
+        if (rc) return rc;
+        size_t off = 0;
+        auto slot = [&](size_t bytes) { size_t o = off; off = al(off + bytes); return o; };
+        const size_t o_keys = slot(n * 8), o_R = slot(n * D * 8), o_Rm = slot(sparse ? n * W * 8 : 0),
+                     o_txid = slot(n * 8), o_gc = slot(n), o_cap = slot((n + 1) * 8);
+        const size_t in_bytes = off;
+        const size_t o_sct = slot(n * D * 8), o_sctm = slot(sparse ? n * W * 8 : 0),
+                     o_ign = slot(n), o_base = slot(n * 8), o_first = slot(n);
+        const size_t out_start = off;
+        const size_t o_hole = slot(n * 8), o_ct = slot(n * D * 8),
+                     o_ctm = slot(sparse ? n * W * 8 : 0), o_cnt = slot(n * 4), o_flg = slot(n * 4),
+                     o_epos = slot(n * 4), o_st = slot(n), o_pr = slot(n), o_outn = slot(n * 4),
+                     o_otag = slot(std::max<uint64_t>(ncap, 1) * 4),
+                     o_otok = slot(std::max<uint64_t>(ncap, 1) * 8);
+        rc = grow(B, off);
+        if (rc) return rc;
+        o_keys_saved = o_keys;
+        o_pr_saved = o_pr;
+        char *h = B->hbuf, *d = B->dbuf;
+        auto H = [&](size_t o) { return h + o; };
+        uint64_t full[4] = {0, 0, 0, 0};
+        for (uint32_t x = 0; x < D; ++x) full[x >> 6] |= 1ull << (x & 63);
+        for (uint64_t i = 0; i < n; ++i) {
+            const agn_key_read *r = b[i]->rd;
+            ((uint64_t *)H(o_keys))[i] = r->key;
+            std::memcpy(H(o_R) + i * D * 8, r->R, D * 8);
+            if (sparse) std::memcpy(H(o_Rm) + i * W * 8, r->R_mask ? r->R_mask : full, W * 8);
+            ((uint64_t *)H(o_txid))[i] = r->txid;
+            ((uint8_t *)H(o_gc))[i] = (r->flags & AGN_READ_GC) ? 1 : 0;
+        }
+        std::memcpy(H(o_cap), co.data(), (n + 1) * 8);
+        AGN_HIP(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, B->stream));
+        agn_log view;
+        oplog_view(B->log, &view);
+        const uint64_t *dkeys = (const uint64_t *)(d + o_keys);
+        rc = launch_ss_lookup(B->ss, n, dkeys, (const uint64_t *)(d + o_R),
+                              sparse ? (const uint64_t *)(d + o_Rm) : nullptr,
+                              (uint64_t *)(d + o_sct), sparse ? (uint64_t *)(d + o_sctm) : nullptr,
+                              (uint8_t *)(d + o_ign), (int64_t *)(d + o_base),
+                              (uint8_t *)(d + o_first), (uint8_t *)(d + o_st), B->stream);
+        if (rc) return rc;
+        agn_read req;
+        std::memset(&req, 0, sizeof req);
+        req.n_req = n;
+        req.keys = dkeys;
+        req.R = (const uint64_t *)(d + o_R);
+        req.R_mask = sparse ? (const uint64_t *)(d + o_Rm) : nullptr;
+        req.sct = (const uint64_t *)(d + o_sct);
+        req.sct_mask = sparse ? (const uint64_t *)(d + o_sctm) : nullptr;
+        req.sct_ignore = (const uint8_t *)(d + o_ign);
+        req.txid = (const uint64_t *)(d + o_txid);
+        req.req_type = B->crdt;
+        req.base_value = (const int64_t *)(d + o_base);  // AGN_SS_STATE into the arena
+        req.base_tag = B->ss.state_tag;
+        req.base_tok = B->ss.state_tok;
+        agn_result res;
+        std::memset(&res, 0, sizeof res);
+        res.hole = (int64_t *)(d + o_hole);
+        res.lastct = (uint64_t *)(d + o_ct);
+        res.lastct_mask = sparse ? (uint64_t *)(d + o_ctm) : nullptr;
+        res.count = (uint32_t *)(d + o_cnt);
+        res.flags = (uint32_t *)(d + o_flg);
+        res.err_pos = (uint32_t *)(d + o_epos);
+        res.out_off = (const uint64_t *)(d + o_cap);
+        res.out_n = (uint32_t *)(d + o_outn);
+        res.out_tag = (uint32_t *)(d + o_otag);
+        res.out_tok = (uint64_t *)(d + o_otok);
+        rc = launch_tags(view, req, res, B->stream);
+        if (rc) return rc;
+        rc = launch_ss_store_req(B->ss, view.key_off, view.key_len, n, dkeys,
+                                 (const uint8_t *)(d + o_first), (const uint8_t *)(d + o_st),
+                                 (const uint8_t *)(d + o_gc), res, (uint8_t *)(d + o_pr), B->thr,
+                                 B->thrm, B->stream);
+        if (rc) return rc;
+        AGN_HIP(hipMemcpyAsync(h + out_start, d + out_start, off - out_start, hipMemcpyDeviceToHost,
+                               B->stream));
+        AGN_HIP(hipMemcpyAsync(B->ctl_h, B->ss.state_ctl, 4 * 8, hipMemcpyDeviceToHost, B->stream));
+        rc = wait_batch(B);
+        if (rc) return rc;
+        if (B->ctl_h[2]) return fail(AGN_ECAPACITY, "batcher: state arena overflow");
+        bool any_prune = false;
+        for (uint64_t i = 0; i < n; ++i) {
+            agn_key_result *o = b[i]->out;
+            const uint32_t m = ((const uint32_t *)H(o_outn))[i];
+            o->status = ((const uint8_t *)H(o_st))[i];
+            o->value = 0;
+            o->hole = ((const int64_t *)H(o_hole))[i];
+            std::memcpy(o->lastct, H(o_ct) + i * D * 8, D * 8);
+            if (o->lastct_mask)
+                std::memcpy(o->lastct_mask, sparse ? H(o_ctm) + i * W * 8 : (char *)full, W * 8);
+            o->count = ((const uint32_t *)H(o_cnt))[i];
+            o->flags = ((const uint32_t *)H(o_flg))[i];
+            o->err_pos = ((const uint32_t *)H(o_epos))[i];
+            any_prune = any_prune || ((const uint8_t *)H(o_pr))[i] != 0;
+            const bool ok = !(o->flags & (AGN_F_ERR_CORRUPTED | AGN_F_ERR_UNEXPECTED |
+                                          AGN_F_ERR_CAPACITY));
+            o->out_n = ok ? m : 0;
+            if (ok) B->kbound[keys[i]] = std::max(B->kbound[keys[i]], m);
+            if (!ok || o->status == AGN_SS_LOG) continue;
+            if (m > o->out_cap) {  // the caller retries with out_cap >= out_n
+                b[i]->rc = AGN_ECAPACITY;
+                std::snprintf(b[i]->err, sizeof b[i]->err, "batcher_read: %u pairs, out_cap %u",
+                              m, o->out_cap);
+                continue;
+            }
+            if (m) {
+                std::memcpy(o->out_tag, H(o_otag) + co[i] * 4, m * 4);
+                std::memcpy(o->out_tok, H(o_otok) + co[i] * 8, m * 8);
+            }
+        }
+        if (!any_prune) return AGN_OK;
+    }  // the shared hold ends: the GC takes the log exclusively
+    return oplog_prune_keys(B->log, n, keys.data(), (const uint64_t *)(B->dbuf + o_keys_saved),
+                            (const uint8_t *)(B->dbuf + o_pr_saved), B->thr, B->thrm, B->stream);
+}
+
 // Cached mode: read/6 for a batch of distinct keys (see the file comment).
 int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
     const uint64_t n = b.size();
     const uint32_t D = B->D, W = B->W;
+    if (B->crdt != AGN_COUNTER_PN) return run_batch_cached_tags(B, b);
     bool sparse = B->sparse_log != 0;
     for (Pending *p : b) sparse = sparse || p->rd->R_mask;
     if (!sparse && D <= 8 && B->read6) return run_batch_read6(B, b);
@@ -561,8 +743,10 @@ int agn_batcher_destroy(agn_batcher *B) {
     if (B->dbuf) (void)hipFree(B->dbuf);
     if (B->hbuf) (void)hipHostFree(B->hbuf);
     for (void *p : {(void *)B->ss.n, (void *)B->ss.clock, (void *)B->ss.clock_mask,
-                    (void *)B->ss.last_op, (void *)B->ss.value, (void *)B->thr, (void *)B->thrm})
+                    (void *)B->ss.last_op, (void *)B->ss.value, (void *)B->thr, (void *)B->thrm,
+                    (void *)B->ss.state_tag, (void *)B->ss.state_tok, (void *)B->ss.state_ctl})
         if (p) (void)hipFree(p);
+    if (B->ctl_h) (void)hipHostFree(B->ctl_h);
     if (B->stream) (void)hipStreamDestroy(B->stream);
     delete B;
     return AGN_OK;
@@ -576,9 +760,6 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     int sparse;
     uint64_t K;
     oplog_shape(log, &crdt, &D, &sparse, &K);
-    if (crdt != AGN_COUNTER_PN)
-        return fail(AGN_ENOTSUP, "batcher_create_cached: counter_pn only (set/register states "
-                                 "are cached by the caller)");
     if (slots == 0) slots = AGN_SNAPSHOT_THRESHOLD;
     if (slots < AGN_SNAPSHOT_THRESHOLD - 1)
         return fail(AGN_EINVAL, "batcher_create_cached: slots %u < %d", slots,
@@ -600,11 +781,33 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     if (e == hipSuccess) e = hipMalloc((void **)&c.value, K1 * slots * 8);
     if (e == hipSuccess) e = hipMalloc((void **)&thr, K1 * D * 8);
     if (e == hipSuccess && sparse) e = hipMalloc((void **)&thrm, K1 * W * 8);
+    // set_aw / register_mv: the snapshots' states live in a device arena
+    // (16 pairs per key to start; re-packed / grown between batches)
+    uint64_t *ctl_h = nullptr;
+    if (crdt != AGN_COUNTER_PN) {
+        c.state_cap = std::max<uint64_t>(16 * K1, 1u << 16);
+        if (e == hipSuccess) e = hipMalloc((void **)&c.state_tag, c.state_cap * 4);
+        if (e == hipSuccess) e = hipMalloc((void **)&c.state_tok, c.state_cap * 8);
+        if (e == hipSuccess) e = hipMalloc((void **)&c.state_ctl, 4 * 8);
+        if (e == hipSuccess) e = hipMemset(c.state_ctl, 0, 4 * 8);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&ctl_h, 4 * 8, hipHostMallocDefault);
+        if (e == hipSuccess) std::memset(ctl_h, 0, 4 * 8);
+    }
+    std::vector<uint32_t> kb;  // set/register: per-key state bounds
+    if (e == hipSuccess && crdt != AGN_COUNTER_PN) {
+        try {
+            kb.assign(K1, 0);
+        } catch (...) {
+            e = hipErrorOutOfMemory;
+        }
+    }
     if (e == hipSuccess) rc = agn_batcher_create(log, max_batch, max_wait_us, out);
     if (e != hipSuccess || rc != AGN_OK) {
         for (void *p : {(void *)c.n, (void *)c.clock, (void *)c.clock_mask, (void *)c.last_op,
-                        (void *)c.value, (void *)thr, (void *)thrm})
+                        (void *)c.value, (void *)thr, (void *)thrm, (void *)c.state_tag,
+                        (void *)c.state_tok, (void *)c.state_ctl})
             if (p) (void)hipFree(p);
+        if (ctl_h) (void)hipHostFree(ctl_h);
         return e != hipSuccess ? fail(AGN_ENOMEM, "batcher_create_cached: snapshot cache") : rc;
     }
     // the worker only looks at `cached` under the queue lock, after a read arrives
@@ -615,6 +818,8 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     (*out)->ss = c;
     (*out)->thr = thr;
     (*out)->thrm = thrm;
+    (*out)->ctl_h = ctl_h;
+    (*out)->kbound.swap(kb);
     return AGN_OK;
 }
 

@@ -61,11 +61,15 @@ __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t
     if (i >= n_req) return;
     const uint32_t D = c.n_dcs, W = n_words(D);
     const uint64_t k = keys ? keys[i] : i;
+    // a state arena stores the result's state pairs (set_aw / register_mv)
+    const bool st = c.state_tag != nullptr && res.out_off != nullptr;
+    const uint64_t so = st ? res.out_off[i] : 0ull;
     const bool pr = ss_store_one<G>(
         g, c, k, key_n(key_off, key_len, k), status[i], is_first[i],
         should_gc != nullptr && should_gc[i] != 0, res.lastct + i * D,
         res.lastct_mask ? res.lastct_mask + i * W : nullptr, res.hole[i],
-        handle ? handle[i] : res.value[i], res.count[i], res.flags[i], thr, thrm);
+        (handle && !st) ? handle[i] : st ? 0 : res.value[i], res.count[i], res.flags[i], thr, thrm,
+        st ? res.out_tag + so : nullptr, st ? res.out_tok + so : nullptr, st ? res.out_n[i] : 0u);
     // by_req: prune flags per request (prune[i], every request written),
     // otherwise per key (prune[k], the caller cleared the array)
     if (g.sub == 0) {
@@ -98,7 +102,57 @@ int store_g(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_
     return AGN_OK;
 }
 
+// agn_ss_state_compact: one wave per key; the key's live slots' states are
+// copied into the fresh arena at one atomically reserved range, and their
+// references rewritten.  ctl[0] (reset to 0 before) ends as the live pairs.
+__global__ __launch_bounds__(256) void k_ss_compact(agn_ss_cache c, uint32_t *__restrict__ nt,
+                                                   uint64_t *__restrict__ nk, uint64_t ncap,
+                                                   uint64_t *__restrict__ ovf) {
+    const uint64_t k = uniform_u64((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (k >= c.n_keys) return;
+    const int lane = lane_id();
+    const uint32_t S = c.slots, n = c.n[k];
+    uint64_t tot = 0;
+    for (uint32_t j = 0; j < n; ++j) tot += AGN_SS_STATE_PAIRS(c.value[k * S + j]);
+    if (tot == 0) {
+        if (lane == 0)
+            for (uint32_t j = 0; j < n; ++j) c.value[k * S + j] = AGN_SS_STATE(0, 0);
+        return;
+    }
+    uint64_t base = 0;
+    if (lane == 0) base = atomicAdd((unsigned long long *)&c.state_ctl[0], (unsigned long long)tot);
+    base = uniform_u64(base);  // lane 0's (the first active lane)
+    if (base + tot > ncap) {  // the host sized the arena from ctl: cannot happen
+        if (lane == 0) *ovf = 1ull;
+        return;
+    }
+    for (uint32_t j = 0; j < n; ++j) {
+        const int64_t v = c.value[k * S + j];
+        const uint64_t s0 = AGN_SS_STATE_START(v);
+        const uint32_t p = AGN_SS_STATE_PAIRS(v);
+        for (uint32_t x = lane; x < p; x += AGN_WAVE) {
+            nt[base + x] = c.state_tag[s0 + x];
+            nk[base + x] = c.state_tok[s0 + x];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) c.value[k * S + j] = AGN_SS_STATE(p ? base : 0, p);
+        base += p;
+    }
+}
+
 }  // namespace
+
+int launch_ss_compact(const agn_ss_cache &c, uint32_t *new_tag, uint64_t *new_tok, uint64_t new_cap,
+                      uint64_t *ovf, hipStream_t st) {
+    AGN_HIP(hipMemsetAsync(c.state_ctl, 0, 4 * sizeof(uint64_t), st));
+    if (c.n_keys == 0) return AGN_OK;
+    const uint64_t nb = (c.n_keys + 3) / 4;
+    if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "ss_state_compact: too many keys");
+    hipLaunchKernelGGL(k_ss_compact, dim3((unsigned)nb), dim3(256), 0, st, c, new_tag, new_tok,
+                       new_cap, ovf);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
 
 #define AGN_GROUP_DISPATCH(D, CALL)    \
     switch (group_of(D)) {             \

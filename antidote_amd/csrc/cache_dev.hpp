@@ -121,20 +121,34 @@ __device__ __forceinline__ LookupOut ss_lookup_one(const Grp<G> &g, const agn_ss
                                           : 0};
 }
 
+// 64-bit value of the group's first lane
+template <int G>
+__device__ __forceinline__ uint64_t grp_bcast(const Grp<G> &g, uint64_t v) {
+    const int src = lane_id() - (int)g.sub;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, AGN_WAVE);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, AGN_WAVE);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // The cache half of materialize_snapshot for one request on its group
 // (internal_store_ss / insert_bigger / snapshot_insert_gc, :341-364, 466-563):
 // nops = the key's op count, the materialize result (LastOpCt row + mask row
 // or NULL, NewLastOp `hole`, value, count, flags), status / is_first from
 // the lookup, gc = a GC read (op_insert_gc, :640).  Writes the GC threshold
 // of key k (vectorclock:min of the kept clocks, :523-527) and returns whether
-// its ops are to be pruned.  Group-uniform.
+// its ops are to be pruned.  Group-uniform.  A set_aw / register_mv cache
+// with a state arena (c.state_tag) stores the result's state (st_tag /
+// st_tok, st_n pairs) there and records the pairs of the snapshots it drops.
 template <int G>
 __device__ __forceinline__ bool ss_store_one(const Grp<G> &g, const agn_ss_cache &c, uint64_t k,
                                              uint64_t nops, uint8_t status, uint8_t is_first,
                                              bool gc, const uint64_t *lastct_row,
                                              const uint64_t *lastct_mask_row, int64_t new_op,
                                              int64_t val, uint32_t count, uint32_t fl,
-                                             uint64_t *thr, uint64_t *thrm) {
+                                             uint64_t *thr, uint64_t *thrm,
+                                             const uint32_t *st_tag = nullptr,
+                                             const uint64_t *st_tok = nullptr,
+                                             uint32_t st_n = 0) {
     const uint32_t D = c.n_dcs, W = n_words(D), S = c.slots;
     if (status == AGN_SS_LOG) return false;
     if (nops == 0) return false;  // number_of_ops = 0 (:468-471)
@@ -156,6 +170,34 @@ __device__ __forceinline__ bool ss_store_one(const Grp<G> &g, const agn_ss_cache
     if (collect) old_kept = prepend ? (n < AGN_SNAPSHOT_MIN - 1 ? n : AGN_SNAPSHOT_MIN - 1)
                                     : (n < AGN_SNAPSHOT_MIN ? n : AGN_SNAPSHOT_MIN);
     const uint32_t new_n = old_kept + (prepend ? 1u : 0u);
+    if (c.state_tag) {
+        // the new snapshot's state: appended to the arena (before any change,
+        // so a store that does not fit changes nothing); the dropped
+        // snapshots' pairs are released
+        if (prepend) {
+            uint64_t start = 0;
+            if (g.sub == 0)
+                start = atomicAdd((unsigned long long *)&c.state_ctl[0], (unsigned long long)st_n);
+            start = grp_bcast<G>(g, start);
+            if (start + st_n > c.state_cap || st_n > AGN_SS_STATE_MAX_PAIRS) {
+                if (g.sub == 0) {
+                    c.state_ctl[2] = 1ull;
+                    atomicAdd((unsigned long long *)&c.state_ctl[1], (unsigned long long)st_n);
+                }
+                return false;
+            }
+            for (uint32_t x = g.sub; x < st_n; x += G) {
+                c.state_tag[start + x] = st_tag[x];
+                c.state_tok[start + x] = st_tok[x];
+            }
+            val = AGN_SS_STATE(start, st_n);
+        }
+        if (g.sub == 0 && old_kept < n) {
+            uint64_t rel = 0;
+            for (uint32_t j = old_kept; j < n; ++j) rel += AGN_SS_STATE_PAIRS(c.value[k * S + j]);
+            if (rel) atomicAdd((unsigned long long *)&c.state_ctl[1], (unsigned long long)rel);
+        }
+    }
     if (prepend) {
         for (int j = (int)old_kept - 1; j >= 0; --j) {  // shift down, newest first
             copy_row<G>(g, c.clock, k * S + j + 1, c.clock, k * S + j, D);

@@ -225,7 +225,12 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             (uint32_t)(req.sct_ignore ? req.sct_ignore
                                       : reinterpret_cast<const uint8_t *>(req.R))[i]);
         const uint64_t txv = uniform_u64((req.txid ? req.txid : req.R)[i]);
-        const uint64_t *bop = req.base_off ? req.base_off + i : req.R + i;
+        // base state: CSR base_off, or AGN_SS_STATE(start, pairs) in
+        // base_value (a snapshot cache's state arena, agn_ss_lookup)
+        const bool packed = req.base_off == nullptr && req.base_value != nullptr;
+        const uint64_t *bop = req.base_off ? req.base_off + i
+                            : packed        ? reinterpret_cast<const uint64_t *>(req.base_value) + i
+                                            : req.R + i;
         const uint64_t b0v = uniform_u64(bop[0]);
         const uint64_t b1v = uniform_u64((req.base_off ? bop + 1 : bop)[0]);
         const uint64_t n = log.key_len ? lv : lv - off;
@@ -276,8 +281,10 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 
         // ---- base snapshot state: candidates with ord = index (< B)
         heads_clear<CAP>(L);
-        const uint64_t b0 = req.base_off ? b0v : 0ull;
-        const uint32_t B = req.base_off ? (uint32_t)(b1v - b0v) : 0u;
+        const uint64_t b0 = req.base_off ? b0v : packed ? AGN_SS_STATE_START(b0v) : 0ull;
+        const uint32_t B = req.base_off ? (uint32_t)(b1v - b0v)
+                         : packed        ? AGN_SS_STATE_PAIRS(b0v)
+                                         : 0u;
         bool overflow = B > (uint32_t)(CAP - AGN_WAVE);
         uint32_t used = 0;
         if (!overflow) {

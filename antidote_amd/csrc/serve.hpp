@@ -14,6 +14,11 @@ int launch_ss_store_req(const agn_ss_cache &c, const uint64_t *key_off, const ui
                         const uint8_t *status, const uint8_t *should_gc, const agn_result &res,
                         uint8_t *prune_req, uint64_t *thr, uint64_t *thrm, hipStream_t st);
 
+// agn_ss_state_compact's kernel: the live states into new_tag / new_tok
+// (state_ctl reset, then the live pairs; *ovf = 1 if they do not fit).
+int launch_ss_compact(const agn_ss_cache &c, uint32_t *new_tag, uint64_t *new_tok, uint64_t new_cap,
+                      uint64_t *ovf, hipStream_t st);
+
 // prune_ops in place over a key list (entry i: key keys[i], GC'd iff
 // flags[i] != 0); meta[6][n] per entry.
 int launch_prune_keys(const agn_log &view, uint64_t *key_len, uint32_t *key_id0,

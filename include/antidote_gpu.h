@@ -134,7 +134,11 @@ typedef struct agn_read {
     uint32_t req_type;          /* Type argument of materialize/4 */
     uint32_t _pad;
     /* base snapshot value (#materialized_snapshot.value) */
-    const int64_t *base_value;  /* counter: [n_req] or NULL (= 0, Type:new()) */
+    const int64_t *base_value;  /* counter: [n_req] or NULL (= 0, Type:new());
+                                   set/register with base_off NULL: [n_req]
+                                   AGN_SS_STATE(start, pairs) references into
+                                   base_tag / base_tok (a cache's state arena,
+                                   as agn_ss_lookup writes them) */
     const uint64_t *base_off;   /* set/register: CSR [n_req+1] or NULL (= empty) */
     const uint32_t *base_tag;   /* set: elem, register: value */
     const uint64_t *base_tok;   /* token */
@@ -430,10 +434,13 @@ int agn_update_stable(uint32_t n_dcs, uint64_t *last, const uint64_t *new_,
  * (src/materializer_vnode.erl:341-413, 466-563) as a device table: per key a
  * vector_orddict (src/vector_orddict.erl:36-146) of at most `slots` entries,
  * newest first, each {commit clock, #materialized_snapshot{last_op_id, value}}
- * (include/antidote.hrl:169-176).  `value` is the counter_pn value, or for
- * set_aw / register_mv a caller handle to the state (e.g. an index into the
- * caller's state store).  Clocks are dense rows (+ optional presence masks;
- * an empty clock, vectorclock:new(), is all-absent / all-zero). */
+ * (include/antidote.hrl:169-176).  `value` is the counter_pn value; for
+ * set_aw / register_mv it is the snapshot's state (the orddict the reference
+ * stores) kept on the device: AGN_SS_STATE(start, pairs) into the cache's
+ * state arena (state_tag / state_tok), or -- a cache without an arena -- a
+ * caller handle (e.g. an index into the caller's state store).  Clocks are
+ * dense rows (+ optional presence masks; an empty clock, vectorclock:new(),
+ * is all-absent / all-zero). */
 #define AGN_SNAPSHOT_THRESHOLD 10 /* src/materializer_vnode.erl:37 */
 #define AGN_SNAPSHOT_MIN 3        /* :39 */
 #define AGN_MIN_OP_STORE_SS 5     /* :47 */
@@ -445,8 +452,24 @@ typedef struct agn_ss_cache {
     uint64_t *clock;       /* [n_keys][slots][D] */
     uint64_t *clock_mask;  /* [n_keys][slots][W] or NULL (dense) */
     int64_t *last_op;      /* [n_keys][slots] last_op_id */
-    int64_t *value;        /* [n_keys][slots] value / state handle */
+    int64_t *value;        /* [n_keys][slots] value / AGN_SS_STATE / state handle */
+    /* ABI v4, set_aw / register_mv (NULL = value is a caller handle): the
+     * snapshot states as (tag, token) pairs, the layout of agn_result's
+     * out_tag / out_tok.  agn_ss_store appends a stored snapshot's state at
+     * state_ctl[0] (the next free pair) and adds the pairs of the snapshots
+     * it drops to state_ctl[1]; a store that would pass state_cap is not made
+     * and sets state_ctl[2] = 1 -- keep state_cap - state_ctl[0] >= the
+     * batch's result capacity, re-packing with agn_ss_state_compact. */
+    uint32_t *state_tag;   /* [state_cap] elem / value */
+    uint64_t *state_tok;   /* [state_cap] token */
+    uint64_t state_cap;    /* pairs */
+    uint64_t *state_ctl;   /* [4] device: next free pair, pairs released, overflow, 0 */
 } agn_ss_cache;
+/* a snapshot state in a cache's arena: pairs [start, start + pairs) */
+#define AGN_SS_STATE(start, pairs) ((int64_t)(((uint64_t)(start) << 24) | (uint64_t)(pairs)))
+#define AGN_SS_STATE_START(v) ((uint64_t)(v) >> 24)
+#define AGN_SS_STATE_PAIRS(v) ((uint32_t)((uint64_t)(v) & 0xFFFFFFu))
+#define AGN_SS_STATE_MAX_PAIRS 0xFFFFFFu
 
 /* lookup status */
 #define AGN_SS_HIT 0 /* a cached snapshot <= R: base = it */
@@ -495,7 +518,12 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
 /* materializer_vnode:read/6 for a batch (:96-102, 371-509) in ONE kernel:
  * agn_ss_lookup -> agn_materialize from the cached base -> agn_ss_store, per
  * request, for counter_pn logs with dense clocks (D <= 8; the read
- * batcher's fused path over device arrays).  keys[n_req] (distinct, device),
+ * batcher's fused path over device arrays).  For set_aw / register_mv caches
+ * with a state arena (and any clock width) the same three steps run as the
+ * batched kernels, the base state read from the arena by the tags kernel and
+ * the stored state appended to it: out.out_off is the caller's capacity CSR
+ * (a request whose state does not fit gets AGN_F_ERR_CAPACITY and no store),
+ * out.out_n / out_tag / out_tok receive the states.  keys[n_req] (distinct, device),
  * R[n_req][D], txid[n_req] (NULL: ignore), should_gc[n_req] (NULL: none);
  * results in out (value, hole, lastct, count, flags, err_pos), status[n_req]
  * (AGN_SS_*), prune[n_req] (per request, unlike agn_ss_store's per key) and
@@ -511,6 +539,17 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
                     const uint64_t *keys, const uint64_t *R, const uint64_t *txid,
                     const uint8_t *should_gc, agn_result *out, uint8_t *status, uint8_t *prune,
                     uint64_t *threshold, void *stream);
+
+/* Re-packs the live snapshot states of a set_aw / register_mv cache into a
+ * fresh arena new_tag / new_tok of new_cap pairs (device, caller-owned): every
+ * slot's AGN_SS_STATE is rewritten to its new place, state_ctl becomes {live
+ * pairs, 0, 0, 0} and cache->state_tag / state_tok / state_cap point to the new
+ * arrays (the host struct is updated; the old arrays are free once `stream`
+ * has passed this call).  AGN_ECAPACITY (nothing changed) when the live states
+ * need more than new_cap pairs -- read state_ctl[0] - state_ctl[1] first.
+ * Not part of the reference's API (the ETS table's memory is the runtime's). */
+int agn_ss_state_compact(agn_ctx *ctx, agn_ss_cache *cache, uint32_t *new_tag,
+                         uint64_t *new_tok, uint64_t new_cap, void *stream);
 
 /* ---- log-read fallback and recovery ingest ------------------------------
  * A partition's logging_vnode disk log, decoded into records in log order

@@ -642,8 +642,9 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
         if (!enif_is_identical(base, atom(env, "undefined")) && !enif_get_int64(env, base, &v))
             return enif_make_badarg(env);
         rd.base_value = v;
-    } else {
-        /* base state pairs: set_aw orddict [{Elem, [Tok]}], register_mv [{V, Tok}] */
+    } else if (!p->cached) {
+        /* base state pairs: set_aw orddict [{Elem, [Tok]}], register_mv [{V, Tok}]
+         * (a cached partition's base state is the device snapshot cache's) */
         unsigned nl = 0;
         if (!enif_get_list_length(env, base, &nl)) return enif_make_badarg(env);
         ERL_NIF_TERM h, t = base;
@@ -658,6 +659,7 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
         }
         btag = enif_alloc(4 * (cap + 1));
         btok = enif_alloc(8 * (cap + 1));
+        if (!btag || !btok) goto oom;
         for (t = base; enif_get_list_cell(env, t, &h, &t);) {
             int ar;
             const ERL_NIF_TERM *tp;
@@ -680,14 +682,33 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
         rd.n_base = nb;
         rd.base_tag = btag;
         rd.base_tok = btok;
+    }
+    if (p->type != AGN_COUNTER_PN) {
+        /* room for the state: the key's entries + the base (a cached base is
+         * sized by the retry below) */
         if (agn_oplog_key_meta(p->log, 1, &k, &len, NULL, NULL)) goto oom;
-        o.out_cap = len + nb;
+        o.out_cap = len + nb + (p->cached ? 16u : 0u);
         otag = enif_alloc(4 * (o.out_cap + 1));
         otok = enif_alloc(8 * (o.out_cap + 1));
+        if (!otag || !otok) goto oom;
         o.out_tag = otag;
         o.out_tok = otok;
     }
     rc = agn_batcher_read(p->bt, &rd, &o);
+    if (rc == AGN_ECAPACITY && p->type != AGN_COUNTER_PN && o.out_n > o.out_cap) {
+        /* the state outgrew the buffer (an update landed after key_meta, or a
+         * larger cached base): read again with room for it (a read/6 is
+         * repeatable: the second one is served from what the first stored) */
+        enif_free(otag);
+        enif_free(otok);
+        o.out_cap = o.out_n + 16u;
+        otag = enif_alloc(4 * (o.out_cap + 1));
+        otok = enif_alloc(8 * (o.out_cap + 1));
+        if (!otag || !otok) goto oom;
+        o.out_tag = otag;
+        o.out_tok = otok;
+        rc = agn_batcher_read(p->bt, &rd, &o);
+    }
     ERL_NIF_TERM r;
     if (rc) r = error_tuple(env, rc);
     else if (p->cached && o.status == AGN_SS_LOG)
@@ -701,12 +722,18 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
 oom:
     enif_free(btag);
     enif_free(btok);
+    enif_free(otag);
+    enif_free(otok);
     return error_tuple(env, AGN_ENOMEM);
 }
 
 static ERL_NIF_TERM nif_part_read(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
-    if (argc != 5 || !get_part(env, argv[0], &p) || !p->cached) return enif_make_badarg(env);
+    if (argc != 5 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    /* read/6 through the device snapshot cache: a partition opened with
+     * Cached = false keeps the reference's ETS cache (use part_materialize) */
+    if (!p->cached)
+        return enif_make_tuple2(env, atom(env, "error"), atom(env, "not_cached"));
     return part_read_common(env, p, argv[1], argv[2], atom(env, "ignore"), argv[3],
                             atom(env, "undefined"), enif_is_identical(argv[4], atom(env, "true")));
 }

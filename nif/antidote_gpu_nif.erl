@@ -336,8 +336,9 @@ get_min_time(Dict) ->
 
 %% ---------------------------------------------------------------------------
 %% The engine-owned partition: materializer_vnode's ops cache in HBM.
-%% Cached = true: the snapshot cache lives on the device too (counter_pn),
-%% read/4 is the whole read/6; Cached = false: the reference's own ETS
+%% Cached = true: the snapshot cache lives on the device too (every type: the
+%% set_aw / register_mv snapshot states stay on the device), read/4 is the
+%% whole read/6; Cached = false: the reference's own ETS
 %% snapshot cache stays, and read_from/6 is materialize/4 over the resident ops.
 new_partition(Type, NKeys, Cached) ->
     {ok, Ps} = application:get_env(antidote, gpu_dcs),   % DC slots per clock (<= 256)
@@ -354,7 +355,14 @@ new_partition(Type, NKeys, Cached) ->
 update(Part, Key, #clocksi_payload{snapshot_time = SS, commit_time = {Dc, Ct},
                                    txid = TxId, op_param = Effect}) ->
     GcRan = case part_gc_due(Part, Key) of
-                true -> _ = part_read(Part, Key, dict:to_list(SS), ignore, true), true;
+                true ->
+                    case part_read(Part, Key, dict:to_list(SS), ignore, true) of
+                        {error, not_cached} ->
+                            %% an uncached partition's GC read is the vnode's own
+                            %% (its ETS snapshot cache): use part_update/5 there
+                            erlang:error({update_needs_cached_partition, Key});
+                        _ -> true
+                    end;
                 false -> false
             end,
     case part_update(Part, Key, dict:to_list(dict:store(Dc, Ct, SS)), TxId, Effect) of

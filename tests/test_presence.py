@@ -107,10 +107,12 @@ def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
         got = device_result(eng, log, req, index=(path == "device_indexed"))
     bad = compare(_abi.COUNTER_PN, D, got, want, True, req.n_req)
     assert not bad, bad[:10]
-    # absent LastOpCt columns are 0, as the oracle writes them
+    # absent LastOpCt columns are 0, as the oracle writes them (a corrupted
+    # key's result is only its error)
     m = got.lastct_mask[:, 0]
+    written = (got.flags & _abi.F_ERR_CORRUPTED) == 0
     for d in range(D):
-        absent = ((m >> np.uint64(d)) & np.uint64(1)) == 0
+        absent = (((m >> np.uint64(d)) & np.uint64(1)) == 0) & written
         assert not got.lastct[absent, d].any()
 
 

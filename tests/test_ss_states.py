@@ -1,0 +1,281 @@
+"""set_aw / register_mv snapshot states on the device (ABI v4 state arena).
+
+materializer_vnode's snapshot cache stores, for every CRDT type, the full
+#materialized_snapshot{value} -- for set_aw / register_mv the state orddict
+(src/materializer_vnode.erl:384-413, 466-509, include/antidote.hrl:169-176) --
+and a read materializes from that cached state.  Here the cached states live
+in a device arena next to the cache (agn_ss_cache.state_*): agn_ss_lookup
+hands the hit slot's state to the tags kernel as its base, agn_ss_store
+appends the result's state.  Checked against the reference's transcription
+(oracle/py_oracle.MaterializerVnode: ETS ops tuple, snapshot cache, GC,
+resize) read for read:
+
+  * the cached read batcher (the NIF's read/4 on a Cached partition), with
+    update/2's GC reads, dense and presence-masked logs;
+  * agn_read_cached over device arrays, rounds of whole-partition batches,
+    with the GC applied and the arena re-packed (agn_ss_state_compact).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from antidote_amd import _abi
+from antidote_amd.engine import Batcher, OpLog
+from oracle import py_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+D = 3
+PTYPE = {_abi.SET_AW: po.SET_AW, _abi.REGISTER_MV: po.REGISTER_MV}
+
+
+def vc(row):
+    return {d: int(row[d]) for d in range(D)}
+
+
+class TagWorkload:
+    """Causal clocks as in test_vnode_replay; effects built the way the CRDTs'
+    downstream does: set_aw add = {Elem, [new token], observed tokens of Elem},
+    remove = {Elem, [], observed}; register_mv assign = {V, new token, all
+    observed}, reset = {reset, all observed} (observed = the writer's view)."""
+
+    def __init__(self, seed, K, typ):
+        self.rng = np.random.default_rng(seed)
+        self.K, self.typ = K, typ
+        self.clk = np.full(D, 1000, np.int64)
+        self.live = [dict() for _ in range(K)]   # key -> elem -> [tok]
+        self.tok = 1
+
+    def op(self, key):
+        c = int(self.rng.integers(0, D))
+        ss = np.maximum(self.clk - self.rng.integers(0, 40, D), 0)
+        self.clk[c] += int(self.rng.integers(1, 30))
+        oc = ss.copy()
+        oc[c] = self.clk[c]
+        live = self.live[key]
+        if self.typ == _abi.SET_AW:
+            e = int(self.rng.integers(0, 6))
+            obs = list(live.get(e, []))
+            if self.rng.random() < 0.75:
+                t = self.tok
+                self.tok += 1
+                live[e] = [t]
+                eff, entry = [(e, [t], obs)], (e, t, obs)
+            else:
+                live[e] = []
+                eff, entry = [(e, [], obs)], (e, 0, obs)
+        else:
+            obs = [t for ts in live.values() for t in ts]
+            if self.rng.random() < 0.1:
+                live.clear()
+                eff, entry = ("reset", obs), (0, 0, obs)
+            else:
+                v, t = int(self.rng.integers(0, 5)), self.tok
+                self.tok += 1
+                live.clear()
+                live[0] = [t]
+                eff, entry = (v, t, obs), (v, t, obs)
+        return c, ss, int(self.clk[c]), oc, eff, entry
+
+    def read_clock(self, lag=400):
+        return np.maximum(self.clk - self.rng.integers(0, lag, D), 0)
+
+
+def state_of(typ, tags, toks):
+    """Engine pairs -> the reference's state: set_aw orddict [{Elem, [Tok]}]
+    (pairs grouped by elem, tokens in fold order), register_mv [{V, Tok}]."""
+    if typ == _abi.REGISTER_MV:
+        return [(int(v), int(t)) for v, t in zip(tags, toks)]
+    out = []
+    for e, t in zip(tags, toks):
+        if out and out[-1][0] == int(e):
+            out[-1][1].append(int(t))
+        else:
+            out.append((int(e), [int(t)]))
+    return out
+
+
+def append_entry(ol, key, oc, entry, txid, mask=None):
+    tag, add, rems = entry
+    ol.append(np.array([key], np.uint64), oc.reshape(1, D).astype(np.uint64),
+              oc_mask=None if mask is None else np.array([[mask]], np.uint64),
+              tag=np.array([tag], np.uint32), add_tok=np.array([add], np.uint64),
+              rem_off=np.array([0, len(rems)], np.uint32),
+              rem_tok=np.array(rems if rems else [0], np.uint64),
+              txid=np.array([txid], np.uint64))
+
+
+def placeholder(vn, key):
+    tup = vn.ops_cache.get(key)
+    return tup is not None and any(tup[po.FIRST_OP - 1 + i] == 0 for i in range(tup[1][0]))
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("typ", [_abi.SET_AW, _abi.REGISTER_MV])
+def test_batcher_states_vs_reference(eng, typ, sparse):
+    """update/2 (+ its GC read) and read/6 through a cached set/register
+    partition: every served state equals the reference's, and the ETS list
+    sizes follow it slot for slot."""
+    K, steps = 16, 2500
+    w = TagWorkload(31 + typ, K, typ)
+    vn = po.MaterializerVnode()
+    quirk, served, log_reads = set(), 0, 0
+    full = np.uint64((1 << D) - 1)
+    rm = np.array([full]) if sparse else None
+    with OpLog(eng, typ, D, K, sparse=sparse) as ol, \
+            Batcher(ol, max_batch=8, cached=True) as bt:
+        for s in range(steps):
+            key = int(w.rng.integers(0, K))
+            if w.rng.random() < 0.7:
+                c, ss, ct, oc, eff, entry = w.op(key)
+                try:
+                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss), (c, ct), s + 1))
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                if ol.gc_due(key)[0]:
+                    bt.read(key, R=ss.astype(np.uint64), R_mask=rm, gc=True, out_cap=4096)
+                append_entry(ol, key, oc, entry, s + 1, full if sparse else None)
+                if placeholder(vn, key):
+                    quirk.add(key)
+            else:
+                R = w.read_clock(lag=400 if w.rng.random() < 0.85 else 20000)
+                g = bt.read(key, R=R.astype(np.uint64), R_mask=rm, out_cap=4096)
+                if key in quirk:
+                    continue
+                try:
+                    want = vn.read(key, PTYPE[typ], vc(R), po.IGNORE)
+                except NotImplementedError:
+                    assert g["status"] == _abi.SS_LOG, (s, key)
+                    log_reads += 1
+                    continue
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                    continue
+                assert g["status"] in (_abi.SS_HIT, _abi.SS_NEW), (s, key, g["status"])
+                got = state_of(typ, g["out_tag"], g["out_tok"])
+                assert want == ("ok", got), (s, key, want, got)
+                served += 1
+                if placeholder(vn, key):
+                    quirk.add(key)
+        ln, ll, ct = ol.key_meta()
+    assert served > 500 and log_reads > 0, (served, log_reads)
+    assert len(quirk) < K // 2
+    for k in range(K):
+        if k in quirk or k not in vn.ops_cache:
+            continue
+        length, list_len = vn.ops_cache[k][1]
+        assert (int(ln[k]), int(ll[k])) == (length, list_len), k
+
+
+def test_batcher_state_bound_grows(eng):
+    """A key whose state outgrows the caller's buffer: the read reports
+    AGN_ECAPACITY, a second read with room for the state is served (the NIF's
+    retry) from the snapshot the first one stored."""
+    from antidote_amd._lib import EngineError
+    K = 2
+    with OpLog(eng, _abi.SET_AW, D, K) as ol, Batcher(ol, max_batch=4, cached=True) as bt:
+        n = 300
+        oc = np.tile(np.arange(1, n + 1, dtype=np.uint64)[:, None], (1, D))
+        ol.append(np.zeros(n, np.uint64), oc, tag=np.arange(n, dtype=np.uint32),
+                  add_tok=np.arange(1, n + 1, dtype=np.uint64),
+                  rem_off=np.zeros(n + 1, np.uint32), rem_tok=np.zeros(1, np.uint64))
+        R = np.full(D, n, np.uint64)
+        with pytest.raises(EngineError):
+            bt.read(0, R=R, out_cap=10)
+        g = bt.read(0, R=R, out_cap=n)
+        assert g["out_n"] == n
+        assert state_of(_abi.SET_AW, g["out_tag"], g["out_tok"]) == \
+            [(e, [e + 1]) for e in range(n)]
+
+
+@pytest.mark.parametrize("typ", [_abi.SET_AW, _abi.REGISTER_MV])
+def test_read_cached_states_vs_reference(eng, typ):
+    """agn_read_cached over device arrays: rounds of reads of every key at a
+    growing clock (with GC reads), the selected keys pruned in the log, and the
+    arena re-packed into a fresh one every other round."""
+    K, rounds = 64, 6
+    w = TagWorkload(77 + typ, K, typ)
+    vn = po.MaterializerVnode()
+    S = _abi.SNAPSHOT_THRESHOLD
+    with OpLog(eng, typ, D, K) as ol:
+        bufs = {"n": eng.empty(4 * K), "clock": eng.empty(8 * K * S * D),
+                "last_op": eng.empty(8 * K * S), "value": eng.empty(8 * K * S),
+                "ctl": eng.empty(32), "status": eng.empty(K), "prune": eng.empty(K),
+                "thr": eng.empty(8 * K * D)}
+        eng.lib.agn_memset_d(eng.ctx, bufs["n"].ptr, 0, 4 * K, None)
+        eng.lib.agn_memset_d(eng.ctx, bufs["ctl"].ptr, 0, 32, None)
+        cap = 1 << 14
+        arena = [eng.empty(4 * cap), eng.empty(8 * cap)]
+        c = _abi.AgnSsCache()
+        c.n_dcs, c.slots, c.n_keys = D, S, K
+        c.n, c.clock, c.last_op, c.value = (bufs[x].ptr for x in ("n", "clock", "last_op", "value"))
+        c.state_tag, c.state_tok, c.state_cap, c.state_ctl = arena[0].ptr, arena[1].ptr, cap, \
+            bufs["ctl"].ptr
+        keys = eng.upload(np.arange(K, dtype=np.uint64))
+        quirk = set()
+        s = 0
+        for rnd in range(rounds):
+            # ~3 ops per key per round: no key reaches op_insert_gc's GC
+            # trigger (50 ops, :635), so the reference's GC runs only where the
+            # batch's gc flags run it on the device too
+            for _ in range(3 * K):
+                key = int(w.rng.integers(0, K))
+                c_, ss, ct, oc, eff, entry = w.op(key)
+                s += 1
+                try:
+                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss), (c_, ct), s))
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(key)
+                append_entry(ol, key, oc, entry, s)
+                if placeholder(vn, key):
+                    quirk.add(key)
+            view = ol.flush()
+            ln, _, _ = ol.key_meta()
+            cap_off = np.zeros(K + 1, np.uint64)
+            cap_off[1:] = np.cumsum(ln.astype(np.uint64) + np.uint64(512))
+            dres = eng.alloc_result(K, D, sparse=False, cap_off=cap_off)
+            R = w.read_clock(lag=300).astype(np.uint64)
+            dR = eng.upload(np.tile(R, (K, 1)))
+            gc = (w.rng.random(K) < 0.2).astype(np.uint8)
+            dgc = eng.upload(gc)
+            eng.read_cached(c, view, K, keys.ptr, dR.ptr, None, dgc.ptr, dres, bufs["status"].ptr,
+                            bufs["prune"].ptr, bufs["thr"].ptr)
+            res = eng.fetch_result(dres)
+            status = eng.download(bufs["status"], np.uint8, (K,))
+            for k in range(K):
+                if k in quirk:
+                    continue
+                try:
+                    want = vn.internal_read(k, PTYPE[typ], vc(R), po.IGNORE, bool(gc[k]))
+                except NotImplementedError:
+                    assert status[k] == _abi.SS_LOG, (rnd, k)
+                    continue
+                except (po.BadMatch, TypeError, ValueError):
+                    quirk.add(k)
+                    continue
+                assert status[k] in (_abi.SS_HIT, _abi.SS_NEW), (rnd, k, status[k])
+                o, m = int(res.out_off[k]), int(res.out_n[k])
+                got = state_of(typ, res.out_tag[o:o + m], res.out_tok[o:o + m])
+                assert want == ("ok", got), (rnd, k, want, got)
+                if placeholder(vn, k):
+                    quirk.add(k)
+            # the GC the store selected, in the log
+            ol.prune(bufs["prune"].ptr, bufs["thr"].ptr)
+            ctl = eng.download(bufs["ctl"], np.uint64, (4,))
+            assert ctl[2] == 0, "state arena overflow"
+            if rnd % 2 == 1:  # re-pack into a fresh arena
+                live = int(ctl[0] - ctl[1])
+                nt, nk = eng.empty(4 * cap), eng.empty(8 * cap)
+                assert eng.lib.agn_ss_state_compact(eng.ctx, C.byref(c), nt.ptr, nk.ptr, cap,
+                                                    None) == 0
+                ctl = eng.download(bufs["ctl"], np.uint64, (4,))
+                assert int(ctl[0]) == live and int(ctl[1]) == 0
+                for b in arena:
+                    b.free()
+                arena = [nt, nk]
+            for b in (dR, dgc):
+                b.free()
+            for b in dres.bufs.values():
+                b.free()
+        assert len(quirk) < K // 2
