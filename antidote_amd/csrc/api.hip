@@ -459,10 +459,10 @@ int agn_materialize_host(agn_ctx *ctx, const agn_log *log, const agn_read *req, 
     const uint64_t n_out = out->out_off ? out->out_off[Q] : 0;
     // a sparse log without agn_log.key_mask: build it here (one pass over the
     // masks already in host memory), so keys whose entries share one DC set
-    // take the dense row scan (D <= 8)
+    // take the dense row scans (D <= 64)
     std::vector<uint64_t> hkm;
     const uint64_t *kmask = log->key_mask;
-    if (log->oc_mask && !kmask && D <= 8 && log->crdt_type == AGN_COUNTER_PN) {
+    if (log->oc_mask && !kmask && D <= 64) {
         const uint64_t full = low_bits(D);
         hkm.assign(K, 0);
         for (uint64_t k = 0; k < K; ++k) {

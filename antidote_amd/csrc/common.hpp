@@ -73,6 +73,18 @@ __device__ __forceinline__ uint64_t group_any(uint64_t b) {
     return m;
 }
 
+// Bit q of the result = some bit of nibble q of b (q = 0..15), on the scalar
+// unit: the per-op verdict of a ballot whose 4 lanes per op are its 4 parts.
+__device__ __forceinline__ uint64_t nib_any16(uint64_t b) {
+    b |= b >> 1;
+    b |= b >> 2;
+    b &= 0x1111111111111111ull;
+    b = (b | (b >> 3)) & 0x0303030303030303ull;
+    b = (b | (b >> 6)) & 0x000F000F000F000Full;
+    b = (b | (b >> 12)) & 0x000000FF000000FFull;
+    return (b | (b >> 24)) & 0xFFFFull;
+}
+
 __host__ __device__ inline uint64_t low_bits(uint64_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
 
 // Entries of key k: [key_off[k], key_off[k] + key_len[k]) or CSR.

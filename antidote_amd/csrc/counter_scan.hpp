@@ -274,18 +274,6 @@ __device__ __forceinline__ uint64_t wave_or_bits(uint64_t um) {
     return r;
 }
 
-// Bit q of the result = some bit of nibble q of b (q = 0..15), on the scalar
-// unit: the per-op verdict of a ballot whose 4 lanes per op are its 4 parts.
-__device__ __forceinline__ uint64_t nib_any16(uint64_t b) {
-    b |= b >> 1;
-    b |= b >> 2;
-    b &= 0x1111111111111111ull;
-    b = (b | (b >> 3)) & 0x0303030303030303ull;
-    b = (b | (b >> 6)) & 0x000F000F000F000Full;
-    b = (b | (b >> 12)) & 0x000000FF000000FFull;
-    return (b | (b >> 24)) & 0xFFFFull;
-}
-
 // scan_key for D = 8 with lane-CONTIGUOUS row loads ("quad rows"): load j of a
 // 64-op chunk reads bytes [1 KiB j, 1 KiB (j+1)) of the chunk's rows, so
 // every instruction covers 8 whole 128-byte lines -- the row-per-lane loads

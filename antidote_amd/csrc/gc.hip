@@ -580,6 +580,16 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
 // slot.  Consecutive-id index: with an index before the GC the kept ids are
 // id0 + position, so it survives iff the kept positions are contiguous and no
 // id is loaded; without one the kept entries' ids are loaded and checked.
+//
+// QUAD (dense D = 8, one op per lane): a chunk's 4 KiB of rows are read
+// lane-contiguously, non-temporal -- load j covers bytes [1 KiB j, 1 KiB
+// (j+1)), 8 whole lines per instruction, lane l holding DCs 2p, 2p+1 (p = l &
+// 3) of op 16 j + (l >> 2), the counter kernel's quad rows (counter_scan.hpp)
+// -- where the row-per-lane loads touch 32 lines per instruction, a quarter
+// of each, and request every line four times.  belongs_to_snapshot_op's
+// verdicts are nibbles of wave ballots folded on the scalar unit; a moving
+// row is written back from the same registers (its parts' lanes fetch its
+// destination).  On a prefix drop nothing moves and the GC is a read pass.
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS>
 __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
                                                    const uint8_t *__restrict__ prune,
@@ -589,6 +599,7 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
                                                    uint32_t *__restrict__ flags) {
     using S = Shape<DPL, LPO>;
     constexpr int OPI = S::OPI;
+    constexpr bool QUAD = FULL && DPL == 8 && LPO == 1 && !SPARSE;
     const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint64_t i = blk;
     if (i >= a.n_keys) return;
@@ -630,6 +641,10 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
         return l;
     }();
     const bool derive = id0_old != AGN_ID0_NONE;
+    // QUAD: this lane's part of the threshold (DCs 2p, 2p+1)
+    const int qp = lane & 3;
+    const uint64_t tA = qp == 0 ? t[0] : qp == 1 ? t[2 % DPL] : qp == 2 ? t[4 % DPL] : t[6 % DPL];
+    const uint64_t tB = qp == 0 ? t[1 % DPL] : qp == 1 ? t[3 % DPL] : qp == 2 ? t[5 % DPL] : t[7 % DPL];
     uint64_t written = 0;             // kept entries above the current chunk
     uint32_t twritten = 0;            // their tokens
     uint32_t rtop = te;               // token start of the entry just above the chunk
@@ -642,8 +657,19 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
         const bool valid = pos < n;
         const uint64_t e = off + (valid ? pos : 0ull);
         uint64_t o[DPL];
-        uint32_t obits;
-        if constexpr (FULL) {
+        uint32_t obits = 0;
+        u64x2 qx[4];
+        uint64_t gtm = 0;  // QUAD: ops with a DC above the threshold
+        if constexpr (QUAD) {
+            const u64x2 *rows = reinterpret_cast<const u64x2 *>(a.oc);
+            const uint64_t lim = (off + n) * 4u - 1u;  // the key's last part
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint64_t u = (off + b) * 4u + (uint64_t)(j * AGN_WAVE + lane);
+                u = u < lim ? u : lim;
+                qx[j] = __builtin_nontemporal_load(rows + u);
+            }
+        } else if constexpr (FULL) {
             load_rows<DPL, SPARSE, FULL>(rl, e, d0, D, W, o, obits);
         } else {
             obits = chunk_bits<DPL, SPARSE>(a.mask, e, W, d0, D);
@@ -653,16 +679,25 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
         }
         uint32_t r0 = 0;
         if constexpr (TAGS) r0 = (valid && sub == 0) ? a.rem_off[e] : 0u;
-        if (!valid) obits = 0u;
-        bool le = true;
+        bool kp;
+        if constexpr (QUAD) {
+            __builtin_amdgcn_sched_barrier(0);  // every load of the chunk in flight first
 #pragma unroll
-        for (int j = 0; j < DPL; ++j)
-            if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
-        if (LPO > 1) {
-            const uint64_t grp = ((1ull << LPO) - 1ull) << hl;
-            le = (ballot(!le) & grp) == 0ull;
+            for (int j = 0; j < 4; ++j)
+                gtm |= nib_any16(ballot(qx[j].x > tA || qx[j].y > tB)) << (16 * j);
+            kp = valid && ((gtm >> lane) & 1ull);  // belongs_to_snapshot_op(Threshold, op)
+        } else {
+            if (!valid) obits = 0u;
+            bool le = true;
+#pragma unroll
+            for (int j = 0; j < DPL; ++j)
+                if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
+            if (LPO > 1) {
+                const uint64_t grp = ((1ull << LPO) - 1ull) << hl;
+                le = (ballot(!le) & grp) == 0ull;
+            }
+            kp = valid && !le;  // belongs_to_snapshot_op(Threshold, op)
         }
-        const bool kp = valid && !le;  // belongs_to_snapshot_op(Threshold, op)
         const bool head = kp && sub == 0;
         const uint64_t km = ballot(head);  // one bit per kept op (its head lane)
         const uint32_t nk = (uint32_t)__builtin_popcountll(km);
@@ -714,7 +749,18 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // stores: the moving entries only
-        if (mv) {
+        if constexpr (QUAD) {
+            const uint64_t mvm = ballot(mv);
+            if (mvm) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = 16 * j + (lane >> 2);  // the op whose part this lane holds
+                    const uint64_t dq = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), q, AGN_WAVE) << 32) |
+                                        (uint32_t)__shfl((int)(uint32_t)dst, q, AGN_WAVE);
+                    if ((mvm >> q) & 1ull) reinterpret_cast<u64x2 *>(a.d_oc)[dq * 4u + (uint64_t)qp] = qx[j];
+                }
+            }
+        } else if (mv) {
             if constexpr (FULL) {
                 u64x2 *q = reinterpret_cast<u64x2 *>(a.d_oc + dst * D + (uint32_t)d0);
 #pragma unroll

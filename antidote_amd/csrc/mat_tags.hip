@@ -189,13 +189,31 @@ __device__ __forceinline__ Side load_side(const agn_log &log, uint64_t off, uint
 // l holds DCs 2 (l % P), 2 (l % P) + 1 (P = D / 2 parts per op) of op l / P
 // of each half; the per-op verdicts are group-any folds of wave ballots
 // (scalar), LastOpCt stays per part until the end of the key.
+// Work lists of one launch sequence: `in` (NULL: the batch) the requests this
+// launch serves; keys whose live state overflows the fast table go to ovf;
+// MSK: keys the dense scan cannot serve exactly go to mix (see MSK below).
+struct TagLists {
+    const uint32_t *in, *in_n;
+    uint32_t *ovf, *ovf_n;
+    uint32_t *mix, *mix_n;
+};
+
+// MSK (presence masks on a dense-loadable shape, D <= 64): per request the
+// key's shared DC set U (agn_log.key_mask), R's and SCT's mask words; a key
+// with U known and inside R runs the dense row scan with R and SCT at +inf
+// outside U (so those columns never exclude an op nor keep it out of the
+// snapshot, is_op_in_snapshot :236-258), SCT's missing DCs at 0, LastOpCt
+// outside U kept at SCT's value and its DC set = SCT's | (U if any op was
+// included).  Any other key goes to the `mix` list, served by the per-entry-
+// mask (SPARSE) kernel in a second launch.
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, int CAP, int WPB, int RB,
-          bool WARM, bool SLOW, bool CT>
+          bool WARM, bool SLOW, bool CT, bool MSK>
 __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, agn_result out,
-                                                   uint32_t *wl, uint32_t *wl_n, uint32_t xcd) {
+                                                   TagLists tl, uint32_t xcd) {
     using S = Shape<DPL, LPO>;
     constexpr int OPI = S::OPI;
     static_assert(!CT || (DPL == 4 && FULL && !SPARSE), "CT: dense rows, 4 DCs per lane");
+    static_assert(!MSK || (FULL && !SPARSE), "MSK: the dense row scans");
     constexpr int P = CT ? DPL * LPO / 2 : 1;  // 16-byte parts per op
     constexpr int OPH = AGN_WAVE / P;          // ops per 1 KiB load (OPI / 2)
     __shared__ CandLds<CAP> Lall[WPB];
@@ -205,12 +223,12 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
     const uint32_t D = log.n_dcs, W = n_words(D);
     const uint64_t lt = lanes_below();
-    const uint64_t n_items = SLOW ? (uint64_t)uniform_u64(*wl_n) : req.n_req;
+    const uint64_t n_items = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(*tl.in_n) : req.n_req;
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
 
     const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     for (uint64_t it = (uint64_t)blk * WPB + (uint64_t)w; it < n_items; it += nw) {
-        const uint64_t i = SLOW ? (uint64_t)__builtin_amdgcn_readfirstlane(wl[it]) : it;
+        const uint64_t i = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(tl.in[it]) : it;
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
         // The key's and the request's side values load together and
         // unconditionally (in-bounds dummies for absent columns): each
@@ -235,11 +253,30 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         const uint64_t b1v = uniform_u64((req.base_off ? bop + 1 : bop)[0]);
         const uint64_t n = log.key_len ? lv : lv - off;
 
+        uint64_t kmw = 0, rmw = 0, smw = 0;
+        if constexpr (MSK) {
+            kmw = uniform_u64(*(log.key_mask ? log.key_mask + key : req.R));
+            rmw = uniform_u64(*(req.R_mask ? req.R_mask + i : req.R));
+            smw = uniform_u64(*((req.sct && req.sct_mask) ? req.sct_mask + i : req.R));
+        }
+
         if (n != 0 && log.key_type != nullptr && kt != (uint32_t)(uint8_t)req.req_type) {
             if (lane == 0) {  // erlang:error(corrupted_ops_cache) (:190-191)
                 out.flags[i] = AGN_F_ERR_CORRUPTED;
                 out.err_pos[i] = 0xffffffffu;
                 out.out_n[i] = 0;
+            }
+            continue;
+        }
+        // MSK: the key's DC set U, R's and SCT's (see above)
+        const uint64_t FULLW = low_bits(D);
+        const uint64_t mU = !MSK ? FULLW : log.oc_mask ? (log.key_mask ? (kmw & FULLW) : 0ull) : FULLW;
+        const uint64_t mR = (MSK && req.R_mask) ? (rmw & FULLW) : FULLW;
+        const uint64_t mS = (MSK && req.sct && req.sct_mask) ? (smw & FULLW) : FULLW;
+        if (MSK && !(n == 0 || (mU != 0ull && (mU & ~mR) == 0ull))) {
+            if (lane == 0) {
+                const uint32_t at = atomicAdd(tl.mix_n, 1u);
+                tl.mix[at] = (uint32_t)i;
             }
             continue;
         }
@@ -249,7 +286,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         const uint64_t *sctp = req.sct ? req.sct : req.R;
         const uint32_t rbits = chunk_bits<DPL, SPARSE>(req.R_mask, i, W, d0, D);
         const uint32_t sbits = sct_ign ? 0u : chunk_bits<DPL, SPARSE>(req.sct_mask, i, W, d0, D);
-        uint64_t r[DPL], s[DPL], ct[DPL];
+        uint64_t r[DPL], s[DPL], ct[DPL], e[DPL];
 #pragma unroll
         for (int j = 0; j < DPL; ++j) {
             const uint32_t d = (uint32_t)(d0 + j);
@@ -261,11 +298,19 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             // LastOpCt starts as SnapshotCommitTime (materialize/4 :94-95);
             // "+1 encoded" in sparse mode (0 = DC absent from the dict)
             ct[j] = ((sbits >> j) & 1u) ? (SPARSE ? s[j] + 1ull : s[j]) : 0ull;
+            if constexpr (MSK) {  // dict read of SCT; +inf outside U
+                const bool inU = d < D && ((mU >> (d & 63u)) & 1ull);
+                e[j] = (sct_ign || d >= D || !((mS >> (d & 63u)) & 1ull)) ? 0ull : sv;
+                ct[j] = e[j];
+                s[j] = inU ? e[j] : ~0ull;
+                r[j] = inU ? r[j] : ~0ull;
+            }
         }
         const uint64_t txr = req.txid ? txv : 0ull;
         const bool use_tx = txr != 0ull && log.txid != nullptr;
         // CT: this lane's parts of R / SCT / LastOpCt (DCs dp, dp + 1)
-        uint64_t rA = 0, rB = 0, sA = 0, sB = 0, ctA = 0, ctB = 0;
+        uint64_t rA = 0, rB = 0, sA = 0, sB = 0, ctA = 0, ctB = 0, eA = 0, eB = 0;
+        bool uA = true, uB = true;  // MSK: this lane's DCs are in U
         if constexpr (CT) {
             const uint32_t dp = 2u * (uint32_t)(lane % P);
             rA = req.R[i * D + dp];
@@ -275,8 +320,20 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 sA = sct_ign ? 0ull : xa;
                 sB = sct_ign ? 0ull : xb;
             }
-            ctA = sA;
-            ctB = sB;
+            if constexpr (MSK) {
+                uA = ((mU >> (dp & 63u)) & 1ull) != 0ull;
+                uB = ((mU >> ((dp + 1u) & 63u)) & 1ull) != 0ull;
+                sA = ((mS >> (dp & 63u)) & 1ull) ? sA : 0ull;
+                sB = ((mS >> ((dp + 1u) & 63u)) & 1ull) ? sB : 0ull;
+                eA = sA;
+                eB = sB;
+                rA = uA ? rA : ~0ull;
+                rB = uB ? rB : ~0ull;
+                sA = uA ? sA : ~0ull;
+                sB = uB ? sB : ~0ull;
+            }
+            ctA = MSK ? eA : sA;
+            ctB = MSK ? eB : sB;
         }
 
         // ---- base snapshot state: candidates with ord = index (< B)
@@ -512,8 +569,8 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         // ---- fast path overflow: hand the key to the 4096-slot pass
         if (!SLOW && overflow && first_err < 0) {
             if (lane == 0) {
-                const uint32_t at = atomicAdd(wl_n, 1u);
-                wl[at] = (uint32_t)i;
+                const uint32_t at = atomicAdd(tl.ovf_n, 1u);
+                tl.ovf[at] = (uint32_t)i;
             }
             continue;
         }
@@ -538,6 +595,17 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 
         // ---- LastOpCt: max over the lanes that hold the same DC slice
         const bool ct_ign = sct_ign && cnt == 0u;
+        if constexpr (MSK) {  // outside U: SCT's value (an op's row there is not in its dict)
+            ctA = uA ? ctA : eA;
+            ctB = uB ? ctB : eB;
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) {
+                const uint32_t d = (uint32_t)(d0 + j);
+                ct[j] = (d < D && ((mU >> (d & 63u)) & 1ull)) ? ct[j] : e[j];
+            }
+            if (out.lastct_mask != nullptr && lane == 0)
+                out.lastct_mask[i] = ct_ign ? 0ull : ((sct_ign ? 0ull : mS) | (cnt ? mU : 0ull));
+        }
         if constexpr (CT) {
 #pragma unroll
             for (int x = P; x < AGN_WAVE; x <<= 1) {
@@ -606,38 +674,81 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 // profiles/r01/ab_tags_wpb_unbiased.log)
 constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 1, RBATCH = 2;
 
+// One fast pass (grid = the batch, or a resident grid over a list) and the
+// 4096-slot pass over its overflow list.  `in` / `in_n`: the requests (NULL =
+// the batch); lists: the scratch of the launch sequence.
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM, bool CT, bool MSK>
+hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result &out,
+                       const uint32_t *in, const uint32_t *in_n, uint32_t *ovf, uint32_t *ovf_n,
+                       uint32_t *mix, uint32_t *mix_n, hipStream_t st) {
+    // one wave per key: the grid is the batch (the wave dispatcher then
+    // overlaps keys; AGN_TAGS_GRID=<blocks> caps it for A/B); a list pass
+    // grid-strides over a resident grid
+    const char *ge = getenv("AGN_TAGS_GRID");
+    const unsigned cap = in ? 8192u : ge ? (unsigned)atoi(ge) : 0x7fffffffu;
+    const unsigned blocks = grid_for(req.n_req, FAST_WPB, cap);
+    TagLists fast{in, in_n, ovf, ovf_n, mix, mix_n};
+    hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, WARM, false,
+                               CT, MSK>),
+                       dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, fast,
+                       xcd_remap() ? 1u : 0u);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    TagLists slow{ovf, ovf_n, nullptr, nullptr, mix, mix_n};
+    hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM, true, CT,
+                               MSK>),
+                       dim3(256), dim3(64), 0, st, log, req, out, slow, 0u);
+    return hipGetLastError();
+}
+
+// Scratch of a launch sequence: [0] overflow count, [1] mixed-key count,
+// [2] the mixed keys' overflow count, then three lists of n_req entries.
+struct TagScratch {
+    uint32_t *base = nullptr;
+    uint64_t n = 0;
+    uint32_t *ovf_n() const { return base; }
+    uint32_t *mix_n() const { return base + 1; }
+    uint32_t *ovf2_n() const { return base + 2; }
+    uint32_t *ovf() const { return base + 4; }
+    uint32_t *mix() const { return base + 4 + n; }
+    uint32_t *ovf2() const { return base + 4 + 2 * n; }
+};
+
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM, bool CT>
 int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
                  hipStream_t st) {
-    // worklist of keys whose live state overflows the fast table: [0] = count
-    uint32_t *wl = nullptr;
-    AGN_HIP(pool_malloc((void **)&wl, (req.n_req + 1) * sizeof(uint32_t), st));
-    int rc = AGN_OK;
-    {
-        hipError_t e = hipMemsetAsync(wl, 0, sizeof(uint32_t), st);
-        // one wave per key: the grid is the batch (the wave dispatcher then
-        // overlaps keys; AGN_TAGS_GRID=<blocks> caps it for A/B)
-        const char *ge = getenv("AGN_TAGS_GRID");
-        const unsigned blocks =
-            grid_for(req.n_req, FAST_WPB, ge ? (unsigned)atoi(ge) : 0x7fffffffu);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH,
-                                       WARM, false, CT>),
-                               dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, wl + 1,
-                               wl, xcd_remap() ? 1u : 0u);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM,
-                                       true, CT>),
-                               dim3(256), dim3(64), 0, st, log, req, out, wl + 1, wl, 0u);
-            e = hipGetLastError();
-        }
-        if (e != hipSuccess) rc = fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
-    }
-    const hipError_t ef = hipFreeAsync(wl, st);
+    TagScratch w;
+    w.n = req.n_req;
+    AGN_HIP(pool_malloc((void **)&w.base, (3 * req.n_req + 4) * sizeof(uint32_t), st));
+    hipError_t e = hipMemsetAsync(w.base, 0, 4 * sizeof(uint32_t), st);
+    if (e == hipSuccess)
+        e = tags_passes<DPL, LPO, SPARSE, FULL, SET, WARM, CT, false>(
+            log, req, out, nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n(), st);
+    const int rc = e == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
+    const hipError_t ef = hipFreeAsync(w.base, st);
     if (rc == AGN_OK && ef != hipSuccess)
-        rc = fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
+        return fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
+    return rc;
+}
+
+// Presence masks with a dense-loadable shape: the MSK dense passes, then the
+// per-entry-mask (SPARSE) passes over the keys they handed on.
+template <int DPL, int LPO, bool SET, bool WARM, bool CT, int SDPL, int SLPO>
+int launch_masked(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    TagScratch w;
+    w.n = req.n_req;
+    AGN_HIP(pool_malloc((void **)&w.base, (3 * req.n_req + 4) * sizeof(uint32_t), st));
+    hipError_t e = hipMemsetAsync(w.base, 0, 4 * sizeof(uint32_t), st);
+    if (e == hipSuccess)
+        e = tags_passes<DPL, LPO, false, true, SET, WARM, CT, true>(
+            log, req, out, nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n(), st);
+    if (e == hipSuccess)
+        e = tags_passes<SDPL, SLPO, true, false, SET, WARM, false, false>(
+            log, req, out, w.mix(), w.mix_n(), w.ovf2(), w.ovf2_n(), nullptr, nullptr, st);
+    const int rc = e == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
+    const hipError_t ef = hipFreeAsync(w.base, st);
+    if (rc == AGN_OK && ef != hipSuccess)
+        return fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
     return rc;
 }
 
@@ -694,6 +805,33 @@ int dispatch(const agn_log &log, const agn_read &req, const agn_result &out, hip
 #undef AGN_L
 }
 
+// A sparse batch whose width has a dense-loadable shape (D = 2, 4, 6, 8: one
+// lane per op; 16, 32, 64: 4 DCs per lane, contiguous rows): AGN_ENOTSUP
+// otherwise (the SPARSE kernel then serves every key).  AGN_TAGS_MSK=0 (A/B
+// knob) disables it.
+template <bool SET>
+int dispatch_masked(const agn_log &log, const agn_read &req, const agn_result &out,
+                    hipStream_t st) {
+    const char *v = getenv("AGN_TAGS_MSK");
+    if (v && v[0] == '0') return AGN_ENOTSUP;
+    const bool warm = req.sct != nullptr;
+#define AGN_M(DPL, LPO, CTV, SD, SL)                                                         \
+    return warm ? launch_masked<DPL, LPO, SET, true, CTV, SD, SL>(log, req, out, st)       \
+                : launch_masked<DPL, LPO, SET, false, CTV, SD, SL>(log, req, out, st)
+    switch (log.n_dcs) {
+        case 2: AGN_M(2, 1, false, 2, 1);
+        case 4: AGN_M(4, 1, false, 4, 1);
+        case 6: AGN_M(6, 1, false, 6, 1);
+        case 8: AGN_M(8, 1, false, 8, 1);
+        case 16: if (tags_ct()) AGN_M(4, 4, true, 8, 2); break;
+        case 32: if (tags_ct()) AGN_M(4, 8, true, 8, 4); break;
+        case 64: if (tags_ct()) AGN_M(4, 16, true, 8, 8); break;
+        default: break;
+    }
+#undef AGN_M
+    return AGN_ENOTSUP;
+}
+
 }  // namespace
 
 int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
@@ -701,6 +839,11 @@ int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
     if (req.n_req == 0) return AGN_OK;
     const bool sparse = log.oc_mask || req.R_mask || req.sct_mask || out.lastct_mask;
     const bool set = log.crdt_type == AGN_SET_AW;
+    if (sparse) {
+        const int rc = set ? dispatch_masked<true>(log, req, out, st)
+                           : dispatch_masked<false>(log, req, out, st);
+        if (rc != AGN_ENOTSUP) return rc;
+    }
     if (sparse) return set ? dispatch<true, true>(log, req, out, st)
                            : dispatch<true, false>(log, req, out, st);
     return set ? dispatch<false, true>(log, req, out, st) : dispatch<false, false>(log, req, out, st);

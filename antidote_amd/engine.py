@@ -238,6 +238,24 @@ class Engine:
         check(self.lib.agn_materialize(self.ctx, C.byref(ls), C.byref(rs), C.byref(os_), stream),
               "agn_materialize")
 
+    def bind_materialize(self, dlog, dreq, dres, stream=None):
+        """agn_materialize with its arguments converted once: returns a
+        zero-argument callable for repeated launches of the same batch (a
+        small batch's step is otherwise dominated by the per-call ctypes
+        argument conversion)."""
+        ls = dlog.struct if isinstance(dlog, DeviceArrays) else dlog
+        rs = dreq.struct if isinstance(dreq, DeviceArrays) else dreq
+        os_ = dres.struct if isinstance(dres, DeviceArrays) else dres
+        fn, ctx = self.lib.agn_materialize, self.ctx
+        args = (ctx, C.byref(ls), C.byref(rs), C.byref(os_), stream)
+        keep = (ls, rs, os_)  # the structs outlive the callable
+
+        def call(_fn=fn, _args=args, _keep=keep):
+            rc = _fn(*_args)
+            if rc:
+                check(rc, "agn_materialize")
+        return call
+
     def tune(self, dlog, dreq, dres, stream=None, rounds=3):
         """agn_tune: time the bit-identical kernel variants of this batch's
         path, select the fastest for this device; returns (choice, ms) with

@@ -154,7 +154,8 @@ def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0, mask_keys=0, mask_ops=0):
         return ops * per_op + n_keys * per_key + 24 * mask_keys + 8 * mask_ops
     per_op = 8 * D + 4 + 4 + 8 + 4            # oc, op_id, tag, add_tok, rem_off
     per_key = 8 + 8 * D + 8 * D + 24 + 8 + 4  # key_off, R, LastOpCt, hole/count/flags/err, out_off, out_n
-    return ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key
+    return (ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key + 24 * mask_keys +
+            8 * mask_ops)
 
 
 def presence_masks(mode, D, n_ops, n_keys, rng=None, torch=None):
@@ -299,17 +300,18 @@ def main():
     if a.sparse:
         # presence masks on every clock, as the Erlang NIF's partition logs
         # carry them; agn_log.key_mask as the engine-owned op log maintains it
-        if cfg["crdt_type"] != 1:
-            raise SystemExit("--sparse: counter_pn configs (1, 2)")
         ocm_t, rm_t = presence_masks(a.sparse, cfg["n_dcs"], int(dl.n_entries), n_keys,
                                      torch=torch)
         dl.oc_mask, dr.R_mask = ocm_t.data_ptr(), rm_t.data_ptr()
         kmask = eng.index_masks(dl, sp)
         km = eng.download(kmask, np.uint64, (n_keys,), stream=sp)
         mixed = int((km == 0).sum())
+        # counter_pn reads a mask per entry only for the keys whose entries
+        # differ (agn_log.key_mask); the set/register kernel reads every one
+        per_entry = mixed if cfg["crdt_type"] == 1 else n_keys
         presence = {"mode": a.sparse, "key_mask": "agn_log_index_masks",
                     "uniform_keys": n_keys - mixed, "mixed_keys": mixed,
-                    "mask_ops": mixed * cfg["ops_per_key"]}
+                    "mask_ops": per_entry * cfg["ops_per_key"]}
     res = eng.alloc_result(n_keys, cfg["n_dcs"], sparse=bool(a.sparse), cap_off=cap)
 
     def barrier():

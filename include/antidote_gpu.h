@@ -589,7 +589,10 @@ typedef struct agn_log_records {
  * reverse_and_add_op_id, :586-591; 1 for the op_insert_gc ids of
  * load_from_log, src/materializer_vnode.erl:288-319), txid = the
  * transaction id.  out_totals (device, may be NULL) = {ops, removal tokens}.
- * Requires n_keys < 2^24 and n < 2^40. */
+ * Keys index the partition's key space [0, n_keys): a partition's log holds
+ * only its own keys (every update is logged at its key's partition,
+ * src/log_utilities.erl:58-68), and a record naming a key outside it is
+ * another partition's and is skipped.  Requires n_keys < 2^24 and n < 2^40. */
 int agn_log_ingest(agn_ctx *ctx, const agn_log_records *recs, uint32_t crdt_type,
                    uint32_t n_dcs, uint64_t n_keys, const uint64_t *max_time,
                    const uint64_t *max_time_mask, uint32_t op_id_base, agn_log *out,

@@ -396,7 +396,14 @@ int oracle_log_ingest(const agn_log_records *r, uint32_t crdt, uint32_t D, uint6
             if (!tab[s].used || tab[s].head < 0) continue; /* dict:find -> error */
             for (int64_t u = tab[s].head; u >= 0; u = next[u]) {
                 const uint64_t k = r->key[u];
-                if (k >= K) continue; /* not this partition's key (agn_log_ingest skips it too) */
+                /* A partition's log holds only its own keys: logging_vnode writes
+                 * every update to the log of its key's partition
+                 * (log_utilities:get_key_partition / get_preflist_from_key,
+                 * src/log_utilities.erl:58-68; the log id is [Partition],
+                 * src/materializer_vnode.erl:289-292), so the partition's key
+                 * index space [0, K) covers its log.  A record outside it
+                 * belongs to another partition's table and is not loaded here. */
+                if (k >= K) continue;
                 int ok = 1;
                 if (max_t) /* check_max_time: vectorclock:le(SnapshotTime, Max) */
                     ok = oracle_vc_le(D, r->ss + x * D, r->ss_mask ? r->ss_mask + x * W : NULL,

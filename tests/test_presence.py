@@ -35,13 +35,13 @@ pytestmark = pytest.mark.gpu
 
 
 def presence_case(seed, K, D, nmax, *, p_uniform=0.7, p_cover=0.85, garbage=True, warm=0.4,
-                  **kw):
+                  crdt=_abi.COUNTER_PN, with_cap=False, **kw):
     """random_case with per-key DC sets: a fraction p_uniform of the keys have
     one DC set U on every entry; R covers U for a fraction p_cover of the
     reads; absent columns of op rows, R and SCT hold garbage."""
-    log, req, cap = random_case(seed, _abi.COUNTER_PN, K, D, nmax, sparse=True, warm=warm, **kw)
+    log, req, cap = random_case(seed, crdt, K, D, nmax, sparse=True, warm=warm, **kw)
     rng = np.random.default_rng(seed + 1)
-    full = (1 << D) - 1
+    full = (1 << D) - 1 if D < 64 else (1 << 64) - 1
     keys = req.keys
     inv = np.empty(K, np.int64)
     inv[keys.astype(np.int64)] = np.arange(K)
@@ -49,12 +49,12 @@ def presence_case(seed, K, D, nmax, *, p_uniform=0.7, p_cover=0.85, garbage=True
         a, b = int(log.key_off[k]), int(log.key_off[k + 1])
         i = inv[k]
         if rng.random() < p_uniform:
-            U = int(rng.integers(1, full + 1))
+            U = int(rng.integers(1, min(full, (1 << 62)) + 1))
             log.oc_mask[a:b, 0] = np.uint64(U)
         else:
             U = int(np.bitwise_or.reduce(log.oc_mask[a:b, 0])) if b > a else full
         if rng.random() < p_cover:
-            req.R_mask[i, 0] = np.uint64(U | int(rng.integers(0, full + 1)))
+            req.R_mask[i, 0] = np.uint64(U | int(rng.integers(0, min(full, (1 << 62)) + 1)))
         # a few present values are 0 (a DC at time 0 is still present)
         z = rng.random((b - a, D)) < 0.02
         log.oc[a:b][z] = 0
@@ -66,11 +66,11 @@ def presence_case(seed, K, D, nmax, *, p_uniform=0.7, p_cover=0.85, garbage=True
         req.R[~rb] = big(int((~rb).sum()))
         sb = ((req.sct_mask[:, :1] >> np.arange(D, dtype=np.uint64)) & np.uint64(1)).astype(bool)
         req.sct[~sb] = big(int((~sb).sum()))
-    return log, req
+    return (log, req, cap) if with_cap else (log, req)
 
 
-def oracle_result(oracle_lib, log, req):
-    res = alloc_result(req.n_req, log.n_dcs, sparse=True)
+def oracle_result(oracle_lib, log, req, cap=None):
+    res = alloc_result(req.n_req, log.n_dcs, sparse=True, cap_off=cap)
     ls, rs, os_ = log_struct(log), read_struct(req, sparse=True), result_struct(res)
     assert oracle_lib.oracle_materialize(C.byref(ls), C.byref(rs), C.byref(os_), 4) == 0
     return res
@@ -109,6 +109,30 @@ def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
     assert not bad, bad[:10]
     # absent LastOpCt columns are 0, as the oracle writes them (a corrupted
     # key's result is only its error)
+    m = got.lastct_mask[:, 0]
+    written = (got.flags & _abi.F_ERR_CORRUPTED) == 0
+    for d in range(D):
+        absent = (((m >> np.uint64(d)) & np.uint64(1)) == 0) & written
+        assert not got.lastct[absent, d].any()
+
+
+@pytest.mark.parametrize("msk", ["1", "0"])
+@pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])
+@pytest.mark.parametrize("D", [2, 3, 8, 12, 16, 32, 64])
+def test_tags_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, crdt, msk):
+    """set_aw / register_mv with presence masks: the dense passes for the keys
+    whose entries share a DC set inside R (D = 2, 4, 6, 8, 16, 32, 64), the
+    per-entry-mask kernel for the rest (and for every key at other widths, or
+    with AGN_TAGS_MSK=0)."""
+    monkeypatch.setenv("AGN_TAGS_MSK", msk)
+    log, req, cap = presence_case(3000 * crdt + D, 160 if D < 32 else 90, D, 140, crdt=crdt,
+                                  with_cap=True, txid=0.3, invalid=0.02, corrupt=0.03, base=0.4,
+                                  multi=0.15 if crdt == _abi.SET_AW else 0.0,
+                                  identity=(D % 2 == 0))
+    want = oracle_result(oracle_lib, log, req, cap)
+    got = eng.materialize_host(log, req, sparse=True, cap_off=cap)
+    bad = compare(crdt, D, got, want, True, req.n_req)
+    assert not bad, bad[:10]
     m = got.lastct_mask[:, 0]
     written = (got.flags & _abi.F_ERR_CORRUPTED) == 0
     for d in range(D):
