@@ -58,6 +58,18 @@ expand() {
         echo "gcwrite$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_gcwrite$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
         echo "gcpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_gcfetch$c/run_counter_collection.csv gpurun_out/prof_gcwrite$c/run_counter_collection.csv k_prune_inplace $n gc gpurun_out/pmc/gc_cfg$c.json"
       done;;
+    pmcsparse)
+      # cfg2 with presence masks (bench.py --sparse MODE): the masked counter kernel
+      for m in ${PMC_SPARSE-full mixed}; do
+        echo "sfetch$m|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_sfetch$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "swrite$m|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_swrite$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "spmcj$m|60|python3 scripts/pmc_traffic.py gpurun_out/prof_sfetch$m/run_counter_collection.csv gpurun_out/prof_swrite$m/run_counter_collection.csv k_counter_key 10000000 2 gpurun_out/pmc/cfg2_sparse_$m.json"
+      done;;
+    pmctail)
+      # the engine-owned log's in-place GC (k_prune_tail) on the prefix-drop bench
+      echo "tfetch|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_tfetch -o run -- python3 scripts/bench_oplog_prune.py 2000000 64 3"
+      echo "twrite|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_twrite -o run -- python3 scripts/bench_oplog_prune.py 2000000 64 3"
+      echo "tpmcj|60|python3 scripts/pmc_traffic.py gpurun_out/prof_tfetch/run_counter_collection.csv gpurun_out/prof_twrite/run_counter_collection.csv k_prune_tail 2000000 gc gpurun_out/pmc/oplog_prune_tail.json";;
     serve)
       # native read/6 serving (tools/serve_bench): 250k keys x 64 ops per
       # partition, D = 8, 20 read servers per partition; 1 and 8 partitions
@@ -66,7 +78,18 @@ expand() {
       echo "serve1|150|./tools/serve_bench parts=1 threads=20 reads=20000"
       echo "serve8|150|./tools/serve_bench parts=8 threads=20 reads=5000"
       echo "serve8w|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000"
-      echo "serve8h|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000 hot=2000";;
+      echo "serve8h|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000 hot=2000"
+      # the logs the Erlang NIF builds: presence masks on every clock, all 8
+      # DCs interned, or 3 of 8 columns interned (partition width 8)
+      echo "serve1s|150|./tools/serve_bench parts=1 threads=20 reads=20000 sparse=1"
+      echo "serve8s|150|./tools/serve_bench parts=8 threads=20 reads=5000 sparse=1"
+      echo "serve8sw|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000 sparse=1"
+      echo "serve8s3|150|./tools/serve_bench parts=8 threads=20 reads=5000 sparse=1 present=3"
+      echo "serve8sh|150|./tools/serve_bench parts=8 threads=20 reads=5000 wps=2000 hot=2000 sparse=1"
+      # set_aw / register_mv partitions (states in the device cache's arena)
+      echo "serve8set|150|./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000 sparse=1"
+      echo "serve8reg|150|./tools/serve_bench type=register parts=8 threads=20 reads=5000 wps=2000 sparse=1"
+      echo "serve8seth|150|./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000 hot=2000 sparse=1";;
     *) echo "$1";;
   esac
 }

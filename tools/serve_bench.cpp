@@ -21,8 +21,14 @@
 // reads' R, LastOpCt), `dcs` columns of which the first `present` are
 // interned DCs (the rest absent from every dict clock).
 //
-//   serve_bench [keys=N] [ops=N] [dcs=N] [present=N] [sparse=0|1] [parts=N]
-//               [threads=N] [reads=N] [batch=N] [wait=US] [wps=N] [hot=N]
+// type=set|register serves set_aw / register_mv partitions instead (16
+// elements / values per key; an add / assign removes / overrides the key's
+// previous token of it, as the CRDTs' downstream does): their snapshot states
+// live in the cache's device arena.
+//
+//   serve_bench [type=counter|set|register] [keys=N] [ops=N] [dcs=N] [present=N]
+//               [sparse=0|1] [parts=N] [threads=N] [reads=N] [batch=N] [wait=US]
+//               [wps=N] [hot=N]
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -60,13 +66,30 @@ struct Partition {
     agn_batcher *b = nullptr;
     std::vector<uint64_t> clock;                   // writer's copy
     std::unique_ptr<std::atomic<uint64_t>[]> pub;  // published clock (readers' R)
+    std::vector<uint64_t> last;                    // set/register: last token per key x elem
+    uint64_t tok = 1;
 };
+
+constexpr uint64_t NE = 16;  // set elements / register values per key
+
+// One set/register effect of key k (writer state in pt): tag, add token and
+// the tokens it removes / overrides.
+void tag_effect(Partition &pt, uint32_t crdt, uint64_t k, uint64_t &seed, uint32_t &tag,
+                uint64_t &add, std::vector<uint64_t> &rems) {
+    const uint64_t e = splitmix(seed) % NE;
+    tag = (uint32_t)e;
+    add = pt.tok++;
+    uint64_t &l = pt.last[crdt == AGN_SET_AW ? k * NE + e : k];
+    if (l) rems.push_back(l);
+    l = add;
+}
 
 }  // namespace
 
 int main(int argc, char **argv) {
     uint64_t K = 250000, N = 64, D = 8, P = 1, T = 20, M = 5000, batch = 1024, wait = 0, hot = 0;
     uint64_t sparse = 0, present = 0;
+    uint32_t crdt = AGN_COUNTER_PN;
     double wps = 0;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -89,6 +112,11 @@ int main(int argc, char **argv) {
         else if (k == "hot") hot = std::strtoull(v, nullptr, 10);
         else if (k == "sparse") sparse = std::strtoull(v, nullptr, 10);
         else if (k == "present") present = std::strtoull(v, nullptr, 10);
+        else if (k == "type") {
+            const std::string t = v;
+            crdt = t == "set" ? AGN_SET_AW : t == "register" ? AGN_REGISTER_MV : AGN_COUNTER_PN;
+            if (t != "set" && t != "register" && t != "counter") return 2;
+        }
         else {
             std::fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 2;
@@ -108,20 +136,27 @@ int main(int argc, char **argv) {
     double t_load = now_s();
     for (uint64_t p = 0; p < P; ++p) {
         Partition &pt = parts[p];
-        if ((rc = agn_oplog_create(ctx, AGN_COUNTER_PN, (uint32_t)D, K, (int)sparse, 0, &pt.log)))
+        const bool tags = crdt != AGN_COUNTER_PN;
+        if (tags) pt.last.assign(crdt == AGN_SET_AW ? K * NE : K, 0);
+        if ((rc = agn_oplog_create(ctx, crdt, (uint32_t)D, K, (int)sparse, 0, &pt.log)))
             die("agn_oplog_create", rc);
         // the partition's history: N ops per key, commit clocks increasing per DC
         pt.clock.assign(D, 1700000000000000ull);
         uint64_t seed = 20250112ull + p;
         const uint64_t chunk = 1u << 20;
-        std::vector<uint64_t> keys, oc, ocm;
+        std::vector<uint64_t> keys, oc, ocm, add, rem;
         std::vector<int64_t> eff;
+        std::vector<uint32_t> tag, roff;
         for (uint64_t done = 0; done < K * N;) {
             const uint64_t n = std::min(chunk, K * N - done);
             keys.resize(n);
             oc.resize(n * D);
             eff.resize(n);
             ocm.assign(sparse ? n : 0, pmask);
+            tag.resize(tags ? n : 0);
+            add.resize(tags ? n : 0);
+            roff.assign(tags ? n + 1 : 0, 0);
+            rem.clear();
             for (uint64_t i = 0; i < n; ++i) {
                 keys[i] = (done + i) % K;  // ops of keys interleave, as updates do
                 const uint32_t dc = (uint32_t)(splitmix(seed) % present);
@@ -132,10 +167,17 @@ int main(int argc, char **argv) {
                     oc[i * D + d] = d >= present ? 0 : d == dc ? c : (c > lag ? c - lag : 0);
                 }
                 eff[i] = (int64_t)(splitmix(seed) % 2001) - 1000;
+                if (tags) {
+                    tag_effect(pt, crdt, keys[i], seed, tag[i], add[i], rem);
+                    roff[i + 1] = (uint32_t)rem.size();
+                }
             }
+            if (tags && rem.empty()) rem.push_back(0);
             if ((rc = agn_oplog_append(pt.log, n, keys.data(), nullptr, oc.data(),
-                                       sparse ? ocm.data() : nullptr, nullptr, eff.data(),
-                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr)))
+                                       sparse ? ocm.data() : nullptr, nullptr,
+                                       tags ? nullptr : eff.data(), tags ? tag.data() : nullptr,
+                                       tags ? add.data() : nullptr, tags ? roff.data() : nullptr,
+                                       tags ? rem.data() : nullptr, nullptr, nullptr)))
                 die("agn_oplog_append", rc);
             done += n;
         }
@@ -155,7 +197,8 @@ int main(int argc, char **argv) {
     };
     // warm-up: the first 4096 keys of every partition once
     for (auto &pt : parts) {
-        std::vector<uint64_t> R, ct(D);
+        std::vector<uint64_t> R, ct(D), otok(4 * NE);
+        std::vector<uint32_t> otag(4 * NE);
         uint64_t ctm = 0;
         snapshot_clock(pt, R);
         agn_key_read rd{};
@@ -164,6 +207,9 @@ int main(int argc, char **argv) {
         rd.R_mask = sparse ? &pmask : nullptr;
         o.lastct = ct.data();
         o.lastct_mask = sparse ? &ctm : nullptr;
+        o.out_cap = (uint32_t)otag.size();
+        o.out_tag = otag.data();
+        o.out_tok = otok.data();
         for (uint64_t k = 0; k < std::min<uint64_t>(H, 4096); ++k) {
             rd.key = k;
             if ((rc = agn_batcher_read(pt.b, &rd, &o))) die("agn_batcher_read (warm-up)", rc);
@@ -182,16 +228,25 @@ int main(int argc, char **argv) {
                 uint64_t ws = 777 + p;
                 const double dt = 1.0 / wps;
                 double next = now_s();
-                std::vector<uint64_t> row(D);
+                std::vector<uint64_t> row(D), rems;
+                const bool tags = crdt != AGN_COUNTER_PN;
                 while (!stop.load(std::memory_order_relaxed)) {
                     const uint64_t key = splitmix(ws) % H;
                     const uint32_t dc = (uint32_t)(splitmix(ws) % present);
                     pt.clock[dc] += 1 + splitmix(ws) % 1000;
                     for (uint64_t d = 0; d < D; ++d) row[d] = d < present ? pt.clock[d] : 0;
                     const int64_t e = (int64_t)(splitmix(ws) % 2001) - 1000;
+                    uint32_t tg = 0, ro[2] = {0, 0};
+                    uint64_t ad = 0;
+                    rems.clear();
+                    if (tags) tag_effect(pt, crdt, key, ws, tg, ad, rems);
+                    ro[1] = (uint32_t)rems.size();
+                    if (rems.empty()) rems.push_back(0);
                     if (agn_oplog_append(pt.log, 1, &key, nullptr, row.data(),
-                                         sparse ? &pmask : nullptr, nullptr, &e, nullptr, nullptr,
-                                         nullptr, nullptr, nullptr, nullptr))
+                                         sparse ? &pmask : nullptr, nullptr, tags ? nullptr : &e,
+                                         tags ? &tg : nullptr, tags ? &ad : nullptr,
+                                         tags ? ro : nullptr, tags ? rems.data() : nullptr, nullptr,
+                                         nullptr))
                         die("agn_oplog_append (writer)", -1);
                     // published after the append: a read at the new clock sees the op
                     pt.pub[dc].store(pt.clock[dc], std::memory_order_release);
@@ -213,12 +268,16 @@ int main(int argc, char **argv) {
         th.emplace_back([&, t] {
             Partition &pt = parts[t % P];
             uint64_t s = 1000 + t;
-            std::vector<uint64_t> R, ct(D);
+            std::vector<uint64_t> R, ct(D), otok(4 * NE);
+            std::vector<uint32_t> otag(4 * NE);
             uint64_t ctm = 0;
             agn_key_read rd{};
             agn_key_result o{};
             o.lastct = ct.data();
             o.lastct_mask = sparse ? &ctm : nullptr;
+            o.out_cap = (uint32_t)otag.size();
+            o.out_tag = otag.data();
+            o.out_tok = otok.data();
             rd.R_mask = sparse ? &pmask : nullptr;
             lat[t].reserve(M);
             for (uint64_t i = 0; i < M; ++i) {
@@ -263,7 +322,7 @@ int main(int argc, char **argv) {
     }
     const uint64_t reads = NT * M;
     std::printf(
-        "{\"tool\": \"serve_bench\", \"log\": \"%s\", \"dcs_present\": %llu, "
+        "{\"tool\": \"serve_bench\", \"type\": \"%s\", \"log\": \"%s\", \"dcs_present\": %llu, "
         "\"parts\": %llu, \"keys_per_part\": %llu, \"hot_keys\": %llu, "
         "\"ops_per_key\": %llu, \"n_dcs\": %llu, \"threads_per_part\": %llu, \"reads\": %llu, "
         "\"max_batch\": %llu, \"max_wait_us\": %llu, \"writes_per_s_per_part\": %.0f, "
@@ -271,6 +330,7 @@ int main(int argc, char **argv) {
         "\"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
         "\"batches\": %llu, \"mean_batch\": %.2f, \"status\": {\"hit\": %llu, \"new\": %llu, "
         "\"log\": %llu}, \"errors\": %llu}\n",
+        crdt == AGN_SET_AW ? "set_aw" : crdt == AGN_REGISTER_MV ? "register_mv" : "counter_pn",
         sparse ? "sparse (presence masks, as the NIF builds it)" : "dense", (unsigned long long)present,
         (unsigned long long)P, (unsigned long long)K, (unsigned long long)H, (unsigned long long)N,
         (unsigned long long)D, (unsigned long long)T, (unsigned long long)reads,
