@@ -321,7 +321,14 @@ __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32
 
 constexpr int PT = 4;  // removal tokens a lane buffers per entry
 
-template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB>
+// CTL (dense rows, 8 DCs per lane-slice): an iteration's rows are read
+// lane-contiguously -- load j covers bytes [1 KiB j, 1 KiB (j+1)), whole
+// lines, lane l holding DCs 2p, 2p+1 (p = l mod P, P = D / 2) of op
+// j (64 / P) + l / P -- where the row-slice loads touch every line of the
+// iteration with each instruction and re-request it (the tags kernel's CT
+// rows, k_tags).  Verdicts are group-any folds of wave ballots; a kept row is
+// stored from the same registers (its parts' lanes fetch its destination).
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB, bool CTL = false>
 __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
                                                        const uint8_t *__restrict__ prune,
                                                        const uint64_t *__restrict__ thr,
@@ -329,6 +336,10 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
                                                        uint32_t *__restrict__ meta,
                                                        uint32_t *__restrict__ flags) {
     using S = Shape<DPL, LPO>;
+    static_assert(!CTL || (FULL && !SPARSE && DPL == 8), "CTL: dense 8-DC slices");
+    constexpr int P = DPL * LPO >= 2 ? DPL * LPO / 2 : 1;  // CTL: 16-byte parts per op
+    constexpr int OPL = AGN_WAVE / P;                      // CTL: ops per 1 KiB load
+    constexpr int NQ = DPL >= 2 ? DPL / 2 : 1;             // CTL: loads per lane
     // XCD-aware key order: consecutive keys (whose per-key outputs share lines)
     // run on one XCD's L2
     const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -372,6 +383,9 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         l.oc_mask = a.mask;
         return l;
     }();
+    // CTL: this lane's part of the threshold
+    const uint32_t cp = 2u * (uint32_t)(lane % P);
+    const uint64_t tA = CTL ? thr[k * D + cp] : 0ull, tB = CTL ? thr[k * D + cp + 1u] : 0ull;
     uint64_t written = 0;
     uint32_t rwritten = 0, first_id = AGN_ID0_NONE, last_id = 0;
     bool consec = true;
@@ -381,8 +395,18 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         const uint64_t e = off + (valid ? pos : 0ull);
         // the raw row (absent DCs included: a kept row moves bit for bit)
         uint64_t o[DPL];
-        uint32_t obits;
-        if constexpr (FULL) {
+        uint32_t obits = 0;
+        u64x2 qx[NQ];
+        if constexpr (CTL) {
+            const u64x2 *rows = reinterpret_cast<const u64x2 *>(a.oc);
+            const uint64_t lim = (off + n) * (uint64_t)P - 1u;  // the key's last part
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                uint64_t u = (off + b) * (uint64_t)P + (uint64_t)(j * AGN_WAVE + lane);
+                u = u < lim ? u : lim;
+                qx[j] = __builtin_nontemporal_load(rows + u);
+            }
+        } else if constexpr (FULL) {
             load_rows<DPL, SPARSE, FULL>(rl, e, d0, D, W, o, obits);
         } else {
             obits = chunk_bits<DPL, SPARSE>(a.mask, e, W, d0, D);
@@ -412,12 +436,20 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         const bool late = a.late_fields < 0 ? TAGS : a.late_fields != 0;
         if (!late && valid && sub == 0) load_fields();
         bool le = true;
+        if constexpr (CTL) {
+            uint64_t gtm = 0;  // ops with a DC above the threshold
 #pragma unroll
-        for (int j = 0; j < DPL; ++j)
-            if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
-        if (LPO > 1) {
-            const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
-            le = (ballot(!le) & grp) == 0ull;
+            for (int j = 0; j < NQ; ++j)
+                gtm |= group_any<P>(ballot(qx[j].x > tA || qx[j].y > tB)) << (j * OPL);
+            le = ((gtm >> slot) & 1ull) == 0ull;
+        } else {
+#pragma unroll
+            for (int j = 0; j < DPL; ++j)
+                if ((obits >> j) & 1u) le = le && (o[j] <= t[j]);
+            if (LPO > 1) {
+                const uint64_t grp = ((1ull << LPO) - 1ull) << (slot * LPO);
+                le = (ballot(!le) & grp) == 0ull;
+            }
         }
         const bool kp = valid && (!gc || !le);  // belongs_to_snapshot_op(Threshold, op)
         // set_aw / register_mv: 32 B of fields per entry, loaded for the kept
@@ -452,7 +484,16 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // stores
-        if (kp) {
+        if constexpr (CTL) {
+#pragma unroll
+            for (int j = 0; j < NQ; ++j) {
+                const int hq = (j * OPL + lane / P) * LPO;  // head lane of this part's op
+                const uint64_t dq = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), hq, AGN_WAVE) << 32) |
+                                    (uint32_t)__shfl((int)(uint32_t)dst, hq, AGN_WAVE);
+                if ((km >> hq) & 1ull)
+                    reinterpret_cast<u64x2 *>(a.d_oc)[dq * (uint64_t)P + (uint64_t)(lane % P)] = qx[j];
+            }
+        } else if (kp) {
             if constexpr (FULL) {
                 u64x2 *q = reinterpret_cast<u64x2 *>(a.d_oc + dst * D + (uint32_t)d0);
 #pragma unroll
@@ -909,6 +950,21 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
                                dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
                                flags);                                                         \
     } while (0)
+    // contiguous rows (CTL) for dense 8-DC slices: AGN_PRUNE_CT=1 (A/B knob)
+    if constexpr (DPL == 8 && !SPARSE) {
+        const char *cv = getenv("AGN_PRUNE_CT");
+        if (full && cv && cv[0] == '1') {
+            if (tags)
+                hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, false, true, true, 1, true>),
+                                   dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,
+                                   flags);
+            else
+                hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, false, true, false, 1, true>),
+                                   dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,
+                                   flags);
+            return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_inplace launch");
+        }
+    }
     if (full) {
         if (tags) AGN_K((DPL % 2 == 0), true);
         else AGN_K((DPL % 2 == 0), false);

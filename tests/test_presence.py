@@ -298,3 +298,102 @@ def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6):
         lnd, lld, ctd = ld.key_meta()
     assert served > 600 and n_cmp > 800, (served, n_cmp)
     assert np.array_equal(lns, lnd) and np.array_equal(lls, lld) and np.array_equal(cts, ctd)
+
+
+# ---------------------------------------------------------------- full size
+def entry_masks(e, D, mode, xp):
+    """Deterministic per-entry presence words of a global entry index e (the
+    same on the device with torch and on the host with numpy): 'full' = every
+    DC, 'mixed' = one entry in 8 lacks one DC."""
+    full = (1 << D) - 1
+    if mode == "full":
+        return e * 0 + full
+    h = (e * 2654435761) & 0xFFFFFFFF
+    dc = (h >> 8) % D
+    one = e * 0 + 1
+    drop = (h >> 29) == 0
+    return xp.where(drop, full & ~(one << dc), full)
+
+
+FULL_MASKED = [
+    ("cfg2", dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0,
+                  seed=20250113), "full"),
+    ("cfg2", dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0,
+                  seed=20250113), "mixed"),
+    ("cfg2-warm", dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0,
+                       seed=20250113, warm=1), "mixed"),
+    ("cfg3", dict(crdt_type=2, n_dcs=16, n_keys=1_000_000, ops_per_key=256, n_elems=32,
+                  seed=20250114), "full"),
+    ("cfg3", dict(crdt_type=2, n_dcs=16, n_keys=1_000_000, ops_per_key=256, n_elems=32,
+                  seed=20250114), "mixed"),
+]
+
+
+@pytest.mark.parametrize("name,spec,mode", FULL_MASKED,
+                         ids=[f"{n}-{m}" for n, _, m in FULL_MASKED])
+def test_full_size_masked_sampled(eng, oracle_lib, name, spec, mode):
+    """BASELINE shapes with presence masks on every op clock and read (the
+    NIF's partition logs, bench.py --sparse): key DC sets indexed on the
+    device, every key materialized, a sample bit-exact against the oracle
+    (host-generated keys with the same masks)."""
+    import torch
+    from antidote_amd.engine import free_gen_host, gen_host
+    cfg = _abi.AgnGenCfg(**{"key_base": 0, "key_stride": 1, "warm": 0, **spec})
+    K, D, N = cfg.n_keys, cfg.n_dcs, cfg.ops_per_key
+    dl, dr = eng.gen_dev(cfg)
+    E = int(dl.n_entries)
+    assert E == K * N
+    e = torch.arange(E, dtype=torch.int64, device="cuda")
+    ocm = entry_masks(e, D, mode, torch)
+    del e
+    rm = torch.full((K,), (1 << D) - 1, dtype=torch.int64, device="cuda")
+    dl.oc_mask, dr.R_mask = ocm.data_ptr(), rm.data_ptr()
+    cap = np.arange(K + 1, dtype=np.uint64) * np.uint64(N) if cfg.crdt_type != 1 else None
+    res = eng.alloc_result(K, D, sparse=True, cap_off=cap)
+    kb = None
+    try:
+        kb = eng.index_masks(dl)
+        torch.cuda.synchronize()
+        eng.materialize(dl, dr, res)
+        eng.sync()
+        flags = eng.download(res.bufs["flags"], np.uint32, (K,))
+        assert not (flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED |
+                             _abi.F_ERR_CAPACITY)).any()
+        rng = np.random.default_rng(cfg.seed + 7)
+        sample = np.sort(rng.choice(K, 48, replace=False))
+        sample[0], sample[-1] = 0, K - 1
+        full = eng.fetch_result(res)
+        for k in sample:
+            c1 = _abi.AgnGenCfg(crdt_type=cfg.crdt_type, n_dcs=D, n_keys=1, ops_per_key=N,
+                                n_elems=cfg.n_elems, seed=cfg.seed, key_base=int(k),
+                                key_stride=1, warm=cfg.warm)
+            hl, hr = gen_host(c1)
+            hm = entry_masks(np.arange(int(k) * N, (int(k) + 1) * N, dtype=np.int64), D, mode,
+                             np).astype(np.uint64).reshape(N, 1)
+            hrm = np.full((1, 1), (1 << D) - 1, np.uint64)
+            hl.oc_mask, hr.R_mask = hm.ctypes.data, hrm.ctypes.data
+            capo = np.array([0, N], np.uint64) if cfg.crdt_type != 1 else None
+            w = alloc_result(1, D, sparse=True, cap_off=capo)
+            assert oracle_lib.oracle_materialize(C.byref(hl), C.byref(hr),
+                                                 C.byref(result_struct(w)), 1) == 0
+            hl.oc_mask = hr.R_mask = None
+            free_gen_host(hl, hr)
+            assert int(full.flags[k]) == int(w.flags[0]), k
+            assert int(full.hole[k]) == int(w.hole[0]), k
+            assert int(full.count[k]) == int(w.count[0]), k
+            assert np.array_equal(full.lastct[k], w.lastct[0]), k
+            assert np.array_equal(full.lastct_mask[k], w.lastct_mask[0]), k
+            if cfg.crdt_type == 1:
+                assert int(full.value[k]) == int(w.value[0]), k
+            else:
+                n, o = int(full.out_n[k]), int(full.out_off[k])
+                assert n == int(w.out_n[0]), k
+                assert np.array_equal(full.out_tag[o:o + n], w.out_tag[:n]), k
+                assert np.array_equal(full.out_tok[o:o + n], w.out_tok[:n]), k
+    finally:
+        dl.oc_mask = dr.R_mask = dl.key_mask = None
+        eng.free_gen(dl, dr)
+        for b in list(res.bufs.values()) + ([kb] if kb else []):
+            b.free()
+        del ocm, rm
+        torch.cuda.empty_cache()
