@@ -377,5 +377,64 @@ __device__ __forceinline__ void scan_key_q8(
     }
 }
 
+// scan_key_q8 for a key whose entries carry different DC sets (presence
+// masks, D = 8): the quad rows as above plus each op's mask word (lane = op,
+// loaded with the effects), which the lanes holding its parts read with one
+// shuffle per load.  The dict fold of is_op_in_snapshot (:236-258) per part:
+// a DC of the op missing from R (rm) excludes it, absent DCs are not
+// compared, SCT's absent DCs are 0 in sA / sB; LastOpCt takes each included
+// op's present DCs only, and um (lane = op) collects the included ops' sets.
+template <bool WARM>
+__device__ __forceinline__ void scan_key_q8_msk(
+    const uint64_t *__restrict__ oc, const uint64_t *__restrict__ oc_mask,
+    const int64_t *__restrict__ eff, const uint64_t *__restrict__ txid, uint64_t txr,
+    uint64_t off, uint64_t n, uint64_t n_entries, uint64_t rA, uint64_t rB, uint64_t sA,
+    uint64_t sB, uint64_t rm, uint64_t &ctA, uint64_t &ctB, uint64_t &um, int64_t &sum,
+    uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+    const int lane = lane_id();
+    const int q = lane >> 2, p = lane & 3;
+    const uint64_t lim_e = n_entries - 1u;
+    for (uint64_t b = 0; b < n; b += AGN_WAVE) {
+        const Q8Chunk c = q8_load<true, false>(oc, eff, off, b, n_entries);
+        uint64_t e = off + b + (uint64_t)lane;
+        e = e < lim_e ? e : lim_e;
+        const uint32_t m = (uint32_t)(oc_mask ? oc_mask[e] : 0xFFull) & 0xFFu;
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t valid = (n - b >= (uint64_t)AGN_WAVE) ? ~0ull : ((1ull << (n - b)) - 1ull);
+        // ops with a DC missing from R
+        const uint64_t noR = ballot((m & ~(uint32_t)rm) != 0u);
+        uint64_t bad = noR, gt = 0, pres[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t mq = (uint32_t)__shfl((int)m, 16 * j + q, AGN_WAVE);
+            pres[j] = mq;
+            const bool pa = (mq >> (2 * p)) & 1u, pb = (mq >> (2 * p + 1)) & 1u;
+            bad |= nib_any16(ballot((pa && c.x[j].x > rA) || (pb && c.x[j].y > rB))) << (16 * j);
+            if (WARM)
+                gt |= nib_any16(ballot((pa && c.x[j].x > sA) || (pb && c.x[j].y > sB))) << (16 * j);
+        }
+        uint64_t nip = WARM ? gt : ~0ull;
+        if (txid != nullptr) nip |= ballot(txid[e] == txr);
+        const uint64_t incl = valid & nip & ~bad, excl = valid & nip & bad;
+        if (first_excl < 0 && excl) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(excl);
+        cnt += (uint32_t)__builtin_popcountll(incl);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool in = ((incl >> (16 * j + q)) & 1ull) != 0ull;
+            const bool pa = (pres[j] >> (2 * p)) & 1u, pb = (pres[j] >> (2 * p + 1)) & 1u;
+            ctA = (in && pa && c.x[j].x > ctA) ? c.x[j].x : ctA;
+            ctB = (in && pb && c.x[j].y > ctB) ? c.x[j].y : ctB;
+        }
+        const bool mine = ((incl >> lane) & 1ull) != 0ull;
+        um |= mine ? (uint64_t)m : 0ull;
+        const bool badv = mine && c.ev == AGN_EFFECT_INVALID;
+        if (first_err < 0) {
+            const uint64_t be = ballot(badv);
+            if (be) first_err = (int64_t)b + (int64_t)__builtin_ctzll(be);
+        }
+        sum += (mine && !badv) ? c.ev : 0;
+    }
+}
+
 }  // namespace
 }  // namespace agn

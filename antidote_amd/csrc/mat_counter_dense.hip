@@ -333,13 +333,15 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
                 ctB = ((pr.U >> (2 * p + 1)) & 1ull) ? ctB : eB;
             }
         } else if constexpr (MSK) {
-            AGN_MSK_SCAN();
-#pragma unroll
-            for (int j = 0; j < D; ++j)
-#pragma unroll
-                for (int x = 1; x < AGN_WAVE; x <<= 1) ct[j] = umax64(ct[j], shfl_xor_u64(ct[j], x));
-            ctA = p == 0 ? ct[0] : p == 1 ? ct[2 % D] : p == 2 ? ct[4 % D] : ct[6 % D];
-            ctB = p == 0 ? ct[1 % D] : p == 1 ? ct[3 % D] : p == 2 ? ct[5 % D] : ct[7 % D];
+            // a mixed key: the quad rows with each op's mask word
+            if (!warm)
+                scan_key_q8_msk<false>(oc, mk.oc_mask, eff, tx, txr, off, n, a.n_entries, rA, rB,
+                                       sA, sB, pr.Rm, ctA, ctB, um, sum, cnt, first_excl,
+                                       first_err);
+            else
+                scan_key_q8_msk<ANY_WARM>(oc, mk.oc_mask, eff, tx, txr, off, n, a.n_entries, rA,
+                                          rB, sA, sB, pr.Rm, ctA, ctB, um, sum, cnt, first_excl,
+                                          first_err);
         }
 #undef AGN_Q8
     } else if constexpr (GLDS && D % 2 == 0) {
@@ -563,35 +565,17 @@ template <bool ANY_WARM>
 __device__ __forceinline__ void q2_msk(const Q2Key &k, const uint64_t *__restrict__ oc,
                                        const uint64_t *__restrict__ oc_mask,
                                        const int64_t *__restrict__ eff,
-                                       const uint64_t *__restrict__ log_txid, Q2Acc &s) {
-    constexpr int D = 8;
-    uint64_t r[D], sv[D], ct[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const int p = j >> 1;
-        const uint64_t vr = (j & 1) ? k.rB : k.rA, vs = (j & 1) ? k.sB : k.sA,
-                       ve = (j & 1) ? k.eB : k.eA;
-        r[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vr >> 32), p) << 32) |
-               __builtin_amdgcn_readlane((uint32_t)vr, p);
-        sv[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(vs >> 32), p) << 32) |
-                __builtin_amdgcn_readlane((uint32_t)vs, p);
-        ct[j] = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ve >> 32), p) << 32) |
-                __builtin_amdgcn_readlane((uint32_t)ve, p);
-    }
+                                       const uint64_t *__restrict__ log_txid, uint64_t n_entries,
+                                       Q2Acc &s) {
     const uint64_t *tx = k.txr ? log_txid : nullptr;
     if (ANY_WARM && !k.sct_ign)
-        scan_key_msk<D, true>(oc, oc_mask, eff, tx, k.txr, k.off, k.n, r, sv, k.Rm, ct, s.um,
-                              s.sum, s.cnt, s.first_excl, s.first_err);
+        scan_key_q8_msk<true>(oc, oc_mask, eff, tx, k.txr, k.off, k.n, n_entries, k.rA, k.rB,
+                              k.sA, k.sB, k.Rm, s.ctA, s.ctB, s.um, s.sum, s.cnt, s.first_excl,
+                              s.first_err);
     else
-        scan_key_msk<D, false>(oc, oc_mask, eff, tx, k.txr, k.off, k.n, r, sv, k.Rm, ct, s.um,
-                               s.sum, s.cnt, s.first_excl, s.first_err);
-#pragma unroll
-    for (int j = 0; j < D; ++j)
-#pragma unroll
-        for (int x = 1; x < AGN_WAVE; x <<= 1) ct[j] = umax64(ct[j], shfl_xor_u64(ct[j], x));
-    const int p = lane_id() & 3;
-    s.ctA = p == 0 ? ct[0] : p == 1 ? ct[2] : p == 2 ? ct[4] : ct[6];
-    s.ctB = p == 0 ? ct[1] : p == 1 ? ct[3] : p == 2 ? ct[5] : ct[7];
+        scan_key_q8_msk<false>(oc, oc_mask, eff, tx, k.txr, k.off, k.n, n_entries, k.rA, k.rB,
+                               k.sA, k.sB, k.Rm, s.ctA, s.ctB, s.um, s.sum, s.cnt, s.first_excl,
+                               s.first_err);
 }
 
 template <bool MSK>
@@ -698,8 +682,10 @@ __global__ __launch_bounds__(64) void k_counter_quad2(
         if (d0) q2_rest<ANY_WARM>(k0, oc, eff, log_txid, a.n_entries, s0);
         if (d1) q2_rest<ANY_WARM>(k1, oc, eff, log_txid, a.n_entries, s1);
         if constexpr (MSK) {
-            if (!k0.corrupt && !k0.uni) q2_msk<ANY_WARM>(k0, oc, mk.oc_mask, eff, log_txid, s0);
-            if (!k1.corrupt && !k1.uni) q2_msk<ANY_WARM>(k1, oc, mk.oc_mask, eff, log_txid, s1);
+            if (!k0.corrupt && !k0.uni)
+                q2_msk<ANY_WARM>(k0, oc, mk.oc_mask, eff, log_txid, a.n_entries, s0);
+            if (!k1.corrupt && !k1.uni)
+                q2_msk<ANY_WARM>(k1, oc, mk.oc_mask, eff, log_txid, a.n_entries, s1);
         }
     }
     q2_epilogue<MSK>(k0, s0, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err,

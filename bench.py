@@ -339,21 +339,23 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
-    # the launch's ctypes arguments converted once (a cfg1 step is ~10 us of
-    # kernel: per-call conversion would be a third of it)
+    # the launch's ctypes arguments converted once, and HIP events on the
+    # launch stream around the K timed launches only (an event pair around
+    # every launch measured 14.7 us per cfg1 step against 6.8 us without:
+    # profiles/r03/first_ovh.log) -- kernel_ms is then the kernel's average
+    # duration back to back on its stream
     step = eng.bind_materialize(dl, dr, res, stream=sp)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for s in range(a.steps):
-        ev[s][0].record(stream)
         step()
-        ev[s][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([b.elapsed_time(e) for b, e in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / a.steps
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

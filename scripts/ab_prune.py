@@ -1,7 +1,8 @@
 """A/B of the one-pass prune kernel (agn_prune_ops segmented form, the kernel
 agn_oplog_prune runs in place) on the cfg2 log, variants alternated in one
 process (process-to-process HBM variance is several %):
-  AGN_PRUNE_WPB = 1 | 4 (waves per block) x AGN_PRUNE_LATE_FIELDS = 0 | 1
+  round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT = 0 | 1); round
+  2: AGN_PRUNE_WPB = 1 | 4 (waves per block) x AGN_PRUNE_LATE_FIELDS = 0 | 1
   (entry fields with the rows, or only for kept entries after the filter).
   Earlier runs also compared AGN_XCD_REMAP and non-temporal row loads /
   stores (no effect, removed): profiles/r02/ab_prune_*.log.
@@ -47,12 +48,13 @@ def main():
         out.bufs[name] = eng.empty(nb)
         setattr(s, name, out.bufs[name].ptr)
     din = DeviceArrays(dl)
-    variants = [("wpb1_early", "1", "0"), ("wpb1_late", "1", "1"), ("wpb4_early", "4", "0"),
-                ("wpb4_late", "4", "1")]
+    # round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT), default fields
+    variants = [("rows", "1", "0"), ("ct", "1", "1")]
     best = {v[0]: [] for v in variants}
+    sums = {}
     for r in range(rounds):
-        for name, wpb, late in (variants if r % 2 == 0 else variants[::-1]):
-            os.environ["AGN_PRUNE_WPB"], os.environ["AGN_PRUNE_LATE_FIELDS"] = wpb, late
+        for name, wpb, ct in (variants if r % 2 == 0 else variants[::-1]):
+            os.environ["AGN_PRUNE_WPB"], os.environ["AGN_PRUNE_CT"] = wpb, ct
             eng.prune_ops(din, None, dr.R, None, out)
             torch.cuda.synchronize()
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -61,8 +63,12 @@ def main():
             e.record()
             torch.cuda.synchronize()
             best[name].append(b.elapsed_time(e))
+            if r == 0:  # the variants' outputs must be identical
+                kl = eng.download(out.bufs["key_len"], np.uint64, (K,))
+                ocs = eng.download(out.bufs["oc"], np.uint64, (E * D,))
+                sums[name] = (int(kl.sum()), int(np.bitwise_xor.reduce(ocs)))
     print(json.dumps({"config": config, "ms_median": {k: float(np.median(v)) for k, v in best.items()},
-                      "ms_all": best}), flush=True)
+                      "ms_all": best, "outputs_equal": len(set(sums.values())) == 1}), flush=True)
 
 
 if __name__ == "__main__":
