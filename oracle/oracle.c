@@ -272,9 +272,13 @@ static void materialize_one(const agn_log *log, const agn_read *req, agn_result 
     uint64_t *oct = out->lastct + i * D;
     for (uint32_t d = 0; d < D; ++d)
         oct[d] = ct_ignore ? 0 : (((ctm[d >> 6] >> (d & 63)) & 1u) ? ct[d] : 0);
-    if (out->lastct_mask) {
+    if (out->lastct_mask) {  /* the dict's DCs: bits of columns < D only */
         uint64_t *om = out->lastct_mask + i * W;
-        for (uint32_t w = 0; w < W; ++w) om[w] = ct_ignore ? 0 : ctm[w];
+        for (uint32_t w = 0; w < W; ++w) {
+            const uint32_t left = D - 64u * w;
+            const uint64_t cols = left >= 64u ? ~0ull : ((1ull << left) - 1ull);
+            om[w] = ct_ignore ? 0 : (ctm[w] & cols);
+        }
     }
 }
 
