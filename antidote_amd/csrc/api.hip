@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -100,12 +101,15 @@ hipError_t pool_of(int dev, hipMemPool_t *out) {
 hipError_t pool_malloc(void **p, size_t bytes, hipStream_t st) {
     // test hook: AGN_TEST_POOL_FAIL=n makes the n-th allocation from now fail
     // (tests/test_oplog.py drives the all-or-nothing paths with it)
-    {
+    // (unset -- every production call -- costs one getenv and no lock)
+    static std::atomic<bool> was_armed{false};
+    const char *v = getenv("AGN_TEST_POOL_FAIL");
+    if (v || was_armed.load(std::memory_order_relaxed)) {
         static std::mutex mu;
         static std::string armed;
         static long left = 0;
-        const char *v = getenv("AGN_TEST_POOL_FAIL");
         std::lock_guard<std::mutex> g(mu);
+        was_armed.store(v != nullptr, std::memory_order_relaxed);
         if (!v) {
             armed.clear();
         } else {
@@ -850,8 +854,6 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
     if (n_req >= read_cached_split()) return read_cached_seq(cache, log, n_req, keys, R, txid,
                                                              should_gc, out, status, prune,
                                                              threshold, st);
-    uint64_t *dkeys = nullptr;  // the kernel's copy of the batch's keys (read batcher's GC list)
-    AGN_HIP(pool_malloc((void **)&dkeys, n_req * sizeof(uint64_t), st));
     Read6Args a;
     a.key_off = log->key_off;
     a.key_len = log->key_len;
@@ -877,12 +879,10 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
     a.err_pos = out->err_pos;
     a.status = status;
     a.prune = prune;
-    a.dkeys = dkeys;
-    a.dprune = prune;
+    a.dkeys = nullptr;  // the batcher's GC list copies: not needed here
+    a.dprune = nullptr;
     a.thr = threshold;
-    rc = launch_read6(*cache, a, st);
-    (void)hipFreeAsync(dkeys, st);
-    return rc;
+    return launch_read6(*cache, a, st);
 }
 
 int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,

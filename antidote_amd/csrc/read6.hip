@@ -155,8 +155,8 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             a.err_pos[i] = 0xffffffffu;
             a.status[i] = (uint8_t)st;
             a.prune[i] = 0;
-            a.dkeys[i] = key;
-            a.dprune[i] = 0;
+            if (a.dkeys) a.dkeys[i] = key;
+            if (a.dprune) a.dprune[i] = 0;
         }
         if (lane < D) a.lastct[i * D + (uint64_t)lane] = 0ull;
         return;
@@ -301,8 +301,8 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         a.err_pos[i] = first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
         a.status[i] = (uint8_t)st;
         a.prune[i] = pr ? 1 : 0;
-        a.dkeys[i] = key;
-        a.dprune[i] = pr ? 1 : 0;
+        if (a.dkeys) a.dkeys[i] = key;
+        if (a.dprune) a.dprune[i] = pr ? 1 : 0;
     }
 }
 

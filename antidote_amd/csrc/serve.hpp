@@ -62,7 +62,9 @@ struct Read6Args {
     uint64_t *lastct;
     uint32_t *count, *flags, *err_pos;
     uint8_t *status, *prune;
-    // device: the batch's keys and prune flags again, and the GC thresholds [K][D]
+    // device: the batch's keys and prune flags again (the batcher's GC list;
+    // either may be null when the caller has no GC list), and the GC
+    // thresholds [K][D]
     uint64_t *dkeys;
     uint8_t *dprune;
     uint64_t *thr;
