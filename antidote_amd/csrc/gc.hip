@@ -328,8 +328,9 @@ constexpr int PT = 4;  // removal tokens a lane buffers per entry
 // iteration with each instruction and re-request it (the tags kernel's CT
 // rows, k_tags).  Verdicts are group-any folds of wave ballots; a kept row is
 // stored from the same registers (its parts' lanes fetch its destination).
-template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB, bool CTL = false>
-__global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB, bool CTL = false,
+          int PF = 0>
+__global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : 1) void k_prune_inplace(InplaceArgs a,
                                                        const uint8_t *__restrict__ prune,
                                                        const uint64_t *__restrict__ thr,
                                                        const uint64_t *__restrict__ thr_mask,
@@ -337,6 +338,7 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
                                                        uint32_t *__restrict__ flags) {
     using S = Shape<DPL, LPO>;
     static_assert(!CTL || (FULL && !SPARSE && DPL == 8), "CTL: dense 8-DC slices");
+    static_assert(PF == 0 || !CTL, "PF: row-slice loads");
     constexpr int P = DPL * LPO >= 2 ? DPL * LPO / 2 : 1;  // CTL: 16-byte parts per op
     constexpr int OPL = AGN_WAVE / P;                      // CTL: ops per 1 KiB load
     constexpr int NQ = DPL >= 2 ? DPL / 2 : 1;             // CTL: loads per lane
@@ -356,13 +358,19 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
     const uint64_t n = uniform_u64(key_n(a.key_off, a.key_len, k));
     const bool gc = a.key_list ? a.list_flags[i] != 0 : (prune == nullptr || prune[k] != 0);
     const uint32_t tb = tags ? (uint32_t)uniform_u64(a.rem_off[off]) : 0u;
+    // the ETS ListLen, with the key's metadata: unconditional (a dummy word
+    // when there is none), so it shares their round trip instead of costing
+    // one of its own after the scan
+    const uint32_t lc0 = __builtin_amdgcn_readfirstlane(
+        *(a.key_lcap ? a.key_lcap + k : reinterpret_cast<const uint32_t *>(a.key_off + k)));
+    const uint32_t lc_in = a.key_lcap ? lc0 : 0u;
     if (lane == 0 && a.d_key_off) a.d_key_off[k] = off;
     if (!gc && !a.copy_unselected) {
         if (lane == 0) {
             if (meta) {
                 meta[i] = (uint32_t)n;
                 meta[K + i] = tags ? a.rem_off[off + n] - tb : 0u;
-                meta[2 * K + i] = a.key_lcap ? a.key_lcap[k] : 0u;
+                meta[2 * K + i] = lc_in;
                 meta[3 * K + i] = a.key_id0 ? a.key_id0[k] : AGN_ID0_NONE;
                 if (a.meta6) {
                     meta[4 * K + i] = (uint32_t)off;
@@ -389,6 +397,25 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
     uint64_t written = 0;
     uint32_t rwritten = 0, first_id = AGN_ID0_NONE, last_id = 0;
     bool consec = true;
+    // PF: the next iteration's rows are requested once this iteration's
+    // filter has decided, so they are in flight while its fields, removal
+    // tokens and stores wait (the next rows are above every destination of
+    // this iteration: in place, the early load reads them unchanged)
+    uint64_t on[DPL];
+    uint32_t onb = 0;
+    auto load_slice = [&](uint64_t ee, uint64_t (&v)[DPL], uint32_t &bits) {
+        if constexpr (FULL) {
+            load_rows<DPL, SPARSE, FULL>(rl, ee, d0, D, W, v, bits);
+        } else {
+            bits = chunk_bits<DPL, SPARSE>(a.mask, ee, W, d0, D);
+#pragma unroll
+            for (int j = 0; j < DPL; ++j)
+                v[j] = ((uint32_t)(d0 + j) < D) ? a.oc[ee * D + (uint32_t)(d0 + j)] : 0ull;
+        }
+    };
+    if constexpr (PF != 0) {
+        if (n) load_slice(off + ((uint64_t)slot < n ? (uint64_t)slot : 0ull), on, onb);
+    }
     for (uint64_t b = 0; b < n; b += S::OPI) {
         const uint64_t pos = b + (uint64_t)slot;
         const bool valid = pos < n;
@@ -397,7 +424,11 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         uint64_t o[DPL];
         uint32_t obits = 0;
         u64x2 qx[NQ];
-        if constexpr (CTL) {
+        if constexpr (PF != 0) {
+#pragma unroll
+            for (int j = 0; j < DPL; ++j) o[j] = on[j];
+            obits = onb;
+        } else if constexpr (CTL) {
             const u64x2 *rows = reinterpret_cast<const u64x2 *>(a.oc);
             const uint64_t lim = (off + n) * (uint64_t)P - 1u;  // the key's last part
 #pragma unroll
@@ -456,6 +487,10 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
         // entries only once the filter has decided; counter_pn: 20 B, loaded
         // with the row (one round trip less; measured, scripts/ab_prune.py)
         if (late && kp && sub == 0) load_fields();
+        if constexpr (PF != 0) {
+            const uint64_t pn = b + (uint64_t)S::OPI + (uint64_t)slot;
+            if (b + (uint64_t)S::OPI < n) load_slice(off + (pn < n ? pn : 0ull), on, onb);
+        }
         const uint64_t km = ballot(kp && sub == 0);  // one bit per kept op (its sub-0 lane)
         const uint32_t nk = (uint32_t)__builtin_popcountll(km);
         const uint32_t rank = (uint32_t)__builtin_popcountll(km & ((1ull << (slot * LPO)) - 1ull) &
@@ -579,7 +614,7 @@ __global__ __launch_bounds__(64 * WPB) void k_prune_inplace(InplaceArgs a,
     if (lane == 0) {
         const uint32_t l = (uint32_t)written;
         const uint32_t id0 = (l && consec && first_id != AGN_ID0_NONE) ? first_id : AGN_ID0_NONE;
-        uint32_t lc = a.key_lcap ? a.key_lcap[k] : 0u;
+        uint32_t lc = lc_in;
         if (lc && gc) {
             lc = resize_list_len_dev(l ? l : 1u, lc);  // prune_ops' NewLength (1 if none kept)
             if (lc < l) lc = l;
@@ -656,13 +691,20 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
     // token range [tb, te) of the key, read before any store
     const uint32_t tb = TAGS ? __builtin_amdgcn_readfirstlane(a.rem_off[off]) : 0u;
     const uint32_t te = TAGS ? __builtin_amdgcn_readfirstlane(a.rem_off[off + n]) : 0u;
-    const uint32_t id0_old = a.key_id0 ? __builtin_amdgcn_readfirstlane(a.key_id0[k]) : AGN_ID0_NONE;
+    // the id index and the ETS ListLen, with the key's metadata:
+    // unconditional (a dummy word when absent), so they share its round trip
+    // instead of costing one of their own (ListLen: after the scan)
+    const uint32_t *dummy = reinterpret_cast<const uint32_t *>(a.key_off + k);
+    const uint32_t id0_raw = __builtin_amdgcn_readfirstlane(*(a.key_id0 ? a.key_id0 + k : dummy));
+    const uint32_t lc0 = __builtin_amdgcn_readfirstlane(*(a.key_lcap ? a.key_lcap + k : dummy));
+    const uint32_t id0_old = a.key_id0 ? id0_raw : AGN_ID0_NONE;
+    const uint32_t lc_in = a.key_lcap ? lc0 : 0u;
     if (!gc) {
         if (lane == 0) {
             if (meta) {
                 meta[i] = (uint32_t)n;
                 meta[K + i] = te - tb;
-                meta[2 * K + i] = a.key_lcap ? a.key_lcap[k] : 0u;
+                meta[2 * K + i] = lc_in;
                 meta[3 * K + i] = id0_old;
                 meta[4 * K + i] = (uint32_t)off;
                 meta[5 * K + i] = tb;
@@ -894,7 +936,7 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
                 id0 = low_id;
             }
         }
-        uint32_t lc = a.key_lcap ? a.key_lcap[k] : 0u;
+        uint32_t lc = lc_in;
         if (lc) {
             lc = resize_list_len_dev(l ? l : 1u, lc);  // prune_ops' NewLength (1 if none kept)
             if (lc < l) lc = l;
@@ -964,6 +1006,32 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
                                    flags);
             return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_inplace launch");
         }
+    }
+    // next iteration's rows prefetched (PF) for keys that span iterations:
+    // AGN_PRUNE_PF=0|1|2 (A/B knob; 2: held to 5 waves per SIMD)
+    const char *pv = getenv("AGN_PRUNE_PF");
+    const int pf = (!w4 && pv && (pv[0] == '1' || pv[0] == '2')) ? pv[0] - '0' : 0;
+    if (pf) {
+#define AGN_P(FULLV, TAGSV)                                                                    \
+    do {                                                                                       \
+        if (pf == 2)                                                                           \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1, false, 2>), \
+                               dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
+                               flags);                                                         \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1, false, 1>), \
+                               dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
+                               flags);                                                         \
+    } while (0)
+        if (full) {
+            if (tags) AGN_P((DPL % 2 == 0), true);
+            else AGN_P((DPL % 2 == 0), false);
+        } else {
+            if (tags) AGN_P(false, true);
+            else AGN_P(false, false);
+        }
+#undef AGN_P
+        return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_inplace launch");
     }
     if (full) {
         if (tags) AGN_K((DPL % 2 == 0), true);

@@ -631,7 +631,7 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
     from antidote_amd import _abi
     D = cfg["n_dcs"]
     if cfg["crdt_type"] != 1:
-        return None  # set/register states need a caller state store for the handles
+        return warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps)
     S = _abi.SNAPSHOT_THRESHOLD
     bufs = {"n": eng.empty(4 * n_keys), "clock": eng.empty(8 * n_keys * S * D),
             "last_op": eng.empty(8 * n_keys * S), "value": eng.empty(8 * n_keys * S),
@@ -719,6 +719,110 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
             "cache_hit_frac": float((hits == _abi.SS_HIT).mean()),
             "mean_applied_ops": float(cnt.mean()),
             "error_keys": int((flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED)).astype(bool).sum())}
+
+
+def warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps):
+    """read/6 of set_aw / register_mv keys from the device snapshot cache
+    (materializer_vnode.erl:384-413,466-509: the cached #materialized_snapshot
+    value is the full state): the cache carries a state arena, so a hit's base
+    state is read by the tags kernel straight from HBM (AGN_SS_STATE
+    references) and the store appends the new state to the arena -- no state
+    crosses PCIe.  Priming pass = cold read + store; timed steps = lookup ->
+    materialize from the cached state -> store, then the same through
+    agn_read_cached (the batched kernels)."""
+    from antidote_amd import _abi
+    D, N = cfg["n_dcs"], cfg["ops_per_key"]
+    S = _abi.SNAPSHOT_THRESHOLD
+    # a state never holds more pairs than its key has adding entries (<= N)
+    cap_off = np.arange(n_keys + 1, dtype=np.uint64) * np.uint64(N)
+    arena_cap = 2 * n_keys * N
+    bufs = {"n": eng.empty(4 * n_keys), "clock": eng.empty(8 * n_keys * S * D),
+            "last_op": eng.empty(8 * n_keys * S), "value": eng.empty(8 * n_keys * S),
+            "sct": eng.empty(8 * n_keys * D), "ign": eng.empty(n_keys), "base": eng.empty(8 * n_keys),
+            "first": eng.empty(n_keys), "status": eng.empty(n_keys), "prune": eng.empty(n_keys),
+            "thr": eng.empty(8 * n_keys * D), "ctl": eng.empty(32),
+            "st_tag": eng.empty(4 * arena_cap), "st_tok": eng.empty(8 * arena_cap)}
+    eng.lib.agn_memset_d(eng.ctx, bufs["n"].ptr, 0, 4 * n_keys, sp)
+    eng.lib.agn_memset_d(eng.ctx, bufs["ctl"].ptr, 0, 32, sp)
+    c = _abi.AgnSsCache()
+    c.n_dcs, c.slots, c.n_keys = D, S, n_keys
+    c.n, c.clock, c.last_op, c.value = (bufs[x].ptr for x in ("n", "clock", "last_op", "value"))
+    c.state_tag, c.state_tok, c.state_cap, c.state_ctl = (bufs["st_tag"].ptr, bufs["st_tok"].ptr,
+                                                          arena_cap, bufs["ctl"].ptr)
+    req = _abi.AgnRead()
+    C.memmove(C.addressof(req), C.addressof(dr), C.sizeof(_abi.AgnRead))
+    req.sct, req.sct_ignore, req.base_value = bufs["sct"].ptr, bufs["ign"].ptr, bufs["base"].ptr
+    req.base_off, req.base_tag, req.base_tok = None, bufs["st_tag"].ptr, bufs["st_tok"].ptr
+    res = eng.alloc_result(n_keys, D, sparse=False, cap_off=cap_off)
+
+    def lookup():
+        eng.ss_lookup(c, n_keys, None, dr.R, None, bufs["sct"].ptr, None, bufs["ign"].ptr,
+                      bufs["base"].ptr, bufs["first"].ptr, bufs["status"].ptr, sp)
+
+    def store():
+        eng.ss_store(c, dl, n_keys, None, bufs["first"].ptr, bufs["status"].ptr, None, res, None,
+                     bufs["prune"].ptr, bufs["thr"].ptr, None, sp)
+    for _ in range(2):  # priming: absent keys -> empty snapshot -> cold read -> store
+        lookup()
+        eng.materialize(dl, req, res, sp)
+        store()
+    torch.cuda.synchronize()
+    hits = eng.download(bufs["status"], np.uint8, (n_keys,))
+    base_pairs = int((eng.download(bufs["base"], np.int64, (n_keys,)).astype(np.uint64)
+                      & np.uint64(0xFFFFFF)).sum())  # AGN_SS_STATE_PAIRS
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t_lookup = t_mat = t_store = 0.0
+    for _ in range(steps):
+        ev[0].record()
+        lookup()
+        ev[1].record()
+        eng.materialize(dl, req, res, sp)
+        ev[2].record()
+        store()
+        ev[3].record()
+        torch.cuda.synchronize()
+        t_lookup += ev[0].elapsed_time(ev[1])
+        t_mat += ev[1].elapsed_time(ev[2])
+        t_store += ev[2].elapsed_time(ev[3])
+    ms = (t_lookup + t_mat + t_store) / steps
+    flags = eng.download(res.bufs["flags"], np.uint32, (n_keys,))
+    cnt = eng.download(res.bufs["count"], np.uint32, (n_keys,))
+    n_live = int(eng.download(res.bufs["out_n"], np.uint32, (n_keys,)).astype(np.int64).sum())
+    dkeys = eng.upload(np.arange(n_keys, dtype=np.uint64))
+    t_rc = 0.0
+    for i in range(steps + 1):
+        ev[0].record()
+        eng.read_cached(c, dl, n_keys, dkeys.ptr, dr.R, dr.txid, None, res,
+                        bufs["status"].ptr, bufs["prune"].ptr, bufs["thr"].ptr, sp)
+        ev[1].record()
+        torch.cuda.synchronize()
+        if i:
+            t_rc += ev[0].elapsed_time(ev[1])
+    hits_rc = eng.download(bufs["status"], np.uint8, (n_keys,))
+    ctl = eng.download(bufs["ctl"], np.uint64, (4,))
+    E = n_keys * N
+    n_rem = int(eng.download(type("B", (), {"ptr": dl.rem_off})(), np.uint32, (E + 1,))[-1])
+    for b in list(bufs.values()) + list(res.bufs.values()) + [dkeys]:
+        b.free()
+    ops = n_keys * N
+    # the warm materialize's bytes: the cold kernel's, plus per request the SCT
+    # row, its ignore flag and the base reference, and the base pairs read
+    wbytes = (algorithmic_bytes(cfg, n_keys, n_rem, n_live) + n_keys * (8 * D + 1 + 8)
+              + 12 * base_pairs)
+    return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
+            "materialize_algorithmic_bytes": wbytes,
+            "materialize_frac": wbytes / (t_mat / steps * 1e-3) / 8e12,
+            "store_ms": t_store / steps, "ops_per_s": ops / (ms * 1e-3),
+            "read_cached_ms": t_rc / steps, "read_cached_ops_per_s": ops / (t_rc / steps * 1e-3),
+            "read_cached_hit_frac": float((hits_rc == _abi.SS_HIT).mean()),
+            "vc_compares_per_s": 2 * ops / (ms * 1e-3),
+            "cache_hit_frac": float((hits == _abi.SS_HIT).mean()),
+            "base_pairs": base_pairs, "live_pairs": n_live,
+            "arena_pairs_used": int(ctl[0]), "arena_overflow": int(ctl[2]),
+            "mean_applied_ops": float(cnt.mean()),
+            "state_path": "device (cache state arena; AGN_SS_STATE references)",
+            "error_keys": int((flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED |
+                                        _abi.F_ERR_CAPACITY)).astype(bool).sum())}
 
 
 def gc_bench(eng, dl, dr, cfg, n_keys, sp, torch, cfg_id):

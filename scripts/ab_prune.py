@@ -1,7 +1,8 @@
 """A/B of the one-pass prune kernel (agn_prune_ops segmented form, the kernel
 agn_oplog_prune runs in place) on the cfg2 log, variants alternated in one
 process (process-to-process HBM variance is several %):
-  round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT = 0 | 1); round
+  round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT = 0 | 1), and
+  the next iteration's rows prefetched (AGN_PRUNE_PF = 0 | 1 | 2); round
   2: AGN_PRUNE_WPB = 1 | 4 (waves per block) x AGN_PRUNE_LATE_FIELDS = 0 | 1
   (entry fields with the rows, or only for kept entries after the filter).
   Earlier runs also compared AGN_XCD_REMAP and non-temporal row loads /
@@ -48,13 +49,19 @@ def main():
         out.bufs[name] = eng.empty(nb)
         setattr(s, name, out.bufs[name].ptr)
     din = DeviceArrays(dl)
-    # round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT), default fields
-    variants = [("rows", "1", "0"), ("ct", "1", "1")]
+    # round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT), and the
+    # next iteration's rows prefetched (AGN_PRUNE_PF; 2 = held to 5 waves)
+    variants = [("rows", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0"}),
+                ("ct", {"AGN_PRUNE_CT": "1", "AGN_PRUNE_PF": "0"}),
+                ("pf4", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "1"}),
+                ("pf5", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "2"})]
+    os.environ["AGN_PRUNE_WPB"] = "1"
     best = {v[0]: [] for v in variants}
     sums = {}
+    chk = ["key_len", "oc", "op_id"] + (["eff"] if cfg["crdt_type"] == 1 else ["tag", "add_tok", "rem_tok"])
     for r in range(rounds):
-        for name, wpb, ct in (variants if r % 2 == 0 else variants[::-1]):
-            os.environ["AGN_PRUNE_WPB"], os.environ["AGN_PRUNE_CT"] = wpb, ct
+        for name, env in (variants if r % 2 == 0 else variants[::-1]):
+            os.environ.update(env)
             eng.prune_ops(din, None, dr.R, None, out)
             torch.cuda.synchronize()
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,9 +71,12 @@ def main():
             torch.cuda.synchronize()
             best[name].append(b.elapsed_time(e))
             if r == 0:  # the variants' outputs must be identical
-                kl = eng.download(out.bufs["key_len"], np.uint64, (K,))
-                ocs = eng.download(out.bufs["oc"], np.uint64, (E * D,))
-                sums[name] = (int(kl.sum()), int(np.bitwise_xor.reduce(ocs)))
+                sig = []
+                for c in chk:
+                    nb = out.bufs[c].nbytes if hasattr(out.bufs[c], "nbytes") else spec[c]
+                    a = eng.download(out.bufs[c], np.uint8, (nb // 8 * 8,)).view(np.uint64)
+                    sig.append(int(np.bitwise_xor.reduce(a)) if a.size else 0)
+                sums[name] = tuple(sig)
     print(json.dumps({"config": config, "ms_median": {k: float(np.median(v)) for k, v in best.items()},
                       "ms_all": best, "outputs_equal": len(set(sums.values())) == 1}), flush=True)
 
