@@ -854,7 +854,7 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
     if (n_req >= read_cached_split()) return read_cached_seq(cache, log, n_req, keys, R, txid,
                                                              should_gc, out, status, prune,
                                                              threshold, st);
-    Read6Args a;
+    Read6Args a{};  // dense: the mask pointers stay null
     a.key_off = log->key_off;
     a.key_len = log->key_len;
     a.key_id0 = log->key_id0;

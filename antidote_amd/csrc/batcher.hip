@@ -116,11 +116,11 @@ int wait_batch(agn_batcher *B) {
     return AGN_OK;
 }
 
-// Cached mode, counter_pn with dense clocks (D <= 8): the whole batch is one
-// fused kernel (read6.hip) reading the requests from, and writing the results
-// to, the pinned block directly; its GC follows in stream order from the
-// batch's device key list.
-int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b) {
+// Cached mode, counter_pn with D <= 8 (dense clocks, or presence masks: the
+// Erlang NIF's partitions): the whole batch is one fused kernel (read6.hip)
+// reading the requests from, and writing the results to, the pinned block
+// directly; its GC follows in stream order from the batch's device key list.
+int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
     const uint64_t n = b.size();
     const uint32_t D = B->D;
     std::vector<uint64_t> keys(n);
@@ -135,17 +135,20 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b) {
         const size_t o_keys = slot(n * 8), o_R = slot(n * D * 8), o_txid = slot(n * 8),
                      o_gc = slot(n), o_val = slot(n * 8), o_hole = slot(n * 8),
                      o_ct = slot(n * D * 8), o_cnt = slot(n * 4), o_flg = slot(n * 4),
-                     o_epos = slot(n * 4), o_st = slot(n), o_pr = slot(n);
+                     o_epos = slot(n * 4), o_st = slot(n), o_pr = slot(n),
+                     o_Rm = slot(sparse ? n * 8 : 0), o_ctm = slot(sparse ? n * 8 : 0);
         d_keys = 0;
         d_pr = al(n * 8);
         rc = grow(B, std::max(off, d_pr + n));
         if (rc) return rc;
         char *h = B->hbuf;
         bool any_tx = false;
+        const uint64_t full = (1ull << D) - 1ull;
         for (uint64_t i = 0; i < n; ++i) {
             const agn_key_read *r = b[i]->rd;
             ((uint64_t *)(h + o_keys))[i] = r->key;
             std::memcpy(h + o_R + i * D * 8, r->R, D * 8);
+            if (sparse) ((uint64_t *)(h + o_Rm))[i] = r->R_mask ? r->R_mask[0] : full;
             ((uint64_t *)(h + o_txid))[i] = r->txid;
             any_tx = any_tx || r->txid;
             ((uint8_t *)(h + o_gc))[i] = (r->flags & AGN_READ_GC) ? 1 : 0;
@@ -182,6 +185,13 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b) {
         a.dkeys = (uint64_t *)(B->dbuf + d_keys);
         a.dprune = (uint8_t *)(B->dbuf + d_pr);
         a.thr = B->thr;
+        if (sparse) {
+            a.key_mask = view.key_mask;
+            a.oc_mask = view.oc_mask;
+            a.R_mask = (const uint64_t *)(x + o_Rm);
+            a.lastct_mask = (uint64_t *)(x + o_ctm);
+            a.thrm = B->thrm;
+        }
         rc = launch_read6(B->ss, a, B->stream);
         if (rc) return rc;
         rc = wait_batch(B);
@@ -195,7 +205,7 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b) {
             std::memcpy(o->lastct, h + o_ct + i * D * 8, D * 8);
             if (o->lastct_mask) {
                 std::memset(o->lastct_mask, 0, B->W * 8);
-                for (uint32_t d = 0; d < D; ++d) o->lastct_mask[d >> 6] |= 1ull << (d & 63);
+                o->lastct_mask[0] = sparse ? ((const uint64_t *)(h + o_ctm))[i] : full;
             }
             o->count = ((const uint32_t *)(h + o_cnt))[i];
             o->flags = ((const uint32_t *)(h + o_flg))[i];
@@ -391,7 +401,7 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
     if (B->crdt != AGN_COUNTER_PN) return run_batch_cached_tags(B, b);
     bool sparse = B->sparse_log != 0;
     for (Pending *p : b) sparse = sparse || p->rd->R_mask;
-    if (!sparse && D <= 8 && B->read6) return run_batch_read6(B, b);
+    if (D <= 8 && B->read6) return run_batch_read6(B, b, sparse);
     std::vector<uint64_t> keys(n);
     for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
     int rc;

@@ -1,6 +1,6 @@
 // read6.hip — materializer_vnode:read/6 for a batch of distinct keys in ONE
-// kernel (the cached read batcher's path for counter_pn, dense clocks,
-// D <= 8).  One wave per request, the key's cache slots in registers:
+// kernel (the cached read batcher's path for counter_pn, D <= 8, dense clocks
+// or presence-masked ones as the Erlang NIF's partitions carry).  One wave per request, the key's cache slots in registers:
 //   1. get_from_snapshot_cache (src/materializer_vnode.erl:384-413,
 //      vector_orddict:get_smaller src/vector_orddict.erl:74-87): a ballot of
 //      "slot > R" folded per slot on the scalar unit, SCT and the base value
@@ -44,8 +44,15 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <int D>
+// MSK: presence masks (the logs the Erlang NIF builds, one word per clock for
+// D <= 8).  The lookup and the store's le / min follow vectorclock on dicts
+// (a DC missing from a clock reads 0; cache_dev.hpp grp_le / ss_store_one);
+// the scan routes the key as k_counter_key's MSK instantiations do: a key
+// whose entries share one DC set U inside R's runs the dense scan with R and
+// SCT neutralised (+inf) outside U, a mixed key the per-entry-mask scan.
+template <int D, bool MSK>
 __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
+    constexpr uint64_t FULL = (1ull << D) - 1ull;
     constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
     constexpr int V = DCP;                                          // op slots per lane
     constexpr int SPR = AGN_WAVE / DCP;                             // cache slots per register
@@ -61,6 +68,14 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     uint64_t r[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) r[j] = uniform_u64(a.R[i * D + j]);
+    // MSK: the key's DC set and R's, with the metadata (unconditional, from a
+    // dummy word when absent: a conditional scalar load waits on its own)
+    uint64_t kmw = 0, rmw = 0;
+    if constexpr (MSK) {
+        kmw = uniform_u64(*(a.key_mask ? a.key_mask + key : a.R));
+        rmw = uniform_u64(*(a.R_mask ? a.R_mask + i : a.R));
+    }
+    const uint64_t Rm = (MSK && a.R_mask) ? (rmw & FULL) : FULL;
     const KeyMeta km = key_meta(key, a.key_off, a.key_len, a.key_id0);
     const uint64_t off = km.off, n = km.n;
     // erlang:error(corrupted_ops_cache) (:190-191), read before any store
@@ -79,6 +94,13 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         const uint32_t j = (uint32_t)(jl + q * SPR);
         clk[q] = c.clock[(key * S + (j < nv ? j : 0u)) * D + (uint64_t)dc];
     }
+    // MSK: each slot's DC set (one word per slot; the slot's lanes share it)
+    uint64_t cmk[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        const uint32_t j = (uint32_t)(jl + q * SPR);
+        cmk[q] = (MSK && c.clock_mask) ? (c.clock_mask[key * S + (j < nv ? j : 0u)] & FULL) : FULL;
+    }
     const uint32_t ls = (uint32_t)lane < nv ? (uint32_t)lane : 0u;
     int64_t lop = c.last_op[key * S + ls], val = c.value[key * S + ls];
     // D = 8: the log's first chunk is in flight with the slots.  Unconditional
@@ -96,12 +118,14 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     uint64_t rd = r[0];
 #pragma unroll
     for (int j = 1; j < D; ++j) rd = dl == j ? r[j] : rd;
+    if (MSK && !((Rm >> dl) & 1ull)) rd = 0ull;  // a DC missing from R reads 0
     uint32_t st, is_first;
     bool sct_ign;
     int64_t base = 0;
     uint64_t s[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) s[j] = 0ull;
+    uint64_t smw = FULL;  // SCT's DC set (the hit slot's)
     uint32_t n1 = nv;  // the key's entries after the lookup
     if (n0 == 0) {     // absent: store the empty snapshot at vectorclock:new() (:395-402)
         if (lane < D) c.clock[(key * S) * D + (uint64_t)lane] = 0ull;
@@ -109,8 +133,11 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             c.last_op[key * S] = 0;
             c.value[key * S] = 0;
             c.n[key] = 1;
+            if (MSK && c.clock_mask) c.clock_mask[key * S] = 0ull;
         }
         clk[0] = jl == 0 ? 0ull : clk[0];
+        if (MSK && c.clock_mask) cmk[0] = jl == 0 ? 0ull : cmk[0];
+        smw = 0ull;
         lop = lane == 0 ? 0 : lop;
         val = lane == 0 ? 0 : val;
         n1 = 1;
@@ -121,7 +148,8 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         uint64_t ok = 0;  // bit j: slot j <= R
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
-            const uint64_t gt = group_any<DCP>(ballot(dl < D && clk[q] > rd));
+            const bool pres = !MSK || ((cmk[q] >> dl) & 1ull) != 0ull;
+            const uint64_t gt = group_any<DCP>(ballot(dl < D && pres && clk[q] > rd));
             ok |= (~gt & low_bits(SPR)) << (q * SPR);
         }
         ok &= low_bits(nv);
@@ -134,6 +162,11 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
                 s[j] = v;
             }
             base = (int64_t)readlane_u64((uint64_t)val, f);
+            if constexpr (MSK) {
+                uint64_t mw = readlane_u64(cmk[0], l0);
+                if constexpr (NR > 1) mw = q ? readlane_u64(cmk[1], l0) : mw;
+                smw = mw;
+            }
             st = AGN_SS_HIT;
             is_first = f == 0;
             sct_ign = false;
@@ -159,24 +192,56 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             if (a.dprune) a.dprune[i] = 0;
         }
         if (lane < D) a.lastct[i * D + (uint64_t)lane] = 0ull;
+        if (MSK && a.lastct_mask && lane == 0) a.lastct_mask[i] = 0ull;
         return;
     }
+    // MSK: U, the DC set every entry of the key carries (0 = they differ), and
+    // whether the dense scan serves the key exactly (no ops, or U inside R's)
+    uint64_t U = FULL, Sm = FULL;
+    bool uni = true;
+    if constexpr (MSK) {
+        U = a.oc_mask ? (a.key_mask ? (kmw & FULL) : 0ull) : FULL;
+        Sm = smw & FULL;
+        uni = n == 0 || (U != 0ull && (U & ~Rm) == 0ull);
+    }
+    // e = SCT as a dict read (missing DC = 0), where LastOpCt starts
+    // (materialize/4 :94-95); rc / sc = the compare values: +inf outside U on
+    // the dense scan of a masked key
+    uint64_t e[D], rc[D], sc[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) ct[j] = s[j];  // LastOpCt starts as SCT (materialize/4 :94-95)
+    for (int j = 0; j < D; ++j) {
+        const bool inU = ((U >> j) & 1ull) != 0ull;
+        e[j] = (sct_ign || !((Sm >> j) & 1ull)) ? 0ull : s[j];
+        sc[j] = (MSK && uni && !inU) ? ~0ull : e[j];
+        rc[j] = (MSK && uni && !inU) ? ~0ull : r[j];
+        ct[j] = e[j];
+    }
     const uint64_t txr = a.txid ? uniform_u64(a.txid[i]) : 0ull;
     const uint64_t *tx = (txr != 0ull) ? a.log_txid : nullptr;
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
+    uint64_t um = 0;            // MSK, mixed key: DCs of the included ops (per lane)
     uint64_t ctA = 0, ctB = 0;  // D = 8: quad rows, LastOpCt of DCs 2p, 2p+1 (p = lane & 3)
     if constexpr (D == 8) {
         const int p = lane & 3;
-        const uint64_t rA = p == 0 ? r[0] : p == 1 ? r[2 % D] : p == 2 ? r[4 % D] : r[6 % D];
-        const uint64_t rB = p == 0 ? r[1 % D] : p == 1 ? r[3 % D] : p == 2 ? r[5 % D] : r[7 % D];
-        const uint64_t sA = p == 0 ? s[0] : p == 1 ? s[2 % D] : p == 2 ? s[4 % D] : s[6 % D];
-        const uint64_t sB = p == 0 ? s[1 % D] : p == 1 ? s[3 % D] : p == 2 ? s[5 % D] : s[7 % D];
-        ctA = sA;
-        ctB = sB;
-        if (n != 0) {
+        const uint64_t rA = p == 0 ? rc[0] : p == 1 ? rc[2 % D] : p == 2 ? rc[4 % D] : rc[6 % D];
+        const uint64_t rB = p == 0 ? rc[1 % D] : p == 1 ? rc[3 % D] : p == 2 ? rc[5 % D] : rc[7 % D];
+        const uint64_t sA = p == 0 ? sc[0] : p == 1 ? sc[2 % D] : p == 2 ? sc[4 % D] : sc[6 % D];
+        const uint64_t sB = p == 0 ? sc[1 % D] : p == 1 ? sc[3 % D] : p == 2 ? sc[5 % D] : sc[7 % D];
+        const uint64_t eA = p == 0 ? e[0] : p == 1 ? e[2 % D] : p == 2 ? e[4 % D] : e[6 % D];
+        const uint64_t eB = p == 0 ? e[1 % D] : p == 1 ? e[3 % D] : p == 2 ? e[5 % D] : e[7 % D];
+        ctA = eA;
+        ctB = eB;
+        if (n != 0 && MSK && !uni) {
+            // a mixed key: the quad rows with each op's mask word (chunk 0
+            // is read again with its masks)
+            if (sct_ign)
+                scan_key_q8_msk<false>(a.oc, a.oc_mask, a.eff, tx, txr, off, n, a.n_entries, rA, rB,
+                                       sA, sB, Rm, ctA, ctB, um, sum, cnt, first_excl, first_err);
+            else
+                scan_key_q8_msk<true>(a.oc, a.oc_mask, a.eff, tx, txr, off, n, a.n_entries, rA, rB,
+                                      sA, sB, Rm, ctA, ctB, um, sum, cnt, first_excl, first_err);
+        } else if (n != 0) {
 #define AGN_R6Q(W)                                                                             \
     q8_fold<W>(ch0, tx, txr, off, 0, n, a.n_entries, rA, rB, sA, sB, ctA, ctB, sum, cnt,       \
                first_excl, first_err);                                                         \
@@ -188,11 +253,31 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
                 AGN_R6Q(true);
             }
 #undef AGN_R6Q
+            if (MSK) {  // outside U: SCT's value (an op's row there is not in its dict)
+                ctA = ((U >> (2 * p)) & 1ull) ? ctA : eA;
+                ctB = ((U >> (2 * p + 1)) & 1ull) ? ctB : eB;
+            }
         }
-    } else if (sct_ign) {
-        scan_key<D, false>(a.oc, a.eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl, first_err);
     } else {
-        scan_key<D, true>(a.oc, a.eff, tx, txr, off, n, r, s, ct, sum, cnt, first_excl, first_err);
+        if (MSK && !uni) {
+            if (sct_ign)
+                scan_key_msk<D, false>(a.oc, a.oc_mask, a.eff, tx, txr, off, n, rc, sc, Rm, ct, um,
+                                       sum, cnt, first_excl, first_err);
+            else
+                scan_key_msk<D, true>(a.oc, a.oc_mask, a.eff, tx, txr, off, n, rc, sc, Rm, ct, um,
+                                      sum, cnt, first_excl, first_err);
+        } else {
+            if (sct_ign)
+                scan_key<D, false>(a.oc, a.eff, tx, txr, off, n, rc, sc, ct, sum, cnt, first_excl,
+                                   first_err);
+            else
+                scan_key<D, true>(a.oc, a.eff, tx, txr, off, n, rc, sc, ct, sum, cnt, first_excl,
+                                  first_err);
+            if (MSK) {
+#pragma unroll
+                for (int j = 0; j < D; ++j) ct[j] = ((U >> j) & 1ull) ? ct[j] : e[j];
+            }
+        }
     }
     int64_t hid;
     {
@@ -237,6 +322,13 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         ctl = ct_ign ? 0ull : m;
         if (jl == 0 && dl < D) a.lastct[i * D + (uint64_t)dl] = ctl;
     }
+    // LastOpCt's DC set: SCT's united with the included ops' (U, or the
+    // per-lane sets of a mixed key)
+    uint64_t mo = FULL;
+    if constexpr (MSK) {
+        const uint64_t un = uni ? (cnt ? U : 0ull) : wave_or_bits<D>(um);
+        mo = ct_ign ? 0ull : ((sct_ign ? 0ull : Sm) | un);
+    }
     // NewLastOp = id(oldest excluded) - 1, else get_first_id (:49-63)
     const int64_t hole = first_excl >= 0 ? hid - 1 : hid;
     uint32_t fl = 0;
@@ -253,21 +345,27 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     const int64_t lop0 = (int64_t)readlane_u64((uint64_t)lop, 0);
     if (st != AGN_SS_LOG && n != 0 && !(fl & (AGN_F_ERR_UNEXPECTED | AGN_F_CT_IGNORE)) &&
         (refresh || gc) && (hole - lop0 >= AGN_MIN_OP_STORE_SS || gc)) {
-        // insert_bigger: prepend iff not le(LastOpCt, head clock)
-        const bool prepend = (ballot(jl == 0 && dl < D && ctl > clk[0]) & low_bits(DCP)) != 0ull;
+        // insert_bigger: prepend iff not le(LastOpCt, head clock) (dicts: DCs
+        // of LastOpCt only, the head's missing ones read 0)
+        const bool inct = !MSK || ((mo >> dl) & 1ull) != 0ull;
+        const uint64_t hv = (!MSK || ((cmk[0] >> dl) & 1ull)) ? clk[0] : 0ull;
+        const bool prepend = (ballot(jl == 0 && dl < D && inct && ctl > hv) & low_bits(DCP)) != 0ull;
         const uint32_t size1 = n1 + (prepend ? 1u : 0u);
         const bool collect = size1 >= AGN_SNAPSHOT_THRESHOLD || gc;
         uint32_t kept = n1;
         if (collect) kept = prepend ? (n1 < AGN_SNAPSHOT_MIN - 1 ? n1 : AGN_SNAPSHOT_MIN - 1)
                                     : (n1 < AGN_SNAPSHOT_MIN ? n1 : AGN_SNAPSHOT_MIN);
         const uint32_t new_n = kept + (prepend ? 1u : 0u);
-        uint64_t m = ~0ull;
+        uint64_t m = ~0ull, pm = 0ull;  // CommitTime: min (missing = 0), its DC set
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
             const uint32_t j = (uint32_t)(jl + q * SPR);
             if (j < kept) {
                 if (prepend && dl < D) c.clock[(key * S + j + 1) * D + (uint64_t)dl] = clk[q];
-                m = clk[q] < m ? clk[q] : m;
+                if (MSK && c.clock_mask && prepend && dl == 0) c.clock_mask[key * S + j + 1] = cmk[q];
+                const uint64_t v = (!MSK || ((cmk[q] >> dl) & 1ull)) ? clk[q] : 0ull;
+                m = v < m ? v : m;
+                pm |= cmk[q];
             }
         }
         if (prepend) {
@@ -279,16 +377,23 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             if (lane == 0) {
                 c.last_op[key * S] = hole;
                 c.value[key * S] = value;
+                if (MSK && c.clock_mask) c.clock_mask[key * S] = mo;
             }
-            m = ctl < m ? ctl : m;
+            const uint64_t v = inct ? ctl : 0ull;
+            m = v < m ? v : m;
+            pm |= mo;
         }
         if (collect) {  // CommitTime = vectorclock:min of the kept clocks (:523-527)
 #pragma unroll
             for (int x = DCP; x < AGN_WAVE; x <<= 1) {
                 const uint64_t o = shfl_xor_u64(m, x);
                 m = o < m ? o : m;
+                if (MSK) pm |= shfl_xor_u64(pm, x);
             }
+            // a DC no kept clock has: 0 (and absent from the threshold's set)
+            if (MSK && !((pm >> dl) & 1ull)) m = 0ull;
             if (jl == 0 && dl < D) a.thr[key * D + (uint64_t)dl] = m;
+            if (MSK && a.thrm && lane == 0) a.thrm[key] = pm & FULL;
         }
         if (lane == 0) c.n[key] = new_n;
         pr = collect;
@@ -301,6 +406,7 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         a.err_pos[i] = first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
         a.status[i] = (uint8_t)st;
         a.prune[i] = pr ? 1 : 0;
+        if (MSK && a.lastct_mask) a.lastct_mask[i] = mo;
         if (a.dkeys) a.dkeys[i] = key;
         if (a.dprune) a.dprune[i] = pr ? 1 : 0;
     }
@@ -316,17 +422,23 @@ int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     if (a.n_req == 0) return AGN_OK;
     if (a.n_req > 0x7fffffffull) return fail(AGN_ENOTSUP, "read6: batch too large");
     const dim3 grid((unsigned)a.n_req), block(AGN_WAVE);
+    const bool msk = a.oc_mask || a.R_mask || c.clock_mask;
+#define AGN_R6(DV)                                                                             \
+    if (msk) hipLaunchKernelGGL((k_read6<DV, true>), grid, block, 0, st, c, a);                \
+    else hipLaunchKernelGGL((k_read6<DV, false>), grid, block, 0, st, c, a);                   \
+    break
     switch (a.n_dcs) {
-        case 1: hipLaunchKernelGGL((k_read6<1>), grid, block, 0, st, c, a); break;
-        case 2: hipLaunchKernelGGL((k_read6<2>), grid, block, 0, st, c, a); break;
-        case 3: hipLaunchKernelGGL((k_read6<3>), grid, block, 0, st, c, a); break;
-        case 4: hipLaunchKernelGGL((k_read6<4>), grid, block, 0, st, c, a); break;
-        case 5: hipLaunchKernelGGL((k_read6<5>), grid, block, 0, st, c, a); break;
-        case 6: hipLaunchKernelGGL((k_read6<6>), grid, block, 0, st, c, a); break;
-        case 7: hipLaunchKernelGGL((k_read6<7>), grid, block, 0, st, c, a); break;
-        case 8: hipLaunchKernelGGL((k_read6<8>), grid, block, 0, st, c, a); break;
+        case 1: AGN_R6(1);
+        case 2: AGN_R6(2);
+        case 3: AGN_R6(3);
+        case 4: AGN_R6(4);
+        case 5: AGN_R6(5);
+        case 6: AGN_R6(6);
+        case 7: AGN_R6(7);
+        case 8: AGN_R6(8);
         default: return fail(AGN_ENOTSUP, "read6: n_dcs=%u", a.n_dcs);
     }
+#undef AGN_R6
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }

@@ -68,7 +68,14 @@ struct Read6Args {
     uint64_t *dkeys;
     uint8_t *dprune;
     uint64_t *thr;
+    // presence masks (D <= 8: one word per clock; all null = dense): the
+    // log's key_mask / oc_mask, the requests' R_mask, and the results'
+    // LastOpCt mask and the GC thresholds' [K] masks (with a cache that
+    // carries clock_mask)
+    const uint64_t *key_mask, *oc_mask, *R_mask;
+    uint64_t *lastct_mask, *thrm;
 };
+// agn_read_cached's fused path: dense logs (its cache has no clock masks)
 bool read6_supported(const agn_log &view, uint32_t D);
 int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st);
 
