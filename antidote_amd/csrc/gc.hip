@@ -666,8 +666,8 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : 1) void k_prune_inplace(Inp
 // verdicts are nibbles of wave ballots folded on the scalar unit; a moving
 // row is written back from the same registers (its parts' lanes fetch its
 // destination).  On a prefix drop nothing moves and the GC is a read pass.
-template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS>
-__global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB) void k_prune_tail(InplaceArgs a,
                                                    const uint8_t *__restrict__ prune,
                                                    const uint64_t *__restrict__ thr,
                                                    const uint64_t *__restrict__ thr_mask,
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(64) void k_prune_tail(InplaceArgs a,
     constexpr int OPI = S::OPI;
     constexpr bool QUAD = FULL && DPL == 8 && LPO == 1 && !SPARSE;
     const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t i = blk;
+    const uint64_t i = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
     if (i >= a.n_keys) return;
     const uint64_t K = a.n_keys;  // launch size (meta stride)
     const uint64_t k = a.key_list ? uniform_u64(a.key_list[i]) : i;
@@ -968,9 +968,18 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     const bool full = !a.mask && (DPL % 2 == 0) && a.D == (uint32_t)(DPL * LPO);
     const bool tags = a.rem_off != nullptr;
     if (a.d_key_off && a.meta6) {  // the engine-owned log: toward the end of the live range
+        // waves per block: 1 (default) or 4 (AGN_PRUNE_WPB=4, A/B knob)
 #define AGN_T(FULLV, TAGSV)                                                                    \
-    hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV>), dim3(grid_for(a.n_keys, 1, 0x7fffffffu)), \
-                       dim3(64), 0, st, a, prune, thr, thr_mask, meta, flags)
+    do {                                                                                       \
+        if (w4)                                                                                \
+            hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV, 4>),               \
+                               dim3(grid_for(a.n_keys, 4, 0x7fffffffu)), dim3(256), 0, st, a,  \
+                               prune, thr, thr_mask, meta, flags);                             \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV, 1>),               \
+                               dim3(grid_for(a.n_keys, 1, 0x7fffffffu)), dim3(64), 0, st, a,   \
+                               prune, thr, thr_mask, meta, flags);                             \
+    } while (0)
         if (full) {
             if (tags) AGN_T((DPL % 2 == 0), true);
             else AGN_T((DPL % 2 == 0), false);
