@@ -329,8 +329,8 @@ constexpr int PT = 4;  // removal tokens a lane buffers per entry
 // rows, k_tags).  Verdicts are group-any folds of wave ballots; a kept row is
 // stored from the same registers (its parts' lanes fetch its destination).
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB, bool CTL = false,
-          int PF = 0>
-__global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : 1) void k_prune_inplace(InplaceArgs a,
+          int PF = 0, int MINW = 1>
+__global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(InplaceArgs a,
                                                        const uint8_t *__restrict__ prune,
                                                        const uint64_t *__restrict__ thr,
                                                        const uint64_t *__restrict__ thr_mask,
@@ -666,8 +666,11 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : 1) void k_prune_inplace(Inp
 // verdicts are nibbles of wave ballots folded on the scalar unit; a moving
 // row is written back from the same registers (its parts' lanes fetch its
 // destination).  On a prefix drop nothing moves and the GC is a read pass.
-template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB = 1>
-__global__ __launch_bounds__(64 * WPB) void k_prune_tail(InplaceArgs a,
+// MINW: waves per SIMD the register allocation must allow (1 = the
+// compiler's choice; 8: the counter form fits 8 waves in 59 VGPRs / 78 SGPRs
+// where the default allocation takes 104 SGPRs and 7 waves)
+template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB = 1, int MINW = 1>
+__global__ __launch_bounds__(64 * WPB, MINW) void k_prune_tail(InplaceArgs a,
                                                    const uint8_t *__restrict__ prune,
                                                    const uint64_t *__restrict__ thr,
                                                    const uint64_t *__restrict__ thr_mask,
@@ -967,13 +970,22 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     const unsigned blocks = grid_for(a.n_keys, w4 ? 4 : 1, 0x7fffffffu);
     const bool full = !a.mask && (DPL % 2 == 0) && a.D == (uint32_t)(DPL * LPO);
     const bool tags = a.rem_off != nullptr;
+    // the register budget of MINW waves per SIMD instead of the compiler's
+    // choice: AGN_PRUNE_MINW=6|8 (A/B knob; the tail kernel: 8, counter only)
+    const char *mw = getenv("AGN_PRUNE_MINW");
+    const bool mw6 = mw && mw[0] == '6', mw8 = mw && mw[0] == '8';
     if (a.d_key_off && a.meta6) {  // the engine-owned log: toward the end of the live range
         // waves per block: 1 (default) or 4 (AGN_PRUNE_WPB=4, A/B knob)
+        const bool w8 = mw8;
 #define AGN_T(FULLV, TAGSV)                                                                    \
     do {                                                                                       \
         if (w4)                                                                                \
             hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV, 4>),               \
                                dim3(grid_for(a.n_keys, 4, 0x7fffffffu)), dim3(256), 0, st, a,  \
+                               prune, thr, thr_mask, meta, flags);                             \
+        else if (w8 && !(TAGSV))                                                               \
+            hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV, 1, 8>),            \
+                               dim3(grid_for(a.n_keys, 1, 0x7fffffffu)), dim3(64), 0, st, a,   \
                                prune, thr, thr_mask, meta, flags);                             \
         else                                                                                   \
             hipLaunchKernelGGL((k_prune_tail<DPL, LPO, SPARSE, FULLV, TAGSV, 1>),               \
@@ -995,6 +1007,14 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         if (w4)                                                                                \
             hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 4>),           \
                                dim3(blocks), dim3(256), 0, st, a, prune, thr, thr_mask, meta,  \
+                               flags);                                                         \
+        else if (mw6)                                                                          \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1, false, 0, 6>), \
+                               dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
+                               flags);                                                         \
+        else if (mw8)                                                                          \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1, false, 0, 8>), \
+                               dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
                                flags);                                                         \
         else                                                                                   \
             hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1>),           \

@@ -201,14 +201,15 @@ def test_oplog_append_materialize(eng, oracle_lib, crdt, D, sparse, init):
         assert not materialize_view(eng, oracle_lib, view, log2, req, sparse)
 
 
-@pytest.fixture(params=["tail", "tail4", "front"])
+@pytest.fixture(params=["tail", "tail4", "tail8", "front"])
 def anchor(request, monkeypatch):
     """The engine-owned log's prune kernel: k_prune_tail (kept entries compacted
     toward the end of the live range, the default; "tail4": four waves per
-    block, AGN_PRUNE_WPB=4) or the start-anchored k_prune_inplace
+    block, AGN_PRUNE_WPB=4; "tail8": 8 waves per SIMD, AGN_PRUNE_MINW=8) or the start-anchored k_prune_inplace
     (AGN_PRUNE_TAIL=0)."""
     monkeypatch.setenv("AGN_PRUNE_TAIL", "0" if request.param == "front" else "1")
     monkeypatch.setenv("AGN_PRUNE_WPB", "4" if request.param == "tail4" else "1")
+    monkeypatch.setenv("AGN_PRUNE_MINW", "8" if request.param == "tail8" else "1")
     return "front" if request.param == "front" else "tail"
 
 
