@@ -975,8 +975,13 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     const char *mw = getenv("AGN_PRUNE_MINW");
     const bool mw6 = mw && mw[0] == '6', mw8 = mw && mw[0] == '8';
     if (a.d_key_off && a.meta6) {  // the engine-owned log: toward the end of the live range
-        // waves per block: 1 (default) or 4 (AGN_PRUNE_WPB=4, A/B knob)
-        const bool w8 = mw8;
+        // waves per block: 1 (default) or 4 (AGN_PRUNE_WPB=4, A/B knob).  The
+        // counter forms run with the register budget of 8 waves per SIMD
+        // (prefix drop, 2M x 64: 2.43 vs 2.53 ms for the GC call, 4 waves
+        // per block 2.93; profiles/r03/ab_prune_tail.log); AGN_PRUNE_TAIL_MINW=1
+        // gives the compiler's allocation (7 waves)
+        const char *tmw = getenv("AGN_PRUNE_TAIL_MINW");
+        const bool w8 = !(tmw && tmw[0] == '1');
 #define AGN_T(FULLV, TAGSV)                                                                    \
     do {                                                                                       \
         if (w4)                                                                                \
@@ -1021,10 +1026,14 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
                                dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
                                flags);                                                         \
     } while (0)
-    // contiguous rows (CTL) for dense 8-DC slices: AGN_PRUNE_CT=1 (A/B knob)
+    // contiguous rows (CTL) for dense 8-DC slices: the default for counter_pn
+    // (cfg2: 15.37-15.70 vs 15.60-15.97 ms, three boxes), not for set/register
+    // (cfg3: 13.79 vs 13.26; profiles/r03/*_abp{2,3}.log); AGN_PRUNE_CT=0|1
+    // (A/B knob) overrides
     if constexpr (DPL == 8 && !SPARSE) {
         const char *cv = getenv("AGN_PRUNE_CT");
-        if (full && cv && cv[0] == '1') {
+        const bool ct = (cv && (cv[0] == '0' || cv[0] == '1')) ? cv[0] == '1' : !tags;
+        if (full && ct && !w4) {
             if (tags)
                 hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, false, true, true, 1, true>),
                                    dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,
@@ -1037,9 +1046,13 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         }
     }
     // next iteration's rows prefetched (PF) for keys that span iterations:
-    // AGN_PRUNE_PF=0|1|2 (A/B knob; 2: held to 5 waves per SIMD)
+    // the default for set/register (cfg3: 13.13 vs 13.26 and 13.82 vs 13.97
+    // ms on two boxes), AGN_PRUNE_PF=0|1|2 (A/B knob; 2: held to 5 waves per
+    // SIMD, slower: 14.5)
     const char *pv = getenv("AGN_PRUNE_PF");
-    const int pf = (!w4 && pv && (pv[0] == '1' || pv[0] == '2')) ? pv[0] - '0' : 0;
+    const int pf = w4 || mw6 || mw8 ? 0
+                   : (pv && (pv[0] == '0' || pv[0] == '1' || pv[0] == '2')) ? pv[0] - '0'
+                   : (tags ? 1 : 0);
     if (pf) {
 #define AGN_P(FULLV, TAGSV)                                                                    \
     do {                                                                                       \

@@ -2,8 +2,9 @@
 on the prefix-drop workload of scripts/bench_oplog_prune.py (K keys x N ops,
 D = 8, threshold = the clock of a random position), variants alternated in
 one process on fresh logs (HBM rates move several % between processes):
-  AGN_PRUNE_WPB = 1 | 4 (waves per block), AGN_PRUNE_MINW = 8 (the register
-  budget of 8 waves per SIMD instead of the compiler's 7).
+  AGN_PRUNE_WPB = 1 | 4 (waves per block), AGN_PRUNE_TAIL_MINW = 1 | 8 (the
+  compiler's register allocation, 7 waves per SIMD, or the budget of 8: the
+  default since round 3).
 Times the prune call's GPU span (events on the log's stream: the kernel plus
 the records' copy) and checks that both variants leave identical logs.
 
@@ -40,9 +41,9 @@ def main():
     eng = Engine(0)
     bp, bt = eng.upload(prune), eng.upload(thr)
     fl = eng.empty(4 * K)
-    variants = [("wpb1", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_MINW": "1"}),
-                ("wpb4", {"AGN_PRUNE_WPB": "4", "AGN_PRUNE_MINW": "1"}),
-                ("minw8", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_MINW": "8"})]
+    variants = [("wpb1", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_MINW": "1"}),
+                ("wpb4", {"AGN_PRUNE_WPB": "4", "AGN_PRUNE_TAIL_MINW": "1"}),
+                ("minw8", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_MINW": "8"})]
     ms = {v: [] for v, _ in variants}
     sig = {}
     for r in range(rounds + 1):
