@@ -416,6 +416,15 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
     if constexpr (PF != 0) {
         if (n) load_slice(off + ((uint64_t)slot < n ? (uint64_t)slot : 0ull), on, onb);
     }
+    // EF (PF = 3, set/register): when an iteration keeps every entry, the
+    // next one most likely does too (a GC threshold covers a prefix of the
+    // key's commit-ordered ops), so its entries' fields are requested with
+    // its rows instead of after its filter -- one round trip less per kept
+    // iteration; a misprediction only reads the fields of dropped entries
+    constexpr bool EF = PF == 3 && TAGS;
+    bool nf = false;
+    uint32_t nid = 0, ntg = 0, nr0 = 0, nr1 = 0;
+    uint64_t ntx = 0, nad = 0;
     for (uint64_t b = 0; b < n; b += S::OPI) {
         const uint64_t pos = b + (uint64_t)slot;
         const bool valid = pos < n;
@@ -465,7 +474,19 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             }
         };
         const bool late = a.late_fields < 0 ? TAGS : a.late_fields != 0;
-        if (!late && valid && sub == 0) load_fields();
+        bool have = false;  // EF: this iteration's fields came with its rows
+        if constexpr (EF) {
+            if (nf) {
+                id = nid;
+                tx = ntx;
+                tg = ntg;
+                ad = nad;
+                r0 = nr0;
+                rl_ = nr1 - nr0;
+                have = true;
+            }
+        }
+        if (!late && !have && valid && sub == 0) load_fields();
         bool le = true;
         if constexpr (CTL) {
             uint64_t gtm = 0;  // ops with a DC above the threshold
@@ -486,10 +507,26 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
         // set_aw / register_mv: 32 B of fields per entry, loaded for the kept
         // entries only once the filter has decided; counter_pn: 20 B, loaded
         // with the row (one round trip less; measured, scripts/ab_prune.py)
-        if (late && kp && sub == 0) load_fields();
+        if (late && !have && kp && sub == 0) load_fields();
         if constexpr (PF != 0) {
             const uint64_t pn = b + (uint64_t)S::OPI + (uint64_t)slot;
-            if (b + (uint64_t)S::OPI < n) load_slice(off + (pn < n ? pn : 0ull), on, onb);
+            const bool more = b + (uint64_t)S::OPI < n;
+            if (more) load_slice(off + (pn < n ? pn : 0ull), on, onb);
+            if constexpr (EF) {
+                // the next iteration's fields read their source slots, above
+                // every destination of this iteration (the one rem_off slot
+                // it may rewrite there gets the same value)
+                nf = more && ballot(valid && sub == 0 && !kp) == 0ull;
+                if (nf && pn < n && sub == 0) {
+                    const uint64_t en = off + pn;
+                    nid = a.op_id[en];
+                    ntx = a.txid ? a.txid[en] : 0ull;
+                    ntg = a.tag[en];
+                    nad = a.add[en];
+                    nr0 = a.rem_off[en];
+                    nr1 = a.rem_off[en + 1];
+                }
+            }
         }
         const uint64_t km = ballot(kp && sub == 0);  // one bit per kept op (its sub-0 lane)
         const uint32_t nk = (uint32_t)__builtin_popcountll(km);
@@ -1047,16 +1084,21 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     }
     // next iteration's rows prefetched (PF) for keys that span iterations:
     // the default for set/register (cfg3: 13.13 vs 13.26 and 13.82 vs 13.97
-    // ms on two boxes), AGN_PRUNE_PF=0|1|2 (A/B knob; 2: held to 5 waves per
+    // ms on two boxes), AGN_PRUNE_PF=0|1|2|3 (A/B knob; 3: with the next
+    // iteration's fields predicted (EF); 2: held to 5 waves per
     // SIMD, slower: 14.5)
     const char *pv = getenv("AGN_PRUNE_PF");
     const int pf = w4 || mw6 || mw8 ? 0
-                   : (pv && (pv[0] == '0' || pv[0] == '1' || pv[0] == '2')) ? pv[0] - '0'
+                   : (pv && pv[0] >= '0' && pv[0] <= '3') ? pv[0] - '0'
                    : (tags ? 1 : 0);
     if (pf) {
 #define AGN_P(FULLV, TAGSV)                                                                    \
     do {                                                                                       \
-        if (pf == 2)                                                                           \
+        if (pf == 3)                                                                           \
+            hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1, false, 3>), \
+                               dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
+                               flags);                                                         \
+        else if (pf == 2)                                                                      \
             hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, TAGSV, 1, false, 2>), \
                                dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta,   \
                                flags);                                                         \

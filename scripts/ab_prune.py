@@ -2,7 +2,8 @@
 agn_oplog_prune runs in place) on the cfg2 log, variants alternated in one
 process (process-to-process HBM variance is several %):
   round 3: row-slice loads vs contiguous rows (AGN_PRUNE_CT = 0 | 1), and
-  the next iteration's rows prefetched (AGN_PRUNE_PF = 0 | 1 | 2), the
+  the next iteration's rows prefetched (AGN_PRUNE_PF = 0 | 1 | 2; 3: and its
+  fields when the iteration before kept everything), the
   register budget of 6 / 8 waves per SIMD (AGN_PRUNE_MINW); round
   2: AGN_PRUNE_WPB = 1 | 4 (waves per block) x AGN_PRUNE_LATE_FIELDS = 0 | 1
   (entry fields with the rows, or only for kept entries after the filter).
@@ -55,6 +56,7 @@ def main():
     variants = [("rows", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "1"}),
                 ("ct", {"AGN_PRUNE_CT": "1", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "1"}),
                 ("pf4", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "1", "AGN_PRUNE_MINW": "1"}),
+                ("pf_ef", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "3", "AGN_PRUNE_MINW": "1"}),
                 ("mw6", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "6"}),
                 ("mw8", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "8"})]
     os.environ["AGN_PRUNE_WPB"] = "1"
