@@ -997,6 +997,208 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_prune_tail(InplaceArgs a,
     }
 }
 
+// k_prune_tail for counter_pn with dense 8-DC rows (the engine-owned log the
+// bench and a steady counter partition have), KPW keys per wave: every key's
+// metadata is requested in one round trip and every key's newest chunk of
+// quad rows in the next, before the first key is walked -- KPW x 4 KiB in
+// flight per wave slot where the one-key form has 4 KiB and a metadata round
+// trip in which nothing streams.  Per key the walk, the moves and the
+// records are k_prune_tail's (QUAD, !TAGS) exactly.
+struct TailKey {
+    uint64_t i, k, off, n;
+    uint32_t id0_old, lc_in;
+    bool live, gc;
+    uint64_t tA, tB;
+};
+
+template <int KPW, int MINW>
+__global__ __launch_bounds__(64, MINW) void k_prune_tail_q(InplaceArgs a,
+                                                         const uint8_t *__restrict__ prune,
+                                                         const uint64_t *__restrict__ thr,
+                                                         uint32_t *__restrict__ meta,
+                                                         uint32_t *__restrict__ flags) {
+    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t K = a.n_keys;  // launch size (meta stride)
+    const int lane = lane_id(), qp = lane & 3;
+    TailKey s[KPW];
+    // 1. every key's metadata (unconditional loads, dummies past the launch)
+    uint64_t off_r[KPW], n_r[KPW];
+    uint32_t id0_r[KPW], lc_r[KPW], pr_r[KPW];
+    u64x2 t_r[KPW];
+#pragma unroll
+    for (int x = 0; x < KPW; ++x) {
+        const uint64_t i = (uint64_t)blk * KPW + (uint64_t)x;
+        s[x].i = i;
+        s[x].live = i < K;
+        const uint64_t ic = s[x].live ? i : 0ull;
+        s[x].k = a.key_list ? uniform_u64(a.key_list[ic]) : ic;
+        const uint64_t k = s[x].k;
+        const uint32_t *dummy = reinterpret_cast<const uint32_t *>(a.key_off + k);
+        off_r[x] = a.key_off[k];
+        n_r[x] = a.key_len ? a.key_len[k] : a.key_off[k + 1];
+        id0_r[x] = *(a.key_id0 ? a.key_id0 + k : dummy);
+        lc_r[x] = *(a.key_lcap ? a.key_lcap + k : dummy);
+        pr_r[x] = a.key_list ? a.list_flags[ic] : (prune ? prune[k] : 1u);
+        t_r[x] = reinterpret_cast<const u64x2 *>(thr + k * 8u)[qp];
+    }
+    // 2. every key's newest chunk of rows
+    u64x2 top[KPW][4];
+#pragma unroll
+    for (int x = 0; x < KPW; ++x) {
+        const uint64_t off = uniform_u64(off_r[x]);
+        const uint64_t nn = uniform_u64(n_r[x]);
+        const uint64_t n = a.key_len ? nn : nn - off;
+        s[x].off = off;
+        s[x].n = n;
+        s[x].gc = s[x].live && pr_r[x] != 0u;
+        s[x].id0_old = a.key_id0 ? (uint32_t)__builtin_amdgcn_readfirstlane(id0_r[x]) : AGN_ID0_NONE;
+        s[x].lc_in = a.key_lcap ? (uint32_t)__builtin_amdgcn_readfirstlane(lc_r[x]) : 0u;
+        s[x].tA = t_r[x].x;
+        s[x].tB = t_r[x].y;
+        const uint64_t nc = (n + AGN_WAVE - 1) / AGN_WAVE;
+        const uint64_t b = nc ? (nc - 1) * (uint64_t)AGN_WAVE : 0ull;
+        // an empty key (possibly without a segment) reads its own key_off word
+        const u64x2 *rows = reinterpret_cast<const u64x2 *>(n ? a.oc : a.key_off);
+        const uint64_t lim = n ? (off + n) * 4u - 1u : 0ull;  // the key's last part
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t u = (off + b) * 4u + (uint64_t)(j * AGN_WAVE + lane);
+            u = (n && u < lim) ? u : lim;
+            top[x][j] = __builtin_nontemporal_load(rows + u);
+        }
+    }
+    // 3. each key in turn
+#pragma unroll
+    for (int x = 0; x < KPW; ++x) {
+        if (!s[x].live) continue;
+        const uint64_t i = s[x].i, k = s[x].k, off = s[x].off, n = s[x].n;
+        if (!s[x].gc) {
+            if (lane == 0) {
+                if (meta) {
+                    meta[i] = (uint32_t)n;
+                    meta[K + i] = 0u;
+                    meta[2 * K + i] = s[x].lc_in;
+                    meta[3 * K + i] = s[x].id0_old;
+                    meta[4 * K + i] = (uint32_t)off;
+                    meta[5 * K + i] = 0u;
+                }
+                if (flags) flags[k] = 0u;
+            }
+            continue;
+        }
+        const bool derive = s[x].id0_old != AGN_ID0_NONE;
+        const uint64_t tA = s[x].tA, tB = s[x].tB;
+        uint64_t written = 0;
+        uint32_t low_id = 0;
+        bool consec = true;
+        int64_t lo_pos = -1, hi_pos = -1;
+        const uint64_t nc = (n + AGN_WAVE - 1) / AGN_WAVE;
+        for (uint64_t c = nc; c-- > 0;) {
+            const uint64_t b = c * (uint64_t)AGN_WAVE;
+            const uint64_t pos = b + (uint64_t)lane;
+            const bool valid = pos < n;
+            const uint64_t e = off + (valid ? pos : 0ull);
+            u64x2 qx[4];
+            if (c == nc - 1) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) qx[j] = top[x][j];
+            } else {
+                const u64x2 *rows = reinterpret_cast<const u64x2 *>(a.oc);
+                const uint64_t lim = (off + n) * 4u - 1u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint64_t u = (off + b) * 4u + (uint64_t)(j * AGN_WAVE + lane);
+                    u = u < lim ? u : lim;
+                    qx[j] = __builtin_nontemporal_load(rows + u);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            uint64_t gtm = 0;  // ops with a DC above the threshold
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                gtm |= nib_any16(ballot(qx[j].x > tA || qx[j].y > tB)) << (16 * j);
+            const bool kp = valid && ((gtm >> lane) & 1ull);  // belongs_to_snapshot_op(Threshold, op)
+            const uint64_t km = ballot(kp);
+            const uint32_t nk = (uint32_t)__builtin_popcountll(km);
+            const uint64_t above = lane >= 63 ? 0ull : (km & (~0ull << (lane + 1)));
+            const uint64_t dst = off + n - 1ull - written - (uint64_t)__builtin_popcountll(above);
+            const bool mv = kp && dst != e;
+            uint32_t id = 0;
+            uint64_t tx = 0;
+            int64_t ef = 0;
+            if (mv) {
+                id = a.op_id[e];
+                tx = a.txid ? a.txid[e] : 0ull;
+                ef = a.eff[e];
+            } else if (!derive && kp) {
+                id = a.op_id[e];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t mvm = ballot(mv);
+            if (mvm) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int q = 16 * j + (lane >> 2);  // the op whose part this lane holds
+                    const uint64_t dq = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(dst >> 32), q, AGN_WAVE) << 32) |
+                                        (uint32_t)__shfl((int)(uint32_t)dst, q, AGN_WAVE);
+                    if ((mvm >> q) & 1ull) reinterpret_cast<u64x2 *>(a.d_oc)[dq * 4u + (uint64_t)qp] = qx[j];
+                }
+            }
+            if (mv) {
+                a.d_op_id[dst] = id;
+                if (a.d_txid) a.d_txid[dst] = tx;
+                a.d_eff[dst] = ef;
+            }
+            if (nk) {
+                if (derive) {
+                    if (hi_pos < 0) hi_pos = (int64_t)b + (63 - __builtin_clzll(km));
+                    lo_pos = (int64_t)b + __builtin_ctzll(km);
+                } else {
+                    const int nl = above ? __builtin_ctzll(above) : 0;
+                    const uint32_t nid = (uint32_t)__shfl((int)id, nl, AGN_WAVE);
+                    bool ok = true;
+                    if (kp) ok = above ? (nid == id + 1u) : (written == 0 || low_id == id + 1u);
+                    consec = consec && (ballot(kp && !ok) == 0ull);
+                    low_id = (uint32_t)__shfl((int)id, __builtin_ctzll(km), AGN_WAVE);
+                }
+            }
+            written += nk;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (lane == 0) {
+            const uint32_t l = (uint32_t)written;
+            uint32_t id0 = AGN_ID0_NONE;
+            if (l) {
+                if (derive) {
+                    if (hi_pos - lo_pos + 1 == (int64_t)l) id0 = s[x].id0_old + (uint32_t)lo_pos;
+                } else if (consec && (uint64_t)low_id + (l - 1u) < (uint64_t)AGN_ID0_NONE) {
+                    id0 = low_id;
+                }
+            }
+            uint32_t lc = s[x].lc_in;
+            if (lc) {
+                lc = resize_list_len_dev(l ? l : 1u, lc);  // prune_ops' NewLength (1 if none kept)
+                if (lc < l) lc = l;
+            }
+            a.d_key_len[k] = written;
+            a.d_key_off[k] = off + n - written;
+            if (a.key_id0) a.key_id0[k] = id0;
+            if (a.key_lcap) a.key_lcap[k] = lc;
+            if (meta) {
+                meta[i] = l;
+                meta[K + i] = 0u;
+                meta[2 * K + i] = lc;
+                meta[3 * K + i] = id0;
+                meta[4 * K + i] = (uint32_t)(off + n - written);
+                meta[5 * K + i] = 0u;
+            }
+            if (flags) flags[k] = l == 0 ? AGN_GC_ALL_PRUNED : 0u;
+        }
+    }
+}
+
 template <int DPL, int LPO, bool SPARSE>
 int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *thr,
                   const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags, hipStream_t st) {
@@ -1019,6 +1221,22 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         // gives the compiler's allocation (7 waves)
         const char *tmw = getenv("AGN_PRUNE_TAIL_MINW");
         const bool w8 = !(tmw && tmw[0] == '1');
+        // counter_pn with dense 8-DC rows: KPW keys per wave, every key's
+        // metadata and newest chunk in flight before the first is walked
+        // (AGN_PRUNE_TAIL_KPW=2|4, A/B knob)
+        if constexpr (DPL == 8 && LPO == 1 && !SPARSE) {
+            const char *kv = getenv("AGN_PRUNE_TAIL_KPW");
+            const int kpw = kv ? atoi(kv) : 1;
+            if (full && !tags && !w4 && (kpw == 2 || kpw == 4)) {
+                if (kpw == 2)
+                    hipLaunchKernelGGL((k_prune_tail_q<2, 1>), dim3(grid_for(a.n_keys, 2, 0x7fffffffu)),
+                                       dim3(64), 0, st, a, prune, thr, meta, flags);
+                else
+                    hipLaunchKernelGGL((k_prune_tail_q<4, 1>), dim3(grid_for(a.n_keys, 4, 0x7fffffffu)),
+                                       dim3(64), 0, st, a, prune, thr, meta, flags);
+                return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_tail_q launch");
+            }
+        }
 #define AGN_T(FULLV, TAGSV)                                                                    \
     do {                                                                                       \
         if (w4)                                                                                \

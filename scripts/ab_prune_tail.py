@@ -4,7 +4,8 @@ D = 8, threshold = the clock of a random position), variants alternated in
 one process on fresh logs (HBM rates move several % between processes):
   AGN_PRUNE_WPB = 1 | 4 (waves per block), AGN_PRUNE_TAIL_MINW = 1 | 8 (the
   compiler's register allocation, 7 waves per SIMD, or the budget of 8: the
-  default since round 3).
+  default since round 3), AGN_PRUNE_TAIL_KPW = 2 | 4 (keys per wave, every
+  key's metadata and newest chunk in flight before the first is walked).
 Times the prune call's GPU span (events on the log's stream: the kernel plus
 the records' copy) and checks that both variants leave identical logs.
 
@@ -43,12 +44,14 @@ def main():
     fl = eng.empty(4 * K)
     variants = [("wpb1", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_MINW": "1"}),
                 ("wpb4", {"AGN_PRUNE_WPB": "4", "AGN_PRUNE_TAIL_MINW": "1"}),
-                ("minw8", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_MINW": "8"})]
+                ("minw8", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_MINW": "8"}),
+                ("kpw2", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_KPW": "2"}),
+                ("kpw4", {"AGN_PRUNE_WPB": "1", "AGN_PRUNE_TAIL_KPW": "4"})]
     ms = {v: [] for v, _ in variants}
     sig = {}
     for r in range(rounds + 1):
         for name, env in (variants if r % 2 == 0 else variants[::-1]):
-            os.environ.update(env)
+            os.environ.update({"AGN_PRUNE_TAIL_KPW": "1", **env})
             with OpLog(eng, _abi.COUNTER_PN, D, K, init_slots=N + 8) as ol:
                 ol.append(keys, oc, txid=txid, eff=eff)
                 ol.flush()

@@ -201,16 +201,19 @@ def test_oplog_append_materialize(eng, oracle_lib, crdt, D, sparse, init):
         assert not materialize_view(eng, oracle_lib, view, log2, req, sparse)
 
 
-@pytest.fixture(params=["tail", "tail4", "tail7", "front"])
+@pytest.fixture(params=["tail", "tail4", "tail7", "tailq2", "tailq4", "front"])
 def anchor(request, monkeypatch):
     """The engine-owned log's prune kernel: k_prune_tail (kept entries compacted
     toward the end of the live range, the default; "tail4": four waves per
     block, AGN_PRUNE_WPB=4; "tail7": the compiler's register allocation,
-    AGN_PRUNE_TAIL_MINW=1, instead of the default budget of 8 waves) or the
-    start-anchored k_prune_inplace (AGN_PRUNE_TAIL=0)."""
+    AGN_PRUNE_TAIL_MINW=1, instead of the default budget of 8 waves; "tailq2"
+    / "tailq4": the counter form with 2 / 4 keys per wave, AGN_PRUNE_TAIL_KPW)
+    or the start-anchored k_prune_inplace (AGN_PRUNE_TAIL=0)."""
     monkeypatch.setenv("AGN_PRUNE_TAIL", "0" if request.param == "front" else "1")
     monkeypatch.setenv("AGN_PRUNE_WPB", "4" if request.param == "tail4" else "1")
     monkeypatch.setenv("AGN_PRUNE_TAIL_MINW", "1" if request.param == "tail7" else "8")
+    monkeypatch.setenv("AGN_PRUNE_TAIL_KPW", request.param[5:] if request.param.startswith("tailq")
+                       else "1")
     return "front" if request.param == "front" else "tail"
 
 
