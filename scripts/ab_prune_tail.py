@@ -64,6 +64,7 @@ def main():
                 torch.cuda.synchronize()
                 if r:  # round 0 warms both variants up
                     ms[name].append(b.elapsed_time(e))
+                print(f"# round {r} {name}: {b.elapsed_time(e):.3f} ms", flush=True)
                 if r == 0:
                     ln, lc, ctr = ol.key_meta()
                     sig[name] = (int(st["entries"]), int(ln.astype(np.int64).sum()),
