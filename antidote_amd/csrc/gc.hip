@@ -1222,11 +1222,13 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         const char *tmw = getenv("AGN_PRUNE_TAIL_MINW");
         const bool w8 = !(tmw && tmw[0] == '1');
         // counter_pn with dense 8-DC rows: KPW keys per wave, every key's
-        // metadata and newest chunk in flight before the first is walked
-        // (AGN_PRUNE_TAIL_KPW=2|4, A/B knob)
+        // metadata and newest chunk in flight before the first is walked --
+        // 2 by default (prefix drop, 2M x 64: 2.31 ms per GC call against
+        // 2.43 for one key per wave at 8 waves per SIMD and 2.35 for 4 keys;
+        // profiles/r03/ab_prune_tail_kpw.log); AGN_PRUNE_TAIL_KPW=1|2|4
         if constexpr (DPL == 8 && LPO == 1 && !SPARSE) {
             const char *kv = getenv("AGN_PRUNE_TAIL_KPW");
-            const int kpw = kv ? atoi(kv) : 1;
+            const int kpw = kv ? atoi(kv) : 2;
             if (full && !tags && !w4 && (kpw == 2 || kpw == 4)) {
                 if (kpw == 2)
                     hipLaunchKernelGGL((k_prune_tail_q<2, 1>), dim3(grid_for(a.n_keys, 2, 0x7fffffffu)),
