@@ -694,10 +694,16 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
                        xcd_remap() ? 1u : 0u);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // the overflow pass grid-strides over a list of at most n_req keys: a
+    // resident grid of up to 256 one-wave blocks (112 KB of LDS each), no
+    // more than the batch -- a serving batch of ~10 reads must not occupy
+    // every CU's LDS, while other partitions' batches wait, to find the list
+    // empty
     TagLists slow{ovf, ovf_n, nullptr, nullptr, mix, mix_n};
+    const unsigned sblocks = (unsigned)(req.n_req < 256u ? (req.n_req ? req.n_req : 1u) : 256u);
     hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM, true, CT,
                                MSK>),
-                       dim3(256), dim3(64), 0, st, log, req, out, slow, 0u);
+                       dim3(sblocks), dim3(64), 0, st, log, req, out, slow, 0u);
     return hipGetLastError();
 }
 
