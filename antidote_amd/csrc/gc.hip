@@ -310,6 +310,9 @@ struct InplaceArgs {
     // engine-owned log: meta has 6 rows, the last two the key's live range
     // start after the prune (entry slot, token slot; arenas < 2^32 slots)
     int meta6;
+    // set/register removal tokens of an iteration's kept entries copied by
+    // the whole wave (lane = token) instead of by each entry's head lane
+    int tcoop;
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -537,11 +540,6 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
         uint64_t tk[PT];
         const bool head = kp && sub == 0;
         if (!head) rl_ = 0;
-        const bool long_list = tags && ballot(head && rl_ > (uint32_t)PT) != 0ull;
-        if (tags && !long_list && head) {
-#pragma unroll
-            for (int x = 0; x < PT; ++x) tk[x] = (uint32_t)x < rl_ ? a.tok[r0 + x] : 0ull;
-        }
         // token destinations: exclusive scan of the kept list lengths
         uint32_t tincl = 0;
         if (tags) {
@@ -553,6 +551,47 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             }
         }
         const uint32_t tdst = tb + rwritten + (tincl - rl_);
+        const uint32_t T = tags ? (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63) : 0u;
+        // tcoop: the iteration's kept tokens as one run, lane = token (its
+        // owner entry by a binary search over the lanes' inclusive scan),
+        // TM per lane per round -- one round trip for the whole iteration
+        // where the head-lane copy serialises one round trip per kept entry
+        // once any list is longer than PT.  In place a token's destination
+        // is never above its source and sources rise with the token index,
+        // so a round's stores never reach a later round's sources
+        constexpr int TM = 4;
+        const bool coop = tags && a.tcoop;
+        uint64_t cv[TM];
+        auto coop_load = [&](uint32_t base) {
+#pragma unroll
+            for (int m = 0; m < TM; ++m) {
+                const uint32_t t = base + (uint32_t)(m * AGN_WAVE + lane);
+                int lo = 0;  // first lane whose inclusive count exceeds t
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1) {
+                    const uint32_t v = (uint32_t)__shfl((int)tincl, lo + step - 1, AGN_WAVE);
+                    lo = v <= t ? lo + step : lo;
+                }
+                const int ow = lo < AGN_WAVE ? lo : AGN_WAVE - 1;
+                const uint32_t o0 = (uint32_t)__shfl((int)r0, ow, AGN_WAVE);
+                const uint32_t oi = (uint32_t)__shfl((int)tincl, ow, AGN_WAVE);
+                const uint32_t ol = (uint32_t)__shfl((int)rl_, ow, AGN_WAVE);
+                cv[m] = t < T ? a.tok[o0 + (t - (oi - ol))] : 0ull;
+            }
+        };
+        auto coop_store = [&](uint32_t base) {
+#pragma unroll
+            for (int m = 0; m < TM; ++m) {
+                const uint32_t t = base + (uint32_t)(m * AGN_WAVE + lane);
+                if (t < T) a.d_tok[tb + rwritten + t] = cv[m];
+            }
+        };
+        if (coop) coop_load(0u);
+        const bool long_list = tags && !coop && ballot(head && rl_ > (uint32_t)PT) != 0ull;
+        if (tags && !coop && !long_list && head) {
+#pragma unroll
+            for (int x = 0; x < PT; ++x) tk[x] = (uint32_t)x < rl_ ? a.tok[r0 + x] : 0ull;
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         // stores
@@ -599,7 +638,17 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             }
         }
         if (tags) {
-            if (!long_list) {
+            if (coop) {
+                coop_store(0u);
+                for (uint32_t base = TM * AGN_WAVE; base < T; base += TM * AGN_WAVE) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    coop_load(base);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    coop_store(base);
+                }
+            } else if (!long_list) {
                 if (head) {
 #pragma unroll
                     for (int x = 0; x < PT; ++x)
@@ -1391,6 +1440,8 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.xcd = xcd_remap() ? 1 : 0;
     const char *lf = getenv("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
+    const char *tc = getenv("AGN_PRUNE_TCOOP");  // A/B knob: 0 | 1
+    a.tcoop = (tc && tc[0] == '1') ? 1 : 0;
     a.meta6 = 0;
     return a;
 }
