@@ -78,6 +78,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             best[name].append(b.elapsed_time(e))
+            print(f"# round {r} {name}: {b.elapsed_time(e):.3f} ms", flush=True)
             if r == 0:  # the variants' outputs must be identical
                 sig = []
                 for c in chk:
