@@ -107,6 +107,30 @@ KERNEL_SOURCES = {   # the sources the dominant kernel of each config is built f
 }
 
 
+def lib_provenance():
+    """The shared library this process loaded: its sha256 prefix, size and
+    mtime, and the hash of every HIP source in antidote_amd/csrc plus the
+    header -- so a bench line names the exact build it measured."""
+    import hashlib
+    lib = os.path.join(ROOT, "antidote_amd", "libantidote_gpu.so")
+    h = hashlib.sha256()
+    with open(lib, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    src = hashlib.sha256()
+    cdir = os.path.join(ROOT, "antidote_amd", "csrc")
+    for f in sorted(os.listdir(cdir)) + ["../../include/antidote_gpu.h"]:
+        path = os.path.join(cdir, f)
+        if f.endswith((".hip", ".hpp", ".h")) and os.path.isfile(path):
+            src.update(os.path.basename(f).encode())
+            with open(path, "rb") as fh:
+                src.update(fh.read())
+    st = os.stat(lib)
+    return {"lib_sha16": h.hexdigest()[:16], "lib_bytes": st.st_size,
+            "lib_mtime_utc": time.strftime("%Y-%m-%d %H:%M:%S", time.gmtime(st.st_mtime)),
+            "csrc_sha16": src.hexdigest()[:16]}
+
+
 def kernel_src_sha16(config):
     """Hash of the sources the config's dominant kernel is built from; a PMC
     traffic file (profiles/pmc/cfgN.json, scripts/pmc_traffic.py) is only used
@@ -441,6 +465,7 @@ def main():
             "kernel_variant": tune,
             "error_keys": err_keys, "mean_included_ops": float(count.mean()),
             "gen_s": t_gen,
+            "build": lib_provenance(),
         }
         if presence:
             line["presence"] = presence
