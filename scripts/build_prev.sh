@@ -8,8 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
 git -C "$ROOT" archive "$REV" antidote_amd/csrc include | tar -x -C "$T"
 cd "$T/antidote_amd/csrc"
-make -s -j8 build/api.o build/mat_counter.o build/mat_counter_dense.o build/mat_tags.o build/gst.o \
-    build/gc.o build/cache.o build/ingest.o build/oplog.o build/batcher.o
+make -s -j8 $(ls *.hip | sed 's/\.hip$/.o/; s/^/build\//')
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -o "$ROOT/tools/libagn_prev.so" \
     build/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf "$T"
