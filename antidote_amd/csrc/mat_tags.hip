@@ -46,18 +46,12 @@ constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t NIL = 0xffffffffu;
 
 
-// 16-bit chain links (CAP <= 4096 < NIL16): the fast table is 6.5 KB per
-// wave instead of 7 KB, so 24 one-wave blocks fit a CU's 160 KB of LDS --
-// the VGPR limit of 6 waves per SIMD -- where 22 did
-constexpr uint16_t NIL16 = 0xffffu;
-
 template <int CAP>
 struct CandLds {
-    static_assert(CAP < NIL16, "16-bit chain links");
     uint64_t tok[CAP];
     uint32_t tag[CAP];
     uint32_t ord[CAP];   // B + position (base pairs: index < B); DEAD bit
-    uint16_t nxt[CAP];   // hash chain (NIL16 ends it)
+    uint32_t nxt[CAP];   // hash chain
     uint32_t head[2 * CAP];
 };
 
@@ -86,7 +80,7 @@ __device__ __forceinline__ void heads_clear(CandLds<CAP> &L) {
 template <int CAP>
 __device__ __forceinline__ void link(CandLds<CAP> &L, uint32_t s, uint64_t t) {
     const uint32_t prev = atomicExch(&L.head[hbucket<CAP>(t)], s);
-    L.nxt[s] = prev == NIL ? NIL16 : (uint16_t)prev;
+    L.nxt[s] = prev;
 }
 
 // Stable in-place compaction of the live candidates [0, used); returns the
@@ -560,8 +554,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                     const bool einc = (im >> sidx) & 1ull;
                     if (has && einc) {
                         const uint32_t qpos = B + (uint32_t)(c0 + sidx);
-                        for (uint32_t x = L.head[hbucket<CAP>(t)]; x != NIL;
-                             x = L.nxt[x] == NIL16 ? NIL : (uint32_t)L.nxt[x]) {
+                        for (uint32_t x = L.head[hbucket<CAP>(t)]; x != NIL; x = L.nxt[x]) {
                             if (L.tok[x] != t) continue;
                             if (SET && L.tag[x] != etag) continue;
                             const uint32_t o = L.ord[x];
