@@ -1,6 +1,8 @@
 """A/B of the masked counter kernel (presence masks, uniform keys) against the
 dense one on cfg2 in one process, variants interleaved: which of the masked
-batch's extra inputs / outputs costs what.
+batch's extra inputs / outputs costs what, and the register budget of 8
+waves per SIMD for cold masked batches (AGN_COUNTER_MSK_MINW=8; "_w8"), on
+uniform keys and on mixed ones (bench.py --sparse mixed masks).
 
   python scripts/ab_masked.py [rounds]
 """
@@ -29,8 +31,12 @@ def main():
     dl, dr = eng.gen_dev(g)
     ocm = torch.full((K * N,), 255, dtype=torch.int64, device="cuda")
     rm = torch.full((K,), 255, dtype=torch.int64, device="cuda")
+    from bench import presence_masks
+    ocm_x, _ = presence_masks("mixed", D, K * N, K, torch=torch)
+    kbx = eng.empty(8 * K)
     res_d = eng.alloc_result(K, D, sparse=False)
     res_s = eng.alloc_result(K, D, sparse=True)
+    res_x = eng.alloc_result(K, D, sparse=True)
     kb = eng.empty(8 * K)
 
     def variant(name):
@@ -47,20 +53,28 @@ def main():
             res = res_d
         if name == "masked_no_R_mask":
             rs.R_mask = None
+        if name.startswith("mixed"):
+            ls.oc_mask = ocm_x.data_ptr()
+            ls.key_mask = kbx.ptr
+            res = res_x
         if name == "out_mask_only":
             ls.oc_mask = None
             ls.key_mask = None
             rs.R_mask = None
             res = res_s
         return ls, rs, res
-    names = ["dense", "masked", "masked_no_out_mask", "masked_no_R_mask", "out_mask_only"]
+    names = ["dense", "masked", "masked_w8", "masked_no_out_mask", "masked_no_R_mask",
+             "out_mask_only", "mixed", "mixed_w8"]
     args = {n: variant(n) for n in names}
     check = eng.lib.agn_log_index_masks(eng.ctx, C.byref(args["masked"][0]), kb.ptr, sp)
+    assert check == 0
+    check = eng.lib.agn_log_index_masks(eng.ctx, C.byref(args["mixed"][0]), kbx.ptr, sp)
     assert check == 0
     ms = {n: [] for n in names}
     for r in range(rounds + 1):
         for n in (names if r % 2 == 0 else names[::-1]):
             ls, rs, res = args[n]
+            os.environ["AGN_COUNTER_MSK_MINW"] = "8" if n.endswith("_w8") else "1"
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             b.record(st)
             eng.materialize(ls, rs, res, stream=sp)
@@ -69,7 +83,9 @@ def main():
             if r:
                 ms[n].append(b.elapsed_time(e))
     v = {n: eng.download(args[n][2].bufs["value"], np.int64, (K,)) for n in names}
-    same = {n: bool(np.array_equal(v[n], v["dense"])) for n in names}
+    # uniform masks give the dense values; the mixed log's own pair must agree
+    same = {n: bool(np.array_equal(v[n], v["mixed" if n.startswith("mixed") else "dense"]))
+            for n in names}
     print(json.dumps({"warm": int(os.environ.get("WARM", "0")),
                       "variant": os.environ.get("AGN_COUNTER_VARIANT", "default"),
                       "ms_median": {n: float(np.median(x)) for n, x in ms.items()},
