@@ -211,10 +211,8 @@ enum { ROWS_VGPR = 0, ROWS_GLDS = 1, ROWS_QUAD = 2, ROWS_QUAD2 = 3 };
 // (writing 16 B instead: 8.33 -> 7.57 ms), full 128 B record lines 1 %,
 // non-temporal stores +7 % worse.  The HBM read/write turnaround, not the
 // instruction stream, is the remaining bound.
-// MINW: waves per SIMD the register allocation must allow (1 = the
-// compiler's choice)
-template <int D, bool ANY_WARM, int WPB, int VAR, bool KEYS, bool MSK, int MINW = 1>
-__global__ __launch_bounds__(64 * WPB, MINW) void k_counter_key(
+template <int D, bool ANY_WARM, int WPB, int VAR, bool KEYS, bool MSK>
+__global__ __launch_bounds__(64 * WPB) void k_counter_key(
     DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
     const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
     const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
@@ -788,12 +786,6 @@ int counter_variant() {
     return t >= 0 ? t : default_variant<D>();
 }
 
-// AGN_COUNTER_MSK_MINW=8 (A/B knob): cold masked batches at 8 waves per SIMD
-inline bool msk_minw8() {
-    const char *v = getenv("AGN_COUNTER_MSK_MINW");
-    return v && v[0] == '8';
-}
-
 template <int D, int WPB, int VAR, bool KEYS, bool MSK>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     const char *qv = getenv("AGN_COUNTER_QUAD_NT");
@@ -803,22 +795,12 @@ int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out,
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                         (unsigned long long)req.n_req);
-    const bool msk8 = MSK && msk_minw8();
     if (req.sct)
         hipLaunchKernelGGL((k_counter_key<D, true, WPB, VAR, KEYS, MSK>), dim3((unsigned)nb),
                            dim3(64 * WPB), 0, st, a, mk, req.keys, log.key_off, log.key_len,
                            log.key_type, id0_index(log), log.oc, log.op_id, log.eff, log.txid,
                            req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,
                            out.hole, out.lastct, out.count, out.flags, out.err_pos);
-    else if (msk8)
-        // a cold masked batch with the register budget of 8 waves per SIMD
-        // (the compiler's allocation: 66 VGPRs / 92-106 SGPRs, 7 waves)
-        hipLaunchKernelGGL((k_counter_key<D, false, WPB, VAR, KEYS, MSK, MSK ? 8 : 1>),
-                           dim3((unsigned)nb), dim3(64 * WPB), 0, st, a, mk, req.keys,
-                           log.key_off, log.key_len, log.key_type, id0_index(log), log.oc,
-                           log.op_id, log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid,
-                           req.base_value, out.value, out.hole, out.lastct, out.count, out.flags,
-                           out.err_pos);
     else
         hipLaunchKernelGGL((k_counter_key<D, false, WPB, VAR, KEYS, MSK>), dim3((unsigned)nb),
                            dim3(64 * WPB), 0, st, a, mk, req.keys, log.key_off, log.key_len,

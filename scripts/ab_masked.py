@@ -1,8 +1,9 @@
 """A/B of the masked counter kernel (presence masks, uniform keys) against the
 dense one on cfg2 in one process, variants interleaved: which of the masked
-batch's extra inputs / outputs costs what, and the register budget of 8
-waves per SIMD for cold masked batches (AGN_COUNTER_MSK_MINW=8; "_w8"), on
-uniform keys and on mixed ones (bench.py --sparse mixed masks).
+batch's extra inputs / outputs costs what, on uniform keys and on mixed ones
+(bench.py --sparse mixed masks).  Round 3 also timed the register budget of
+8 waves per SIMD for cold masked batches ("_w8" variants: 8.51 vs 8.49 ms,
+mixed 9.57 vs 9.46; profiles/r03/ab_masked_w8.log) -- not kept.
 
   python scripts/ab_masked.py [rounds]
 """
@@ -63,8 +64,8 @@ def main():
             rs.R_mask = None
             res = res_s
         return ls, rs, res
-    names = ["dense", "masked", "masked_w8", "masked_no_out_mask", "masked_no_R_mask",
-             "out_mask_only", "mixed", "mixed_w8"]
+    names = ["dense", "masked", "masked_no_out_mask", "masked_no_R_mask", "out_mask_only",
+             "mixed"]
     args = {n: variant(n) for n in names}
     check = eng.lib.agn_log_index_masks(eng.ctx, C.byref(args["masked"][0]), kb.ptr, sp)
     assert check == 0
@@ -74,7 +75,6 @@ def main():
     for r in range(rounds + 1):
         for n in (names if r % 2 == 0 else names[::-1]):
             ls, rs, res = args[n]
-            os.environ["AGN_COUNTER_MSK_MINW"] = "8" if n.endswith("_w8") else "1"
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             b.record(st)
             eng.materialize(ls, rs, res, stream=sp)

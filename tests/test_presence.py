@@ -85,18 +85,15 @@ def device_result(eng, log, req, index):
     return eng.fetch_result(dres)
 
 
-IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "vgpr_w8": "0", "quad_w8": "2"}
+IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3"}
 
 
 @pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
-@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "vgpr_w8", "quad_w8"])
+@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
 def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
-    """"_w8": the cold masked kernels with the register budget of 8 waves
-    per SIMD (AGN_COUNTER_MSK_MINW=8)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
-    monkeypatch.setenv("AGN_COUNTER_MSK_MINW", "8" if impl.endswith("_w8") else "1")
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
     else:
