@@ -842,13 +842,17 @@ int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, h
     const int v = counter_variant<D>();
     // quad rows, warm batch (SCT given), not forced: two requests per wave
     // (warm cfg2 8.37-8.45 vs 8.83-9.02 ms; cold no change,
-    // profiles/r02/ab_counter_quad2.log)
+    // profiles/r02/ab_counter_quad2.log) -- for dense batches: a masked warm
+    // batch keeps one request per wave (its two-request form takes 118
+    // VGPRs, 4 waves per SIMD: warm masked cfg2 13.06 vs 11.06 ms, mixed keys
+    // 17.32 vs 13.00; profiles/r03/ab_masked_warm_quad{2,1}.log)
+    const bool masked = sparse_batch(log, req, out);
     if constexpr (D == 8)
-        if (v == ROWS_QUAD2 || (v == ROWS_QUAD && req.sct && forced_variant() < 0))
+        if (v == ROWS_QUAD2 || (v == ROWS_QUAD && req.sct && !masked && forced_variant() < 0))
             return launch_quad2(log, req, out, st);
     const int v2 = v == ROWS_QUAD2 ? default_variant<D>() : v;
-    return sparse_batch(log, req, out) ? launch_var<D, WPB, true>(v2, log, req, out, st)
-                                       : launch_var<D, WPB, false>(v2, log, req, out, st);
+    return masked ? launch_var<D, WPB, true>(v2, log, req, out, st)
+                  : launch_var<D, WPB, false>(v2, log, req, out, st);
 }
 
 // Waves (= requests) per block: 1 measured 1.4-3.4 % faster than 2 and
