@@ -193,13 +193,14 @@ JOIN = 1500   # step at which a fourth DC joins
 
 class DictWorkload:
     """Dict clocks over interned DC columns, as nif clock_row builds them:
-    DCs 0..2 from the start, DC 3 from step JOIN on."""
+    DCs 0..n0-1 from the start (n0 = 3: DC 3 joins at step JOIN; n0 = DCAP:
+    every column interned, full clocks throughout)."""
 
-    def __init__(self, seed, K):
+    def __init__(self, seed, K, n0=3):
         self.rng = np.random.default_rng(seed)
         self.clk = np.zeros(DCAP, np.int64)
-        self.clk[:3] = 1000
-        self.n_dc = 3
+        self.clk[:n0] = 1000
+        self.n_dc = n0
         self.K = K
 
     def join(self):
@@ -233,16 +234,20 @@ def dvc(row, n):
     return {d: int(row[d]) for d in range(n)}
 
 
+@pytest.mark.parametrize("clocks", ["join", "full"])
 @pytest.mark.parametrize("read6", ["1", "0"])
-def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6):
+def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clocks):
     """update/2 + read/6 as nif/antidote_gpu_nif.c issues them, on a sparse
     log (presence masks; the NIF's configuration) and on a dense log: every
     read bit-identical between the two (value, NewLastOp, LastOpCt, Count,
     flags, cache status), LastOpCt's DC set inside the DCs known at the read,
-    and every served value equal to the reference's ETS transcription."""
+    and every served value equal to the reference's ETS transcription.
+    clocks = "join": 3 DCs, a fourth joining halfway (mixed keys, readers
+    whose snapshot predates it); "full": every column interned from the
+    start (the steady deployment: the dense routes serve every read)."""
     monkeypatch.setenv("AGN_READ6", read6)
     K, steps = 24, 3500
-    w = DictWorkload(23, K)
+    w = DictWorkload(23, K, n0=3 if clocks == "join" else DCAP)
     vn = po.MaterializerVnode()
     quirk, served, n_cmp = set(), 0, 0
     with OpLog(eng, _abi.COUNTER_PN, DCAP, K, sparse=True) as ls, \
@@ -250,7 +255,7 @@ def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6):
             Batcher(ls, max_batch=8, cached=True) as bs, \
             Batcher(ld, max_batch=8, cached=True) as bd:
         for s in range(steps):
-            if s == JOIN:
+            if s == JOIN and clocks == "join":
                 w.join()
             key = int(w.rng.integers(0, K))
             if w.rng.random() < 0.7:
