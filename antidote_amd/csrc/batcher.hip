@@ -38,15 +38,6 @@
 
 #include "serve.hpp"
 
-namespace agn {
-// (oplog.hip, mat_tags.hip) the masked tags batch without the per-entry-mask
-// passes when every requested key is uniform inside its read clock
-int oplog_keys_uniform(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint32_t *lens,
-                       const uint64_t *rmask, bool *uni);
-int launch_tags_uniform(const agn_log &log, const agn_read &req, const agn_result &out,
-                        hipStream_t st);
-}  // namespace agn
-
 using namespace agn;
 
 namespace {
@@ -354,16 +345,7 @@ int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
         res.out_n = (uint32_t *)(d + o_outn);
         res.out_tag = (uint32_t *)(d + o_otag);
         res.out_tok = (uint64_t *)(d + o_otok);
-        bool uni = false;  // AGN_TAGS_UNI=0 (A/B knob): always issue the per-entry-mask pair
-        const char *uv = getenv("AGN_TAGS_UNI");
-        if (sparse && W == 1 && !(uv && uv[0] == '0')) {
-            std::vector<uint64_t> rm(n);
-            for (uint64_t i = 0; i < n; ++i) rm[i] = b[i]->rd->R_mask ? b[i]->rd->R_mask[0] : full[0];
-            rc = oplog_keys_uniform(B->log, n, keys.data(), lens.data(), rm.data(), &uni);
-            if (rc) return rc;
-        }
-        rc = uni ? launch_tags_uniform(view, req, res, B->stream)
-                 : launch_tags(view, req, res, B->stream);
+        rc = launch_tags(view, req, res, B->stream);
         if (rc) return rc;
         rc = launch_ss_store_req(B->ss, view.key_off, view.key_len, n, dkeys,
                                  (const uint8_t *)(d + o_first), (const uint8_t *)(d + o_st),

@@ -739,14 +739,8 @@ int launch_shape(const agn_log &log, const agn_read &req, const agn_result &out,
 
 // Presence masks with a dense-loadable shape: the MSK dense passes, then the
 // per-entry-mask (SPARSE) passes over the keys they handed on.
-// skip_mixed: the caller knows every request's key is served by the dense
-// passes (its entries share one DC set inside R's, or it has none), so the
-// per-entry-mask pair -- two launches over an empty list -- is not issued
-// (the read batcher checks the op log's host DC sets; a serving batch of 10
-// set_aw reads: 67 -> 48 us).
 template <int DPL, int LPO, bool SET, bool WARM, bool CT, int SDPL, int SLPO>
-int launch_masked(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st,
-                  bool skip_mixed) {
+int launch_masked(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     TagScratch w;
     w.n = req.n_req;
     AGN_HIP(pool_malloc((void **)&w.base, (3 * req.n_req + 4) * sizeof(uint32_t), st));
@@ -754,7 +748,7 @@ int launch_masked(const agn_log &log, const agn_read &req, const agn_result &out
     if (e == hipSuccess)
         e = tags_passes<DPL, LPO, false, true, SET, WARM, CT, true>(
             log, req, out, nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n(), st);
-    if (e == hipSuccess && !skip_mixed)
+    if (e == hipSuccess)
         e = tags_passes<SDPL, SLPO, true, false, SET, WARM, false, false>(
             log, req, out, w.mix(), w.mix_n(), w.ovf2(), w.ovf2_n(), nullptr, nullptr, st);
     const int rc = e == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
@@ -823,13 +817,13 @@ int dispatch(const agn_log &log, const agn_read &req, const agn_result &out, hip
 // knob) disables it.
 template <bool SET>
 int dispatch_masked(const agn_log &log, const agn_read &req, const agn_result &out,
-                    hipStream_t st, bool skip_mixed = false) {
+                    hipStream_t st) {
     const char *v = getenv("AGN_TAGS_MSK");
     if (v && v[0] == '0') return AGN_ENOTSUP;
     const bool warm = req.sct != nullptr;
 #define AGN_M(DPL, LPO, CTV, SD, SL)                                                         \
-    return warm ? launch_masked<DPL, LPO, SET, true, CTV, SD, SL>(log, req, out, st, skip_mixed) \
-                : launch_masked<DPL, LPO, SET, false, CTV, SD, SL>(log, req, out, st, skip_mixed)
+    return warm ? launch_masked<DPL, LPO, SET, true, CTV, SD, SL>(log, req, out, st)       \
+                : launch_masked<DPL, LPO, SET, false, CTV, SD, SL>(log, req, out, st)
     switch (log.n_dcs) {
         case 2: AGN_M(2, 1, false, 2, 1);
         case 4: AGN_M(4, 1, false, 4, 1);
@@ -859,20 +853,6 @@ int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
     if (sparse) return set ? dispatch<true, true>(log, req, out, st)
                            : dispatch<true, false>(log, req, out, st);
     return set ? dispatch<false, true>(log, req, out, st) : dispatch<false, false>(log, req, out, st);
-}
-
-// launch_tags for a masked batch whose every key the caller has checked to
-// be uniform inside its read clock (see launch_masked's skip_mixed)
-int launch_tags_uniform(const agn_log &log, const agn_read &req, const agn_result &out,
-                        hipStream_t st) {
-    if (req.n_req == 0) return AGN_OK;
-    const bool set = log.crdt_type == AGN_SET_AW;
-    if (log.oc_mask && log.key_mask) {
-        const int rc = set ? dispatch_masked<true>(log, req, out, st, true)
-                           : dispatch_masked<false>(log, req, out, st, true);
-        if (rc != AGN_ENOTSUP) return rc;
-    }
-    return launch_tags(log, req, out, st);
 }
 
 }  // namespace agn

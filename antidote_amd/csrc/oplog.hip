@@ -1046,27 +1046,6 @@ int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *k
 }
 void oplog_view(const agn_oplog *L, agn_log *v) { fill_view(L, v); }
 
-// Whether every request's key is served by the dense (MSK) passes of the
-// masked tags kernel: no entries on the device (lens from oplog_begin_read),
-// or a shared DC set U inside the request's R DCs.  The host DC sets are
-// what the last flush shipped as agn_log.key_mask (an append after it can
-// only clear a set, which makes this answer false, never wrongly true).
-int oplog_keys_uniform(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint32_t *lens,
-                       const uint64_t *rmask, bool *uni) {
-    *uni = false;
-    if (!L->sparse || L->D > 64 || L->umask.empty()) return AGN_OK;
-    const uint64_t full = L->D >= 64 ? ~0ull : ((1ull << L->D) - 1ull);
-    std::lock_guard<std::mutex> g(L->wmu);
-    for (uint64_t i = 0; i < n; ++i) {
-        if (lens[i] == 0) continue;
-        const uint64_t U = L->umask[keys[i]] & full;
-        const uint64_t R = (rmask ? rmask[i] : ~0ull) & full;
-        if (U == 0 || (U & ~R) != 0) return AGN_OK;
-    }
-    *uni = true;
-    return AGN_OK;
-}
-
 int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uint64_t *d_keys,
                      const uint8_t *d_flags, const uint64_t *thr, const uint64_t *thr_mask,
                      hipStream_t st) {
