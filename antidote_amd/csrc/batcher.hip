@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "serve.hpp"
+#include "tags_serve.hpp"
 
 using namespace agn;
 
@@ -81,6 +82,7 @@ struct agn_batcher {
     // cached mode: the partition's device snapshot cache + GC scratch
     bool cached = false;
     bool read6 = true;  // the fused one-kernel batch (AGN_READ6=0: the kernel sequence)
+    bool tags_fused = true;  // set/register batches too (AGN_TAGS_FUSED=0: their sequence)
     agn_ss_cache ss{};
     uint64_t *thr = nullptr;    // [K][D] prune thresholds
     uint64_t *thrm = nullptr;   // [K][W] (sparse logs)
@@ -90,6 +92,10 @@ struct agn_batcher {
     // seen: every cached state is a result's), which sizes a batch's output
     uint64_t *ctl_h = nullptr;  // pinned [4]
     std::vector<uint32_t> kbound;
+    // the fused set/register read's scratch (tags_serve.hpp): 3 n + 4 words,
+    // the first 4 zero between batches
+    uint32_t *tscr = nullptr;
+    uint64_t tscr_n = 0;
 };
 
 namespace {
@@ -252,6 +258,175 @@ int ensure_state_room(agn_batcher *B, uint64_t need) {
     return AGN_OK;
 }
 
+// Cached mode, set_aw / register_mv with D = 2, 4, 6, 8: the fused read
+// (tags_serve.hpp) -- one kernel per batch reading the requests from, and
+// writing the results to, the pinned block (lookup -> fast tags pass ->
+// store, per request on one wave).  The host keeps its copy of state_ctl
+// from the stores' reported deltas.  A batch with keys the kernel handed on
+// (a state past the fast table, a key not uniform inside R's DC set) runs
+// the remaining passes and their store, and reads state_ctl back.
+int run_batch_tags_fused(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
+    const uint64_t n = b.size();
+    const uint32_t D = B->D, W = B->W;
+    std::vector<uint64_t> keys(n);
+    std::vector<uint32_t> lens(n);
+    for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
+    size_t d_keys = 0, d_pr = 0;
+    {
+        std::shared_lock<std::shared_mutex> hold;
+        int rc = oplog_begin_read(B->log, B->stream, n, keys.data(), lens.data(), hold);
+        if (rc) return rc;
+        std::vector<uint64_t> co(n + 1);
+        co[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + B->kbound[keys[i]];
+        const uint64_t ncap = co[n];
+        rc = ensure_state_room(B, ncap);
+        if (rc) return rc;
+        if (B->tscr_n < n) {
+            const uint64_t m = std::max<uint64_t>(n, 2 * B->tscr_n);
+            if (B->tscr) AGN_HIP(hipFree(B->tscr));
+            B->tscr = nullptr;
+            B->tscr_n = 0;
+            AGN_HIP(hipMalloc((void **)&B->tscr, (3 * m + 4) * sizeof(uint32_t)));
+            AGN_HIP(hipMemsetAsync(B->tscr, 0, 4 * sizeof(uint32_t), B->stream));
+            B->tscr_n = m;
+        }
+        // pinned block (the kernel addresses it through hdev)
+        size_t off = 0;
+        auto slot = [&](size_t bytes) { size_t o = off; off = al(off + bytes); return o; };
+        const size_t o_keys = slot(n * 8), o_R = slot(n * D * 8), o_Rm = slot(sparse ? n * W * 8 : 0),
+                     o_txid = slot(n * 8), o_gc = slot(n), o_cap = slot((n + 1) * 8),
+                     o_st = slot(n), o_pr = slot(n), o_dl = slot(n * 16), o_hole = slot(n * 8),
+                     o_ct = slot(n * D * 8), o_ctm = slot(sparse ? n * W * 8 : 0),
+                     o_cnt = slot(n * 4), o_flg = slot(n * 4), o_epos = slot(n * 4),
+                     o_outn = slot(n * 4), o_otag = slot(std::max<uint64_t>(ncap, 1) * 4),
+                     o_otok = slot(std::max<uint64_t>(ncap, 1) * 8);
+        const size_t hbytes = off;
+        // device block: the lookup's rows and the GC list
+        off = 0;
+        const size_t d_sct = slot(n * D * 8), d_sctm = slot(sparse ? n * W * 8 : 0),
+                     d_ign = slot(n), d_base = slot(n * 8), d_first = slot(n);
+        d_keys = slot(n * 8);
+        d_pr = slot(n);
+        rc = grow(B, std::max(hbytes, off));
+        if (rc) return rc;
+        char *h = B->hbuf, *x = B->hdev, *d = B->dbuf;
+        auto H = [&](size_t o) { return h + o; };
+        uint64_t full[4] = {0, 0, 0, 0};
+        for (uint32_t c = 0; c < D; ++c) full[c >> 6] |= 1ull << (c & 63);
+        bool any_tx = false;
+        for (uint64_t i = 0; i < n; ++i) {
+            const agn_key_read *r = b[i]->rd;
+            ((uint64_t *)H(o_keys))[i] = r->key;
+            std::memcpy(H(o_R) + i * D * 8, r->R, D * 8);
+            if (sparse) std::memcpy(H(o_Rm) + i * W * 8, r->R_mask ? r->R_mask : full, W * 8);
+            ((uint64_t *)H(o_txid))[i] = r->txid;
+            any_tx = any_tx || r->txid;
+            ((uint8_t *)H(o_gc))[i] = (r->flags & AGN_READ_GC) ? 1 : 0;
+        }
+        std::memcpy(H(o_cap), co.data(), (n + 1) * 8);
+        agn_log view;
+        oplog_view(B->log, &view);
+        agn_read req;
+        std::memset(&req, 0, sizeof req);
+        req.n_req = n;
+        req.keys = (const uint64_t *)(x + o_keys);
+        req.R = (const uint64_t *)(x + o_R);
+        req.R_mask = sparse ? (const uint64_t *)(x + o_Rm) : nullptr;
+        req.sct = (const uint64_t *)(d + d_sct);
+        req.sct_mask = sparse ? (const uint64_t *)(d + d_sctm) : nullptr;
+        req.sct_ignore = (const uint8_t *)(d + d_ign);
+        req.txid = any_tx ? (const uint64_t *)(x + o_txid) : nullptr;
+        req.req_type = B->crdt;
+        req.base_value = (const int64_t *)(d + d_base);  // AGN_SS_STATE into the arena
+        req.base_tag = B->ss.state_tag;
+        req.base_tok = B->ss.state_tok;
+        agn_result res;
+        std::memset(&res, 0, sizeof res);
+        res.hole = (int64_t *)(x + o_hole);
+        res.lastct = (uint64_t *)(x + o_ct);
+        res.lastct_mask = sparse ? (uint64_t *)(x + o_ctm) : nullptr;
+        res.count = (uint32_t *)(x + o_cnt);
+        res.flags = (uint32_t *)(x + o_flg);
+        res.err_pos = (uint32_t *)(x + o_epos);
+        res.out_off = (const uint64_t *)(x + o_cap);
+        res.out_n = (uint32_t *)(x + o_outn);
+        res.out_tag = (uint32_t *)(x + o_otag);
+        res.out_tok = (uint64_t *)(x + o_otok);
+        TagServe sv;
+        std::memset(&sv, 0, sizeof sv);
+        sv.c = B->ss;
+        sv.sct = (uint64_t *)(d + d_sct);
+        sv.sctm = sparse ? (uint64_t *)(d + d_sctm) : nullptr;
+        sv.ign = (uint8_t *)(d + d_ign);
+        sv.first = (uint8_t *)(d + d_first);
+        sv.base = (int64_t *)(d + d_base);
+        sv.status = (uint8_t *)(x + o_st);
+        sv.gc = (const uint8_t *)(x + o_gc);
+        sv.prune = (uint8_t *)(x + o_pr);
+        sv.delta = (uint64_t *)(x + o_dl);
+        sv.dkeys = (uint64_t *)(d + d_keys);
+        sv.dprune = (uint8_t *)(d + d_pr);
+        sv.thr = B->thr;
+        sv.thrm = B->thrm;
+        rc = launch_tags_serve(view, req, res, sv, B->tscr, B->stream);
+        if (rc) return rc;
+        rc = wait_batch(B);
+        if (rc) return rc;
+        bool handed_on = false;
+        for (uint64_t i = 0; i < n; ++i) handed_on = handed_on || (((const uint8_t *)H(o_pr))[i] & 4u);
+        if (handed_on) {
+            rc = launch_tags_serve_rest(view, req, res, sv, B->tscr, B->stream);
+            if (rc) return rc;
+            AGN_HIP(hipMemcpyAsync(H(o_pr), d + d_pr, n, hipMemcpyDeviceToHost, B->stream));
+            AGN_HIP(hipMemcpyAsync(B->ctl_h, B->ss.state_ctl, 4 * 8, hipMemcpyDeviceToHost, B->stream));
+            rc = wait_batch(B);
+            if (rc) return rc;
+        } else {
+            for (uint64_t i = 0; i < n; ++i) {
+                const uint64_t *dl = (const uint64_t *)H(o_dl) + 2 * i;
+                B->ctl_h[0] += dl[0];
+                B->ctl_h[1] += dl[1];
+                if (((const uint8_t *)H(o_pr))[i] & 2u) B->ctl_h[2] = 1;
+            }
+        }
+        if (B->ctl_h[2]) return fail(AGN_ECAPACITY, "batcher: state arena overflow");
+        bool any_prune = false;
+        for (uint64_t i = 0; i < n; ++i) {
+            agn_key_result *o = b[i]->out;
+            const uint32_t m = ((const uint32_t *)H(o_outn))[i];
+            o->status = ((const uint8_t *)H(o_st))[i];
+            o->value = 0;
+            o->hole = ((const int64_t *)H(o_hole))[i];
+            std::memcpy(o->lastct, H(o_ct) + i * D * 8, D * 8);
+            if (o->lastct_mask)
+                std::memcpy(o->lastct_mask, sparse ? H(o_ctm) + i * W * 8 : (char *)full, W * 8);
+            o->count = ((const uint32_t *)H(o_cnt))[i];
+            o->flags = ((const uint32_t *)H(o_flg))[i];
+            o->err_pos = ((const uint32_t *)H(o_epos))[i];
+            any_prune = any_prune || (((const uint8_t *)H(o_pr))[i] & 1u) != 0;
+            const bool ok = !(o->flags & (AGN_F_ERR_CORRUPTED | AGN_F_ERR_UNEXPECTED |
+                                          AGN_F_ERR_CAPACITY));
+            o->out_n = ok ? m : 0;
+            if (ok) B->kbound[keys[i]] = std::max(B->kbound[keys[i]], m);
+            if (!ok || o->status == AGN_SS_LOG) continue;
+            if (m > o->out_cap) {  // the caller retries with out_cap >= out_n
+                b[i]->rc = AGN_ECAPACITY;
+                std::snprintf(b[i]->err, sizeof b[i]->err, "batcher_read: %u pairs, out_cap %u",
+                              m, o->out_cap);
+                continue;
+            }
+            if (m) {
+                std::memcpy(o->out_tag, H(o_otag) + co[i] * 4, m * 4);
+                std::memcpy(o->out_tok, H(o_otok) + co[i] * 8, m * 8);
+            }
+        }
+        if (!any_prune) return AGN_OK;
+    }  // the shared hold ends: the GC takes the log exclusively
+    return oplog_prune_keys(B->log, n, keys.data(), (const uint64_t *)(B->dbuf + d_keys),
+                            (const uint8_t *)(B->dbuf + d_pr), B->thr, B->thrm, B->stream);
+}
+
 // Cached mode, set_aw / register_mv: read/6 for a batch with the snapshot
 // states on the device.  get_from_snapshot_cache's base is the hit slot's
 // state in the arena (agn_ss_lookup writes its AGN_SS_STATE reference), the
@@ -263,6 +438,12 @@ int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
     const uint32_t D = B->D, W = B->W;
     bool sparse = B->sparse_log != 0;
     for (Pending *p : b) sparse = sparse || p->rd->R_mask;
+    if (B->read6 && B->tags_fused) {
+        agn_log v;  // the shape only (the log's view is taken under its hold)
+        std::memset(&v, 0, sizeof v);
+        v.n_dcs = D;
+        if (tags_serve_supported(v, sparse)) return run_batch_tags_fused(B, b, sparse);
+    }
     std::vector<uint64_t> keys(n);
     std::vector<uint32_t> lens(n);
     for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
@@ -757,6 +938,7 @@ int agn_batcher_destroy(agn_batcher *B) {
                     (void *)B->ss.state_tag, (void *)B->ss.state_tok, (void *)B->ss.state_ctl})
         if (p) (void)hipFree(p);
     if (B->ctl_h) (void)hipHostFree(B->ctl_h);
+    if (B->tscr) (void)hipFree(B->tscr);
     if (B->stream) (void)hipStreamDestroy(B->stream);
     delete B;
     return AGN_OK;
@@ -825,6 +1007,8 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     (*out)->cached = true;
     const char *r6 = getenv("AGN_READ6");
     (*out)->read6 = !(r6 && r6[0] == '0');
+    const char *tf = getenv("AGN_TAGS_FUSED");
+    (*out)->tags_fused = !(tf && tf[0] == '0');
     (*out)->ss = c;
     (*out)->thr = thr;
     (*out)->thrm = thrm;

@@ -15,6 +15,7 @@
 // at most SNAPSHOT_MIN + 1 rows.
 #include "cache_dev.hpp"
 #include "serve.hpp"
+#include "tags_serve.hpp"
 
 namespace agn {
 namespace {
@@ -55,9 +56,15 @@ __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t
                                                   agn_result res, const int64_t *__restrict__ handle,
                                                   uint8_t *__restrict__ prune,
                                                   uint64_t *__restrict__ thr,
-                                                  uint64_t *__restrict__ thrm, int by_req) {
+                                                  uint64_t *__restrict__ thrm, int by_req,
+                                                  const uint32_t *__restrict__ list,
+                                                  const uint32_t *__restrict__ list_n) {
     const Grp<G> g;
-    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    if (list) {  // a request list (the fused set/register read's hand-ons)
+        if (i >= *list_n) return;
+        i = list[i];
+    }
     if (i >= n_req) return;
     const uint32_t D = c.n_dcs, W = n_words(D);
     const uint64_t k = keys ? keys[i] : i;
@@ -94,10 +101,11 @@ template <int G>
 int store_g(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len, uint64_t n_req, const uint64_t *keys,
             const uint8_t *is_first, const uint8_t *status, const uint8_t *should_gc,
             const agn_result &res, const int64_t *handle, uint8_t *prune, uint64_t *thr,
-            uint64_t *thrm, int by_req, hipStream_t st) {
+            uint64_t *thrm, int by_req, hipStream_t st, const uint32_t *list = nullptr,
+            const uint32_t *list_n = nullptr) {
     hipLaunchKernelGGL((k_ss_store<G>), dim3(grid_for(n_req, 256 / G, 0x7fffffffu)), dim3(256), 0,
                        st, c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, handle,
-                       prune, thr, thrm, by_req);
+                       prune, thr, thrm, by_req, list, list_n);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }
@@ -199,6 +207,19 @@ int launch_ss_store_req(const agn_ss_cache &c, const uint64_t *key_off, const ui
 #define AGN_C(G) \
     store_g<G>(c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, nullptr, \
                prune_req, thr, thrm, 1, st)
+    AGN_GROUP_DISPATCH(c.n_dcs, AGN_C)
+#undef AGN_C
+}
+
+int launch_ss_store_list(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_len,
+                         uint64_t n_req, const uint32_t *list, const uint32_t *list_n,
+                         const uint64_t *keys, const uint8_t *is_first, const uint8_t *status,
+                         const uint8_t *should_gc, const agn_result &res, uint8_t *prune_req,
+                         uint64_t *thr, uint64_t *thrm, hipStream_t st) {
+    if (n_req == 0) return AGN_OK;
+#define AGN_C(G) \
+    store_g<G>(c, key_off, key_len, n_req, keys, is_first, status, should_gc, res, nullptr, \
+               prune_req, thr, thrm, 1, st, list, list_n)
     AGN_GROUP_DISPATCH(c.n_dcs, AGN_C)
 #undef AGN_C
 }

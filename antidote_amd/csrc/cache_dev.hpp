@@ -138,7 +138,9 @@ __device__ __forceinline__ uint64_t grp_bcast(const Grp<G> &g, uint64_t v) {
 // of key k (vectorclock:min of the kept clocks, :523-527) and returns whether
 // its ops are to be pruned.  Group-uniform.  A set_aw / register_mv cache
 // with a state arena (c.state_tag) stores the result's state (st_tag /
-// st_tok, st_n pairs) there and records the pairs of the snapshots it drops.
+// st_tok, st_n pairs) there and records the pairs of the snapshots it drops;
+// dl (optional, the group's first lane): the pairs added to state_ctl[0] and
+// [1], and whether the store overflowed the arena.
 template <int G>
 __device__ __forceinline__ bool ss_store_one(const Grp<G> &g, const agn_ss_cache &c, uint64_t k,
                                              uint64_t nops, uint8_t status, uint8_t is_first,
@@ -148,7 +150,7 @@ __device__ __forceinline__ bool ss_store_one(const Grp<G> &g, const agn_ss_cache
                                              uint64_t *thr, uint64_t *thrm,
                                              const uint32_t *st_tag = nullptr,
                                              const uint64_t *st_tok = nullptr,
-                                             uint32_t st_n = 0) {
+                                             uint32_t st_n = 0, uint64_t *dl = nullptr) {
     const uint32_t D = c.n_dcs, W = n_words(D), S = c.slots;
     if (status == AGN_SS_LOG) return false;
     if (nops == 0) return false;  // number_of_ops = 0 (:468-471)
@@ -179,10 +181,15 @@ __device__ __forceinline__ bool ss_store_one(const Grp<G> &g, const agn_ss_cache
             if (g.sub == 0)
                 start = atomicAdd((unsigned long long *)&c.state_ctl[0], (unsigned long long)st_n);
             start = grp_bcast<G>(g, start);
+            if (dl) dl[0] = st_n;
             if (start + st_n > c.state_cap || st_n > AGN_SS_STATE_MAX_PAIRS) {
                 if (g.sub == 0) {
                     c.state_ctl[2] = 1ull;
                     atomicAdd((unsigned long long *)&c.state_ctl[1], (unsigned long long)st_n);
+                }
+                if (dl) {
+                    dl[1] = st_n;
+                    dl[2] = 1;
                 }
                 return false;
             }
@@ -196,6 +203,7 @@ __device__ __forceinline__ bool ss_store_one(const Grp<G> &g, const agn_ss_cache
             uint64_t rel = 0;
             for (uint32_t j = old_kept; j < n; ++j) rel += AGN_SS_STATE_PAIRS(c.value[k * S + j]);
             if (rel) atomicAdd((unsigned long long *)&c.state_ctl[1], (unsigned long long)rel);
+            if (dl) dl[1] = rel;
         }
     }
     if (prepend) {

@@ -37,7 +37,9 @@
 // + 4 (rem_off) + 8 per removed token; plus 12 per live output pair.
 #include <cstdlib>
 
+#include "cache_dev.hpp"
 #include "filter.hpp"
+#include "tags_serve.hpp"
 
 namespace agn {
 namespace {
@@ -206,17 +208,23 @@ struct TagLists {
 // outside U kept at SCT's value and its DC set = SCT's | (U if any op was
 // included).  Any other key goes to the `mix` list, served by the per-entry-
 // mask (SPARSE) kernel in a second launch.
+//
+// SV (the fused set/register read, tags_serve.hpp; fast pass, WARM): the
+// wave runs the snapshot cache's lookup for its request before the pass and
+// the store after it; keys the pass hands on are stored by a later launch.
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, int CAP, int WPB, int RB,
-          bool WARM, bool SLOW, bool CT, bool MSK>
+          bool WARM, bool SLOW, bool CT, bool MSK, bool SV = false>
 __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, agn_result out,
-                                                   TagLists tl, uint32_t xcd) {
+                                                   TagLists tl, uint32_t xcd, TagServe sv) {
     using S = Shape<DPL, LPO>;
     constexpr int OPI = S::OPI;
     static_assert(!CT || (DPL == 4 && FULL && !SPARSE), "CT: dense rows, 4 DCs per lane");
     static_assert(!MSK || (FULL && !SPARSE), "MSK: the dense row scans");
+    static_assert(!SV || (WARM && !SLOW && !SPARSE && DPL * LPO <= 8), "SV: the fast pass, D <= 8");
     constexpr int P = CT ? DPL * LPO / 2 : 1;  // 16-byte parts per op
     constexpr int OPH = AGN_WAVE / P;          // ops per 1 KiB load (OPI / 2)
     __shared__ CandLds<CAP> Lall[WPB];
+    __shared__ uint64_t Sct[WPB][SV ? 9 : 1];  // SV: LastOpCt row + mask word for the store
     const int w = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
     CandLds<CAP> &L = Lall[w];
     const int lane = lane_id();
@@ -230,6 +238,33 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     for (uint64_t it = (uint64_t)blk * WPB + (uint64_t)w; it < n_items; it += nw) {
         const uint64_t i = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(tl.in[it]) : it;
         const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
+        LookupOut lk{};
+        if constexpr (SV) {
+            // get_from_snapshot_cache (materializer_vnode.erl:384-413) on the
+            // whole wave: SCT row (+ mask) and base reference into sv's arrays,
+            // which req.sct / sct_mask / base_value name for the reads below
+            const Grp<AGN_WAVE> g;
+            lk = ss_lookup_one<AGN_WAVE>(g, sv.c, key, req.R + i * D,
+                                         req.R_mask ? req.R_mask + i * W : nullptr, sv.sct + i * D,
+                                         sv.sctm ? sv.sctm + i * W : nullptr);
+            if (lane == 0) {
+                sv.ign[i] = lk.ign;
+                sv.base[i] = lk.base;
+                sv.first[i] = lk.first;
+                sv.status[i] = lk.status;
+                sv.dkeys[i] = key;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // other lanes read the rows
+        }
+        // hand-on / no-store outcomes of SV (lane 0): prune[i] and the deltas
+        auto sv_mark = [&](uint8_t pf) {
+            if (SV && lane == 0) {
+                sv.prune[i] = pf;
+                sv.dprune[i] = 0;
+                sv.delta[2 * i] = 0;
+                sv.delta[2 * i + 1] = 0;
+            }
+        };
         // The key's and the request's side values load together and
         // unconditionally (in-bounds dummies for absent columns): each
         // conditional load was waited for on its own before the next issued.
@@ -239,7 +274,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         const uint32_t kt = __builtin_amdgcn_readfirstlane(
             (uint32_t)(log.key_type ? log.key_type
                                     : reinterpret_cast<const uint8_t *>(log.key_off))[key]);
-        const uint32_t si = __builtin_amdgcn_readfirstlane(
+        const uint32_t si = SV ? (uint32_t)lk.ign : __builtin_amdgcn_readfirstlane(
             (uint32_t)(req.sct_ignore ? req.sct_ignore
                                       : reinterpret_cast<const uint8_t *>(req.R))[i]);
         const uint64_t txv = uniform_u64((req.txid ? req.txid : req.R)[i]);
@@ -249,7 +284,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         const uint64_t *bop = req.base_off ? req.base_off + i
                             : packed        ? reinterpret_cast<const uint64_t *>(req.base_value) + i
                                             : req.R + i;
-        const uint64_t b0v = uniform_u64(bop[0]);
+        const uint64_t b0v = SV ? (uint64_t)lk.base : uniform_u64(bop[0]);
         const uint64_t b1v = uniform_u64((req.base_off ? bop + 1 : bop)[0]);
         const uint64_t n = log.key_len ? lv : lv - off;
 
@@ -266,6 +301,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 out.err_pos[i] = 0xffffffffu;
                 out.out_n[i] = 0;
             }
+            sv_mark(0);  // not stored (materialize_snapshot sees the error)
             continue;
         }
         // MSK: the key's DC set U, R's and SCT's (see above)
@@ -278,6 +314,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 const uint32_t at = atomicAdd(tl.mix_n, 1u);
                 tl.mix[at] = (uint32_t)i;
             }
+            sv_mark(4);
             continue;
         }
 
@@ -572,6 +609,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 const uint32_t at = atomicAdd(tl.ovf_n, 1u);
                 tl.ovf[at] = (uint32_t)i;
             }
+            sv_mark(4);
             continue;
         }
 
@@ -603,8 +641,9 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 const uint32_t d = (uint32_t)(d0 + j);
                 ct[j] = (d < D && ((mU >> (d & 63u)) & 1ull)) ? ct[j] : e[j];
             }
-            if (out.lastct_mask != nullptr && lane == 0)
-                out.lastct_mask[i] = ct_ign ? 0ull : ((sct_ign ? 0ull : mS) | (cnt ? mU : 0ull));
+            const uint64_t ctm = ct_ign ? 0ull : ((sct_ign ? 0ull : mS) | (cnt ? mU : 0ull));
+            if (out.lastct_mask != nullptr && lane == 0) out.lastct_mask[i] = ctm;
+            if (SV && lane == 0) Sct[w][SV ? 8 : 0] = ctm;
         }
         if constexpr (CT) {
 #pragma unroll
@@ -617,6 +656,10 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                 v.x = ct_ign ? 0ull : ctA;
                 v.y = ct_ign ? 0ull : ctB;
                 reinterpret_cast<u64x2 *>(out.lastct + i * D)[lane] = v;
+                if (SV) {
+                    Sct[w][SV ? 2 * lane : 0] = v.x;
+                    Sct[w][SV ? 2 * lane + 1 : 0] = v.y;
+                }
             }
         } else {
 #pragma unroll
@@ -633,6 +676,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                     if (SPARSE) v = (v && !ct_ign) ? v - 1ull : 0ull;
                     else if (ct_ign) v = 0ull;
                     out.lastct[i * D + d] = v;
+                    if (SV) Sct[w][SV ? d : 0] = v;
                 }
             }
         }
@@ -653,13 +697,31 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             }
         }
 
+        // wave-uniform
+        const int64_t hole = first_excl >= 0 ? hid - 1 : hid;  // hid = 0 for n = 0
+        uint32_t fl = 0;
+        if (cnt) fl |= AGN_F_NEWSS;
+        if (ct_ign) fl |= AGN_F_CT_IGNORE;
+        if (first_err >= 0) fl |= AGN_F_ERR_UNEXPECTED;
+        if (cap_err) fl |= AGN_F_ERR_CAPACITY;
+        if constexpr (SV) {
+            // materialize_snapshot's store (:466-509): the state from the LDS
+            // table (sorted, [0, n_live)), LastOpCt from its stash
+            wave_sync();
+            const Grp<AGN_WAVE> g;
+            uint64_t dl[3] = {0ull, 0ull, 0ull};
+            const bool pr = ss_store_one<AGN_WAVE>(
+                g, sv.c, key, n, lk.status, lk.first, sv.gc != nullptr && sv.gc[i] != 0, Sct[w],
+                (MSK && out.lastct_mask != nullptr) ? &Sct[w][SV ? 8 : 0] : nullptr, hole, 0, cnt,
+                fl, sv.thr, sv.thrm, L.tag, L.tok, n_live, dl);
+            if (lane == 0) {
+                sv.prune[i] = (uint8_t)((pr ? 1u : 0u) | (dl[2] ? 2u : 0u));
+                sv.dprune[i] = pr ? 1 : 0;
+                sv.delta[2 * i] = dl[0];
+                sv.delta[2 * i + 1] = dl[1];
+            }
+        }
         if (lane == 0) {
-            const int64_t hole = first_excl >= 0 ? hid - 1 : hid;  // hid = 0 for n = 0
-            uint32_t fl = 0;
-            if (cnt) fl |= AGN_F_NEWSS;
-            if (ct_ign) fl |= AGN_F_CT_IGNORE;
-            if (first_err >= 0) fl |= AGN_F_ERR_UNEXPECTED;
-            if (cap_err) fl |= AGN_F_ERR_CAPACITY;
             out.hole[i] = hole;
             out.count[i] = cnt;
             out.flags[i] = fl;
@@ -680,7 +742,7 @@ constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 1, RBATCH = 2;
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool SET, bool WARM, bool CT, bool MSK>
 hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result &out,
                        const uint32_t *in, const uint32_t *in_n, uint32_t *ovf, uint32_t *ovf_n,
-                       uint32_t *mix, uint32_t *mix_n, hipStream_t st) {
+                       uint32_t *mix, uint32_t *mix_n, hipStream_t st, bool run_fast = true) {
     // one wave per key: the grid is the batch (the wave dispatcher then
     // overlaps keys; AGN_TAGS_GRID=<blocks> caps it for A/B); a list pass
     // grid-strides over a resident grid
@@ -688,12 +750,14 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
     const unsigned cap = in ? 8192u : ge ? (unsigned)atoi(ge) : 0x7fffffffu;
     const unsigned blocks = grid_for(req.n_req, FAST_WPB, cap);
     TagLists fast{in, in_n, ovf, ovf_n, mix, mix_n};
-    hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, WARM, false,
-                               CT, MSK>),
-                       dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, fast,
-                       xcd_remap() ? 1u : 0u);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (run_fast) {  // (false: the fused read ran it, tags_serve.hpp)
+        hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, WARM,
+                                   false, CT, MSK>),
+                           dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, fast,
+                           xcd_remap() ? 1u : 0u, TagServe{});
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     // the overflow pass grid-strides over a list of at most n_req keys: a
     // resident grid of up to 256 one-wave blocks (112 KB of LDS each), no
     // more than the batch -- a serving batch of ~10 reads must not occupy
@@ -703,7 +767,7 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
     const unsigned sblocks = (unsigned)(req.n_req < 256u ? (req.n_req ? req.n_req : 1u) : 256u);
     hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, SLOW_CAP, 1, RBATCH, WARM, true, CT,
                                MSK>),
-                       dim3(sblocks), dim3(64), 0, st, log, req, out, slow, 0u);
+                       dim3(sblocks), dim3(64), 0, st, log, req, out, slow, 0u, TagServe{});
     return hipGetLastError();
 }
 
@@ -838,7 +902,108 @@ int dispatch_masked(const agn_log &log, const agn_read &req, const agn_result &o
     return AGN_ENOTSUP;
 }
 
+// The fused set/register read (tags_serve.hpp): the SV fast pass over the
+// batch; _rest: the passes and the store for the keys it handed on.
+template <int D, bool SET, bool MSK, bool CT>
+int serve_fast(const agn_log &log, const agn_read &req, const agn_result &out, const TagServe &sv,
+               uint32_t *scr, hipStream_t st) {
+    TagScratch w;
+    w.base = scr;
+    w.n = req.n_req;
+    const TagLists fast{nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n()};
+    hipLaunchKernelGGL((k_tags<D, 1, false, true, SET, FAST_CAP, FAST_WPB, RBATCH, true, false, CT,
+                               MSK, true>),
+                       dim3(grid_for(req.n_req, FAST_WPB, 0x7fffffffu)), dim3(64 * FAST_WPB), 0, st,
+                       log, req, out, fast, 0u, sv);
+    AGN_HIP(hipGetLastError());
+    return AGN_OK;
+}
+
+template <int D, bool SET, bool MSK, bool CT>
+int serve_rest(const agn_log &log, const agn_read &req, const agn_result &out, const TagServe &sv,
+               uint32_t *scr, hipStream_t st) {
+    TagScratch w;
+    w.base = scr;
+    w.n = req.n_req;
+    hipError_t e = tags_passes<D, 1, false, true, SET, true, CT, MSK>(
+        log, req, out, nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n(), st, false);
+    if (MSK && e == hipSuccess)
+        e = tags_passes<D, 1, true, false, SET, true, false, false>(
+            log, req, out, w.mix(), w.mix_n(), w.ovf2(), w.ovf2_n(), nullptr, nullptr, st);
+    if (e != hipSuccess) return fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
+    // the store for both lists (the mixed keys' overflow list is part of mix)
+    for (int l = 0; l < (MSK ? 2 : 1); ++l) {
+        const int rc = launch_ss_store_list(
+            sv.c, log.key_off, log.key_len, req.n_req, l ? w.mix() : w.ovf(), l ? w.mix_n() : w.ovf_n(),
+            sv.dkeys, sv.first, sv.status, sv.gc, out, sv.dprune, sv.thr, sv.thrm, st);
+        if (rc) return rc;
+    }
+    AGN_HIP(hipMemsetAsync(scr, 0, 4 * sizeof(uint32_t), st));
+    return AGN_OK;
+}
+
+template <bool REST, bool SET>
+int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &out,
+                   const TagServe &sv, uint32_t *scr, bool msk, hipStream_t st) {
+#define AGN_S(D, MSKV, CTV)                                                        \
+    return REST ? serve_rest<D, SET, MSKV, CTV>(log, req, out, sv, scr, st)         \
+                : serve_fast<D, SET, MSKV, CTV>(log, req, out, sv, scr, st)
+    if (msk) {
+        switch (log.n_dcs) {
+            case 2: AGN_S(2, true, false);
+            case 4: AGN_S(4, true, false);
+            case 6: AGN_S(6, true, false);
+            case 8: AGN_S(8, true, false);
+            default: break;
+        }
+    } else {
+        switch (log.n_dcs) {
+            case 2: AGN_S(2, false, false);
+            case 4: AGN_S(4, false, true);
+            case 6: AGN_S(6, false, false);
+            case 8: AGN_S(8, false, false);
+            default: break;
+        }
+    }
+#undef AGN_S
+    return AGN_ENOTSUP;
+}
+
 }  // namespace
+
+// D = 2, 4, 6, 8; dense rows (D = 4: the CT form, so not with AGN_TAGS_CT=0)
+// or the MSK form (not with AGN_TAGS_MSK=0)
+bool tags_serve_supported(const agn_log &log, bool sparse) {
+    const uint32_t D = log.n_dcs;
+    if (!(D == 2 || D == 4 || D == 6 || D == 8)) return false;
+    if (sparse) {
+        const char *v = getenv("AGN_TAGS_MSK");
+        return !(v && v[0] == '0');
+    }
+    return D != 4 || tags_ct();
+}
+
+static bool serve_masked(const agn_log &log, const agn_read &req, const agn_result &out) {
+    return log.oc_mask || req.R_mask || req.sct_mask || out.lastct_mask;
+}
+
+int launch_tags_serve(const agn_log &log, const agn_read &req, const agn_result &out,
+                      const TagServe &sv, uint32_t *scr, hipStream_t st) {
+    if (req.n_req == 0) return AGN_OK;
+    const bool msk = serve_masked(log, req, out);
+    if (!tags_serve_supported(log, msk)) return AGN_ENOTSUP;
+    return log.crdt_type == AGN_SET_AW ? serve_dispatch<false, true>(log, req, out, sv, scr, msk, st)
+                                       : serve_dispatch<false, false>(log, req, out, sv, scr, msk, st);
+}
+
+int launch_tags_serve_rest(const agn_log &log, const agn_read &req, const agn_result &out,
+                           const TagServe &sv, uint32_t *scr, hipStream_t st) {
+    if (req.n_req == 0) return AGN_OK;
+    const bool msk = serve_masked(log, req, out);
+    if (!tags_serve_supported(log, msk)) return AGN_ENOTSUP;
+    return log.crdt_type == AGN_SET_AW ? serve_dispatch<true, true>(log, req, out, sv, scr, msk, st)
+                                       : serve_dispatch<true, false>(log, req, out, sv, scr, msk, st);
+}
 
 int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
                 hipStream_t st) {

@@ -100,8 +100,8 @@ def fmt_keys(n):
 KERNEL_SOURCES = {   # the sources the dominant kernel of each config is built from
     1: ("mat_counter_dense.hip", "counter_scan.hpp", "filter.hpp", "common.hpp"),
     2: ("mat_counter_dense.hip", "counter_scan.hpp", "filter.hpp", "common.hpp"),
-    3: ("mat_tags.hip", "filter.hpp", "common.hpp"),
-    4: ("mat_tags.hip", "filter.hpp", "common.hpp"),
+    3: ("mat_tags.hip", "cache_dev.hpp", "filter.hpp", "tags_serve.hpp", "common.hpp"),
+    4: ("mat_tags.hip", "cache_dev.hpp", "filter.hpp", "tags_serve.hpp", "common.hpp"),
     5: ("gst.hip", "common.hpp"),
     "gc": ("gc.hip", "filter.hpp", "serve.hpp", "common.hpp"),
 }

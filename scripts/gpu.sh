@@ -90,6 +90,17 @@ expand() {
       echo "serve8set|150|./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000 sparse=1"
       echo "serve8reg|150|./tools/serve_bench type=register parts=8 threads=20 reads=5000 wps=2000 sparse=1"
       echo "serve8seth|150|./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000 hot=2000 sparse=1";;
+    servetags)
+      # set_aw / register_mv serving: the fused read (default) against the
+      # kernel sequence (AGN_READ6=0), interleaved, dense and masked logs
+      for r in 1 0; do
+        echo "st1d_r$r|150|env AGN_READ6=$r ./tools/serve_bench type=set parts=1 threads=20 reads=20000"
+        echo "st1s_r$r|150|env AGN_READ6=$r ./tools/serve_bench type=set parts=1 threads=20 reads=20000 sparse=1"
+        echo "st8d_r$r|150|env AGN_READ6=$r ./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000"
+        echo "st8s_r$r|150|env AGN_READ6=$r ./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000 sparse=1"
+        echo "rg8s_r$r|150|env AGN_READ6=$r ./tools/serve_bench type=register parts=8 threads=20 reads=5000 wps=2000 sparse=1"
+        echo "st8sh_r$r|150|env AGN_READ6=$r ./tools/serve_bench type=set parts=8 threads=20 reads=5000 wps=2000 hot=2000 sparse=1"
+      done;;
     *) echo "$1";;
   esac
 }

@@ -11,7 +11,11 @@ appends the result's state.  Checked against the reference's transcription
 resize) read for read:
 
   * the cached read batcher (the NIF's read/4 on a Cached partition), with
-    update/2's GC reads, dense and presence-masked logs;
+    update/2's GC reads, dense and presence-masked logs; for D = 2, 4, 6, 8
+    the batch is the fused read (lookup -> fast tags pass -> store in one
+    kernel, tags_serve.hpp), with its hand-on path for states past the fast
+    table and for keys whose entries carry different DC sets; AGN_READ6=0
+    runs the kernel sequence on the same workload;
   * agn_read_cached over device arrays, rounds of whole-partition batches,
     with the GC applied and the arena re-packed (agn_ss_state_compact).
 """
@@ -30,8 +34,8 @@ D = 3
 PTYPE = {_abi.SET_AW: po.SET_AW, _abi.REGISTER_MV: po.REGISTER_MV}
 
 
-def vc(row):
-    return {d: int(row[d]) for d in range(D)}
+def vc(row, mask=None):
+    return {d: int(row[d]) for d in range(len(row)) if mask is None or (mask >> d) & 1}
 
 
 class TagWorkload:
@@ -40,14 +44,15 @@ class TagWorkload:
     remove = {Elem, [], observed}; register_mv assign = {V, new token, all
     observed}, reset = {reset, all observed} (observed = the writer's view)."""
 
-    def __init__(self, seed, K, typ):
+    def __init__(self, seed, K, typ, d=D):
         self.rng = np.random.default_rng(seed)
-        self.K, self.typ = K, typ
-        self.clk = np.full(D, 1000, np.int64)
+        self.K, self.typ, self.D = K, typ, d
+        self.clk = np.full(d, 1000, np.int64)
         self.live = [dict() for _ in range(K)]   # key -> elem -> [tok]
         self.tok = 1
 
     def op(self, key):
+        D = self.D
         c = int(self.rng.integers(0, D))
         ss = np.maximum(self.clk - self.rng.integers(0, 40, D), 0)
         self.clk[c] += int(self.rng.integers(1, 30))
@@ -79,7 +84,7 @@ class TagWorkload:
         return c, ss, int(self.clk[c]), oc, eff, entry
 
     def read_clock(self, lag=400):
-        return np.maximum(self.clk - self.rng.integers(0, lag, D), 0)
+        return np.maximum(self.clk - self.rng.integers(0, lag, self.D), 0)
 
 
 def state_of(typ, tags, toks):
@@ -98,7 +103,7 @@ def state_of(typ, tags, toks):
 
 def append_entry(ol, key, oc, entry, txid, mask=None):
     tag, add, rems = entry
-    ol.append(np.array([key], np.uint64), oc.reshape(1, D).astype(np.uint64),
+    ol.append(np.array([key], np.uint64), oc.reshape(1, len(oc)).astype(np.uint64),
               oc_mask=None if mask is None else np.array([[mask]], np.uint64),
               tag=np.array([tag], np.uint32), add_tok=np.array([add], np.uint64),
               rem_off=np.array([0, len(rems)], np.uint32),
@@ -111,31 +116,45 @@ def placeholder(vn, key):
     return tup is not None and any(tup[po.FIRST_OP - 1 + i] == 0 for i in range(tup[1][0]))
 
 
-@pytest.mark.parametrize("sparse", [False, True])
+# (D, log): "dense", "sparse" (every entry carries all D DCs), "mixed" (each
+# entry a random DC subset holding its own DC: keys not uniform, the fused
+# read hands them on); read6: the fused batch ("1") or the kernel sequence
+BATCHER_CASES = [(3, "dense", "1"), (3, "sparse", "1")] + [
+    (d, lg, r6) for d in (4, 8) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
+] + [(2, "sparse", "1"), (6, "dense", "1")]
+
+
+@pytest.mark.parametrize("d,logk,read6", BATCHER_CASES)
 @pytest.mark.parametrize("typ", [_abi.SET_AW, _abi.REGISTER_MV])
-def test_batcher_states_vs_reference(eng, typ, sparse):
+def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
     """update/2 (+ its GC read) and read/6 through a cached set/register
     partition: every served state equals the reference's, and the ETS list
     sizes follow it slot for slot."""
+    monkeypatch.setenv("AGN_READ6", read6)
+    sparse, mixed = logk != "dense", logk == "mixed"
     K, steps = 16, 2500
-    w = TagWorkload(31 + typ, K, typ)
+    w = TagWorkload(31 + typ + 7 * d, K, typ, d)
     vn = po.MaterializerVnode()
     quirk, served, log_reads = set(), 0, 0
-    full = np.uint64((1 << D) - 1)
+    full = np.uint64((1 << d) - 1)
     rm = np.array([full]) if sparse else None
-    with OpLog(eng, typ, D, K, sparse=sparse) as ol, \
+    with OpLog(eng, typ, d, K, sparse=sparse) as ol, \
             Batcher(ol, max_batch=8, cached=True) as bt:
         for s in range(steps):
             key = int(w.rng.integers(0, K))
             if w.rng.random() < 0.7:
                 c, ss, ct, oc, eff, entry = w.op(key)
+                mask = None
+                if mixed:  # a random DC set with the op's own DC
+                    mask = int(w.rng.integers(0, 1 << d)) | (1 << c)
                 try:
-                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss), (c, ct), s + 1))
+                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss, mask), (c, ct), s + 1))
                 except (po.BadMatch, TypeError, ValueError):
                     quirk.add(key)
                 if ol.gc_due(key)[0]:
                     bt.read(key, R=ss.astype(np.uint64), R_mask=rm, gc=True, out_cap=4096)
-                append_entry(ol, key, oc, entry, s + 1, full if sparse else None)
+                append_entry(ol, key, oc, entry, s + 1,
+                             (np.uint64(mask) if mixed else full) if sparse else None)
                 if placeholder(vn, key):
                     quirk.add(key)
             else:
@@ -168,19 +187,22 @@ def test_batcher_states_vs_reference(eng, typ, sparse):
         assert (int(ln[k]), int(ll[k])) == (length, list_len), k
 
 
-def test_batcher_state_bound_grows(eng):
+@pytest.mark.parametrize("d,read6", [(3, "1"), (4, "1"), (8, "1"), (8, "0")])
+def test_batcher_state_bound_grows(eng, d, read6, monkeypatch):
     """A key whose state outgrows the caller's buffer: the read reports
     AGN_ECAPACITY, a second read with room for the state is served (the NIF's
-    retry) from the snapshot the first one stored."""
+    retry) from the snapshot the first one stored.  300 live pairs: past the
+    fast table, so the fused read (D = 4, 8) hands the key on."""
     from antidote_amd._lib import EngineError
+    monkeypatch.setenv("AGN_READ6", read6)
     K = 2
-    with OpLog(eng, _abi.SET_AW, D, K) as ol, Batcher(ol, max_batch=4, cached=True) as bt:
+    with OpLog(eng, _abi.SET_AW, d, K) as ol, Batcher(ol, max_batch=4, cached=True) as bt:
         n = 300
-        oc = np.tile(np.arange(1, n + 1, dtype=np.uint64)[:, None], (1, D))
+        oc = np.tile(np.arange(1, n + 1, dtype=np.uint64)[:, None], (1, d))
         ol.append(np.zeros(n, np.uint64), oc, tag=np.arange(n, dtype=np.uint32),
                   add_tok=np.arange(1, n + 1, dtype=np.uint64),
                   rem_off=np.zeros(n + 1, np.uint32), rem_tok=np.zeros(1, np.uint64))
-        R = np.full(D, n, np.uint64)
+        R = np.full(d, n, np.uint64)
         with pytest.raises(EngineError):
             bt.read(0, R=R, out_cap=10)
         g = bt.read(0, R=R, out_cap=n)
