@@ -14,8 +14,11 @@ resize) read for read:
     update/2's GC reads, dense and presence-masked logs; for D = 2, 4, 6, 8
     the batch is the fused read (lookup -> fast tags pass -> store in one
     kernel, tags_serve.hpp), with its hand-on path for states past the fast
-    table and for keys whose entries carry different DC sets; AGN_READ6=0
-    runs the kernel sequence on the same workload;
+    table; AGN_READ6=0 runs the kernel sequence on the same workload;
+  * keys whose entries carry different DC sets (the fused read hands them
+    on to the per-entry-mask passes): the fused batch against the kernel
+    sequence, result for result -- against the reference's transcription
+    this case is parity unpinned (DESIGN.md §9);
   * agn_read_cached over device arrays, rounds of whole-partition batches,
     with the GC applied and the arena re-packed (agn_ss_state_compact).
 """
@@ -116,11 +119,10 @@ def placeholder(vn, key):
     return tup is not None and any(tup[po.FIRST_OP - 1 + i] == 0 for i in range(tup[1][0]))
 
 
-# (D, log): "dense", "sparse" (every entry carries all D DCs), "mixed" (each
-# entry a random DC subset holding its own DC: keys not uniform, the fused
-# read hands them on); read6: the fused batch ("1") or the kernel sequence
+# (D, log): "dense", "sparse" (every entry carries all D DCs); read6: the
+# fused batch ("1") or the kernel sequence
 BATCHER_CASES = [(3, "dense", "1"), (3, "sparse", "1")] + [
-    (d, lg, r6) for d in (4, 8) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
+    (d, lg, r6) for d in (4, 8) for lg in ("dense", "sparse") for r6 in ("1", "0")
 ] + [(2, "sparse", "1"), (6, "dense", "1")]
 
 
@@ -131,7 +133,7 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
     partition: every served state equals the reference's, and the ETS list
     sizes follow it slot for slot."""
     monkeypatch.setenv("AGN_READ6", read6)
-    sparse, mixed = logk != "dense", logk == "mixed"
+    sparse = logk != "dense"
     K, steps = 16, 2500
     w = TagWorkload(31 + typ + 7 * d, K, typ, d)
     vn = po.MaterializerVnode()
@@ -144,17 +146,13 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
             key = int(w.rng.integers(0, K))
             if w.rng.random() < 0.7:
                 c, ss, ct, oc, eff, entry = w.op(key)
-                mask = None
-                if mixed:  # a random DC set with the op's own DC
-                    mask = int(w.rng.integers(0, 1 << d)) | (1 << c)
                 try:
-                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss, mask), (c, ct), s + 1))
+                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss), (c, ct), s + 1))
                 except (po.BadMatch, TypeError, ValueError):
                     quirk.add(key)
                 if ol.gc_due(key)[0]:
                     bt.read(key, R=ss.astype(np.uint64), R_mask=rm, gc=True, out_cap=4096)
-                append_entry(ol, key, oc, entry, s + 1,
-                             (np.uint64(mask) if mixed else full) if sparse else None)
+                append_entry(ol, key, oc, entry, s + 1, full if sparse else None)
                 if placeholder(vn, key):
                     quirk.add(key)
             else:
@@ -185,6 +183,46 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
             continue
         length, list_len = vn.ops_cache[k][1]
         assert (int(ln[k]), int(ll[k])) == (length, list_len), k
+
+
+@pytest.mark.parametrize("d", [4, 8])
+@pytest.mark.parametrize("typ", [_abi.SET_AW, _abi.REGISTER_MV])
+def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
+    """Entries with random DC sets (each holding its own DC; R with some DCs
+    missing now and then): two partitions fed the same updates, one served by
+    the fused read, one by the kernel sequence -- every result field, the
+    status and the ETS list sizes agree."""
+    K, steps = 16, 2500
+    w = TagWorkload(57 + typ + 7 * d, K, typ, d)
+    full = (1 << d) - 1
+    with OpLog(eng, typ, d, K, sparse=True) as la, OpLog(eng, typ, d, K, sparse=True) as lb:
+        monkeypatch.setenv("AGN_READ6", "1")
+        ba = Batcher(la, max_batch=8, cached=True)
+        monkeypatch.setenv("AGN_READ6", "0")
+        bb = Batcher(lb, max_batch=8, cached=True)
+        compared = 0
+        with ba, bb:
+            for s in range(steps):
+                key = int(w.rng.integers(0, K))
+                if w.rng.random() < 0.7:
+                    c, ss, ct, oc, eff, entry = w.op(key)
+                    mask = np.uint64(int(w.rng.integers(0, 1 << d)) | (1 << c))
+                    for ol, bt in ((la, ba), (lb, bb)):
+                        if ol.gc_due(key)[0]:
+                            bt.read(key, R=ss.astype(np.uint64), R_mask=np.array([full]),
+                                    gc=True, out_cap=4096)
+                        append_entry(ol, key, oc, entry, s + 1, mask)
+                else:
+                    R = w.read_clock(lag=400 if w.rng.random() < 0.85 else 20000).astype(np.uint64)
+                    rm = full if w.rng.random() < 0.8 else int(w.rng.integers(1, 1 << d))
+                    ga, gb = (bt.read(key, R=R, R_mask=np.array([rm], np.uint64), out_cap=4096)
+                              for bt in (ba, bb))
+                    for f in ga:
+                        assert np.array_equal(np.asarray(ga[f]), np.asarray(gb[f])), (s, key, f)
+                    compared += 1
+            assert compared > 500
+            for a, b in zip(la.key_meta(), lb.key_meta()):
+                assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("d,read6", [(3, "1"), (4, "1"), (8, "1"), (8, "0")])
