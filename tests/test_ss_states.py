@@ -16,9 +16,9 @@ resize) read for read:
     kernel, tags_serve.hpp), with its hand-on path for states past the fast
     table; AGN_READ6=0 runs the kernel sequence on the same workload;
   * keys whose entries carry different DC sets (the fused read hands them
-    on to the per-entry-mask passes): the fused batch against the kernel
-    sequence, result for result -- against the reference's transcription
-    this case is parity unpinned (DESIGN.md §9);
+    on to the per-entry-mask passes): against the transcription (the GC read
+    at the op's own snapshot dict, as op_insert_gc reads), and the fused
+    batch against the kernel sequence, result for result;
   * agn_read_cached over device arrays, rounds of whole-partition batches,
     with the GC applied and the arena re-packed (agn_ss_state_compact).
 """
@@ -119,10 +119,11 @@ def placeholder(vn, key):
     return tup is not None and any(tup[po.FIRST_OP - 1 + i] == 0 for i in range(tup[1][0]))
 
 
-# (D, log): "dense", "sparse" (every entry carries all D DCs); read6: the
-# fused batch ("1") or the kernel sequence
+# (D, log): "dense", "sparse" (every entry carries all D DCs), "mixed" (each
+# entry a random DC subset holding its own DC: keys not uniform, the fused
+# read hands them on); read6: the fused batch ("1") or the kernel sequence
 BATCHER_CASES = [(3, "dense", "1"), (3, "sparse", "1")] + [
-    (d, lg, r6) for d in (4, 8) for lg in ("dense", "sparse") for r6 in ("1", "0")
+    (d, lg, r6) for d in (4, 8) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
 ] + [(2, "sparse", "1"), (6, "dense", "1")]
 
 
@@ -133,7 +134,7 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
     partition: every served state equals the reference's, and the ETS list
     sizes follow it slot for slot."""
     monkeypatch.setenv("AGN_READ6", read6)
-    sparse = logk != "dense"
+    sparse, mixed = logk != "dense", logk == "mixed"
     K, steps = 16, 2500
     w = TagWorkload(31 + typ + 7 * d, K, typ, d)
     vn = po.MaterializerVnode()
@@ -146,13 +147,18 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
             key = int(w.rng.integers(0, K))
             if w.rng.random() < 0.7:
                 c, ss, ct, oc, eff, entry = w.op(key)
+                mask = full
+                if mixed:  # a random DC set with the op's own DC
+                    mask = np.uint64(int(w.rng.integers(0, 1 << d)) | (1 << c))
                 try:
-                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss), (c, ct), s + 1))
+                    vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss, int(mask)), (c, ct),
+                                              s + 1))
                 except (po.BadMatch, TypeError, ValueError):
                     quirk.add(key)
-                if ol.gc_due(key)[0]:
-                    bt.read(key, R=ss.astype(np.uint64), R_mask=rm, gc=True, out_cap=4096)
-                append_entry(ol, key, oc, entry, s + 1, full if sparse else None)
+                if ol.gc_due(key)[0]:  # op_insert_gc reads at the op's snapshot dict
+                    bt.read(key, R=ss.astype(np.uint64), R_mask=np.array([mask]) if sparse else None,
+                            gc=True, out_cap=4096)
+                append_entry(ol, key, oc, entry, s + 1, mask if sparse else None)
                 if placeholder(vn, key):
                     quirk.add(key)
             else:
@@ -209,7 +215,7 @@ def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
                     mask = np.uint64(int(w.rng.integers(0, 1 << d)) | (1 << c))
                     for ol, bt in ((la, ba), (lb, bb)):
                         if ol.gc_due(key)[0]:
-                            bt.read(key, R=ss.astype(np.uint64), R_mask=np.array([full]),
+                            bt.read(key, R=ss.astype(np.uint64), R_mask=np.array([mask]),
                                     gc=True, out_cap=4096)
                         append_entry(ol, key, oc, entry, s + 1, mask)
                 else:
