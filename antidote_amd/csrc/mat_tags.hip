@@ -220,7 +220,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     constexpr int OPI = S::OPI;
     static_assert(!CT || (DPL == 4 && FULL && !SPARSE), "CT: dense rows, 4 DCs per lane");
     static_assert(!MSK || (FULL && !SPARSE), "MSK: the dense row scans");
-    static_assert(!SV || (WARM && !SLOW && !SPARSE && DPL * LPO <= 8), "SV: the fast pass, D <= 8");
+    static_assert(!SV || (WARM && !SLOW && DPL * LPO <= 8), "SV: the fast pass, D <= 8");
     constexpr int P = CT ? DPL * LPO / 2 : 1;  // 16-byte parts per op
     constexpr int OPH = AGN_WAVE / P;          // ops per 1 KiB load (OPI / 2)
     __shared__ CandLds<CAP> Lall[WPB];
@@ -694,6 +694,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 #pragma unroll
                 for (int x = 1; x < AGN_WAVE; x <<= 1) v |= shfl_xor_u64(v, x);
                 if (lane == 0) out.lastct_mask[i * W + wd] = v;
+                if (SV && lane == 0 && wd == 0) Sct[w][SV ? 8 : 0] = v;
             }
         }
 
@@ -712,7 +713,8 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             uint64_t dl[3] = {0ull, 0ull, 0ull};
             const bool pr = ss_store_one<AGN_WAVE>(
                 g, sv.c, key, n, lk.status, lk.first, sv.gc != nullptr && sv.gc[i] != 0, Sct[w],
-                (MSK && out.lastct_mask != nullptr) ? &Sct[w][SV ? 8 : 0] : nullptr, hole, 0, cnt,
+                ((MSK || SPARSE) && out.lastct_mask != nullptr) ? &Sct[w][SV ? 8 : 0] : nullptr,
+                hole, 0, cnt,
                 fl, sv.thr, sv.thrm, L.tag, L.tok, n_live, dl);
             if (lane == 0) {
                 sv.prune[i] = (uint8_t)((pr ? 1u : 0u) | (dl[2] ? 2u : 0u));
@@ -904,14 +906,17 @@ int dispatch_masked(const agn_log &log, const agn_read &req, const agn_result &o
 
 // The fused set/register read (tags_serve.hpp): the SV fast pass over the
 // batch; _rest: the passes and the store for the keys it handed on.
-template <int D, bool SET, bool MSK, bool CT>
+// Shapes (as launch_tags picks them for D <= 8): FULL dense rows (even D;
+// D = 4 the CT form), the MSK form (masked, even D), non-FULL dense rows or
+// the per-entry-mask (SPARSE) form for odd D.
+template <int D, bool SET, bool SPARSE, bool FULL, bool MSK, bool CT>
 int serve_fast(const agn_log &log, const agn_read &req, const agn_result &out, const TagServe &sv,
                uint32_t *scr, hipStream_t st) {
     TagScratch w;
     w.base = scr;
     w.n = req.n_req;
     const TagLists fast{nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n()};
-    hipLaunchKernelGGL((k_tags<D, 1, false, true, SET, FAST_CAP, FAST_WPB, RBATCH, true, false, CT,
+    hipLaunchKernelGGL((k_tags<D, 1, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, true, false, CT,
                                MSK, true>),
                        dim3(grid_for(req.n_req, FAST_WPB, 0x7fffffffu)), dim3(64 * FAST_WPB), 0, st,
                        log, req, out, fast, 0u, sv);
@@ -919,13 +924,13 @@ int serve_fast(const agn_log &log, const agn_read &req, const agn_result &out, c
     return AGN_OK;
 }
 
-template <int D, bool SET, bool MSK, bool CT>
+template <int D, bool SET, bool SPARSE, bool FULL, bool MSK, bool CT>
 int serve_rest(const agn_log &log, const agn_read &req, const agn_result &out, const TagServe &sv,
                uint32_t *scr, hipStream_t st) {
     TagScratch w;
     w.base = scr;
     w.n = req.n_req;
-    hipError_t e = tags_passes<D, 1, false, true, SET, true, CT, MSK>(
+    hipError_t e = tags_passes<D, 1, SPARSE, FULL, SET, true, CT, MSK>(
         log, req, out, nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n(), st, false);
     if (MSK && e == hipSuccess)
         e = tags_passes<D, 1, true, false, SET, true, false, false>(
@@ -945,23 +950,31 @@ int serve_rest(const agn_log &log, const agn_read &req, const agn_result &out, c
 template <bool REST, bool SET>
 int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &out,
                    const TagServe &sv, uint32_t *scr, bool msk, hipStream_t st) {
-#define AGN_S(D, MSKV, CTV)                                                        \
-    return REST ? serve_rest<D, SET, MSKV, CTV>(log, req, out, sv, scr, st)         \
-                : serve_fast<D, SET, MSKV, CTV>(log, req, out, sv, scr, st)
+#define AGN_S(D, SPV, FULLV, MSKV, CTV)                                                    \
+    return REST ? serve_rest<D, SET, SPV, FULLV, MSKV, CTV>(log, req, out, sv, scr, st)     \
+                : serve_fast<D, SET, SPV, FULLV, MSKV, CTV>(log, req, out, sv, scr, st)
     if (msk) {
         switch (log.n_dcs) {
-            case 2: AGN_S(2, true, false);
-            case 4: AGN_S(4, true, false);
-            case 6: AGN_S(6, true, false);
-            case 8: AGN_S(8, true, false);
+            case 1: AGN_S(1, true, false, false, false);
+            case 2: AGN_S(2, false, true, true, false);
+            case 3: AGN_S(3, true, false, false, false);
+            case 4: AGN_S(4, false, true, true, false);
+            case 5: AGN_S(5, true, false, false, false);
+            case 6: AGN_S(6, false, true, true, false);
+            case 7: AGN_S(7, true, false, false, false);
+            case 8: AGN_S(8, false, true, true, false);
             default: break;
         }
     } else {
         switch (log.n_dcs) {
-            case 2: AGN_S(2, false, false);
-            case 4: AGN_S(4, false, true);
-            case 6: AGN_S(6, false, false);
-            case 8: AGN_S(8, false, false);
+            case 1: AGN_S(1, false, false, false, false);
+            case 2: AGN_S(2, false, true, false, false);
+            case 3: AGN_S(3, false, false, false, false);
+            case 4: AGN_S(4, false, true, false, true);
+            case 5: AGN_S(5, false, false, false, false);
+            case 6: AGN_S(6, false, true, false, false);
+            case 7: AGN_S(7, false, false, false, false);
+            case 8: AGN_S(8, false, true, false, false);
             default: break;
         }
     }
@@ -971,11 +984,13 @@ int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &ou
 
 }  // namespace
 
-// D = 2, 4, 6, 8; dense rows (D = 4: the CT form, so not with AGN_TAGS_CT=0)
-// or the MSK form (not with AGN_TAGS_MSK=0)
+// D <= 8 in the shape launch_tags picks: even D with the MSK form for masked
+// logs (not with AGN_TAGS_MSK=0) and, dense, D = 4 in the CT form (not with
+// AGN_TAGS_CT=0); odd D with the per-entry-mask or non-FULL dense rows
 bool tags_serve_supported(const agn_log &log, bool sparse) {
     const uint32_t D = log.n_dcs;
-    if (!(D == 2 || D == 4 || D == 6 || D == 8)) return false;
+    if (D == 0 || D > 8) return false;
+    if (D % 2) return true;
     if (sparse) {
         const char *v = getenv("AGN_TAGS_MSK");
         return !(v && v[0] == '0');

@@ -11,7 +11,7 @@ appends the result's state.  Checked against the reference's transcription
 resize) read for read:
 
   * the cached read batcher (the NIF's read/4 on a Cached partition), with
-    update/2's GC reads, dense and presence-masked logs; for D = 2, 4, 6, 8
+    update/2's GC reads, dense and presence-masked logs; for D <= 8
     the batch is the fused read (lookup -> fast tags pass -> store in one
     kernel, tags_serve.hpp), with its hand-on path for states past the fast
     table; AGN_READ6=0 runs the kernel sequence on the same workload;
@@ -122,9 +122,10 @@ def placeholder(vn, key):
 # (D, log): "dense", "sparse" (every entry carries all D DCs), "mixed" (each
 # entry a random DC subset holding its own DC: keys not uniform, the fused
 # read hands them on); read6: the fused batch ("1") or the kernel sequence
-BATCHER_CASES = [(3, "dense", "1"), (3, "sparse", "1")] + [
-    (d, lg, r6) for d in (4, 8) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
-] + [(2, "sparse", "1"), (6, "dense", "1")]
+BATCHER_CASES = [
+    (d, lg, r6) for d in (3, 4, 8) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
+] + [(1, "sparse", "1"), (2, "sparse", "1"), (5, "sparse", "1"), (6, "dense", "1"),
+     (7, "dense", "1"), (7, "mixed", "1")]
 
 
 @pytest.mark.parametrize("d,logk,read6", BATCHER_CASES)
@@ -196,7 +197,7 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
         assert (int(ln[k]), int(ll[k])) == (length, list_len), k
 
 
-@pytest.mark.parametrize("d", [4, 8])
+@pytest.mark.parametrize("d", [3, 4, 8])
 @pytest.mark.parametrize("typ", [_abi.SET_AW, _abi.REGISTER_MV])
 def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
     """Entries with random DC sets (each holding its own DC; R with some DCs
@@ -236,12 +237,12 @@ def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
                 assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("d,read6", [(3, "1"), (4, "1"), (8, "1"), (8, "0")])
+@pytest.mark.parametrize("d,read6", [(3, "1"), (3, "0"), (4, "1"), (8, "1"), (8, "0")])
 def test_batcher_state_bound_grows(eng, d, read6, monkeypatch):
     """A key whose state outgrows the caller's buffer: the read reports
     AGN_ECAPACITY, a second read with room for the state is served (the NIF's
     retry) from the snapshot the first one stored.  300 live pairs: past the
-    fast table, so the fused read (D = 4, 8) hands the key on."""
+    fast table, so the fused read hands the key on."""
     from antidote_amd._lib import EngineError
     monkeypatch.setenv("AGN_READ6", read6)
     K = 2
