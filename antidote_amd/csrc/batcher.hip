@@ -258,7 +258,7 @@ int ensure_state_room(agn_batcher *B, uint64_t need) {
     return AGN_OK;
 }
 
-// Cached mode, set_aw / register_mv with D = 2, 4, 6, 8: the fused read
+// Cached mode, set_aw / register_mv with D <= 8: the fused read
 // (tags_serve.hpp) -- one kernel per batch reading the requests from, and
 // writing the results to, the pinned block (lookup -> fast tags pass ->
 // store, per request on one wave).  The host keeps its copy of state_ctl

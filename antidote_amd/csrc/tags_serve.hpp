@@ -30,7 +30,7 @@ struct TagServe {
     uint64_t *thr, *thrm;  // GC thresholds [K][D], [K][W]
 };
 
-// Fused shapes: D = 2, 4, 6, 8 with dense rows or presence masks.
+// Fused shapes: D <= 8, dense rows or presence masks.
 bool tags_serve_supported(const agn_log &log, bool sparse);
 // scr: 3 n + 4 words, the first 4 zero on entry (and again after _rest).
 int launch_tags_serve(const agn_log &log, const agn_read &req, const agn_result &out,
