@@ -87,6 +87,13 @@ def parse():
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-staged read path (keys + R from pinned host "
                          "memory, results back to pinned host memory; PCIe-inclusive)")
+    ap.add_argument("--configs", default="auto",
+                    help="BASELINE configs measured after the headline and reported in the same "
+                         "line's 'configs' object: comma list of 1, 2:full, 2:mixed, 3, 4, 5; "
+                         "'auto' = every config (N = 1) or the multi-GPU ones 4, 5 (N > 1) when "
+                         "the headline is the default cfg2 run; 'none' = headline only")
+    ap.add_argument("--cpu-target-s", type=float, default=10.0,
+                    help="seconds of CPU work per thread count in the CPU baseline")
     return ap.parse_args()
 
 
@@ -299,11 +306,58 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    env = (torch, dist, world, rank, local, backend)
+    line = (gst_main if a.config == 5 else materialize_main)(a, *env)
+    # the other BASELINE configs, each its own engine (the previous one's HBM
+    # freed), its own warmup + barrier-bracketed timed launches, PMC traffic and
+    # a short CPU baseline -- reported in the same JSON line, never in `value`
+    configs = {}
+    for name, cid, sparse in sub_configs(a, world):
+        sa = argparse.Namespace(**vars(a))
+        sa.config, sa.sparse, sa.keys, sa.configs = cid, sparse, 0, "none"
+        sa.gc = sa.warm = sa.ingest = sa.e2e = sa.gst = sa.post_gc = False
+        sa.steps = max(a.steps, 200) if cid == 1 else a.steps
+        sa.cpu_target_s = min(a.cpu_target_s, 2.0)
+        sa.cpu_keys = 0 if a.cpu_keys == 0 else -2    # -2: the sub-config sample size
+        sub = (gst_main if cid == 5 else materialize_main)(sa, *env)
+        if rank == 0:
+            configs[name] = {k: v for k, v in sub.items()
+                             if k not in ("metric", "higher_is_better", "data", "build",
+                                          "vs_baseline", "dtype", "n_gpus", "gen_s")}
+    if rank == 0:
+        if configs:
+            line["configs"] = configs
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def sub_configs(a, world):
+    """(name, config, sparse) of the configs measured after the headline."""
+    spec = a.configs
+    if spec == "auto":
+        extra = a.gc or a.warm or a.ingest or a.e2e or a.post_gc or a.gst or a.keys
+        if a.config != 2 or a.sparse or extra:
+            return []
+        spec = "1,2:full,3,4,5" if world == 1 else "4,5"
+    if spec == "none":
+        return []
+    out = []
+    for item in spec.split(","):
+        cid, _, sparse = item.strip().partition(":")
+        name = f"cfg{cid}" + (f"_masked_{sparse}" if sparse else "")
+        out.append((name, int(cid), sparse))
+    return out
+
+
+KERNEL_NAME = {1: "k_counter_key", 2: "k_counter_key", 3: "k_tags", 4: "k_tags", 5: "k_gst_cols"}
+
+
+def materialize_main(a, torch, dist, world, rank, local, backend):
+    """One materialize config: returns the bench line (rank 0) or None."""
     from antidote_amd import _abi
     from antidote_amd.engine import Engine
 
-    if a.config == 5:
-        return gst_main(a, torch, dist, world, rank, local, backend)
     cfg = dict(CONFIGS[a.config])
     n_keys = a.keys or cfg["n_keys"]
     if cfg.get("strong") and not a.keys:
@@ -419,13 +473,17 @@ def main():
         gst = gst_bench(eng, torch, dist, world, rank, sp, backend)
     post_gc = post_gc_bench(eng, cfg, n_keys, rank, world, sp, torch, a.steps) if a.post_gc else None
 
+    line = None
     if rank == 0:
         cpu = None
-        # ~64M ops of host-generated sample, timed for ~10 s per thread count
-        n_cpu = a.cpu_keys if a.cpu_keys >= 0 else 64_000_000 // cfg["ops_per_key"]
+        # ~64M ops of host-generated sample (8M for a sub-config), timed for
+        # ~cpu_target_s seconds per thread count
+        n_cpu = a.cpu_keys if a.cpu_keys >= 0 else \
+            (64_000_000 if a.cpu_keys == -1 else 8_000_000) // cfg["ops_per_key"]
         if world == 1 and n_cpu > 0:
             thr = a.cpu_threads or min(16, os.cpu_count() or 1)
-            rates, secs, reps = cpu_baseline(cfg, min(n_cpu, n_keys), thr, sparse=a.sparse)
+            rates, secs, reps = cpu_baseline(cfg, min(n_cpu, n_keys), thr,
+                                             target_s=a.cpu_target_s, sparse=a.sparse)
             cpu = {"value": rates[1], "unit": "ops/s", "cores": 1, "kind": "port",
                    "sample": f"{min(n_cpu, n_keys)} keys x {cfg['ops_per_key']} ops of the same "
                              f"workload (host-generated, same SplitMix64 streams), "
@@ -454,7 +512,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "kernel": KERNEL_NAME[a.config],
                          "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch,
                          "algorithmic_bytes_survey": bytes_survey,
                          "frac_survey_bytes": bytes_survey / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -481,14 +539,14 @@ def main():
             line["ingest"] = ingest
         if e2e:
             line["e2e"] = e2e
-        print(json.dumps(line), flush=True)
 
     if presence:  # the masks are torch's, not the generator's
         dl.oc_mask = dr.R_mask = dl.key_mask = None
+        del ocm_t, rm_t
     eng.free_gen(dl, dr)
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    torch.cuda.empty_cache()
+    return line
 
 
 def ingest_bench(eng, cfg, sp, torch, n_txn=10_000_000, n_keys=1_000_000):
@@ -1258,6 +1316,7 @@ def gst_main(a, torch, dist, world, rank, local, backend):
     bytes_launch = E * Pl * D * 8 + E * (D + 1) * 8
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     value = P * E * a.steps / elapsed
+    line = None
     if rank == 0:
         traffic, traffic_src = pmc_traffic(5, Pl)
         cpu = None
@@ -1268,7 +1327,8 @@ def gst_main(a, torch, dist, world, rank, local, backend):
             host = np.ascontiguousarray(clocks[:Es].cpu().numpy().view(np.uint64))
             res = np.zeros((Es, D + 1), np.uint64)
             reps, secs = 0, 0.0
-            while secs < 5.0:
+            tgt = min(5.0, a.cpu_target_s)
+            while secs < tgt:
                 t1 = time.perf_counter()
                 lib.oracle_gst_min(D, Pl, Es, host.ctypes.data, None, res.ctypes.data, 1)
                 secs += time.perf_counter() - t1
@@ -1282,7 +1342,7 @@ def gst_main(a, torch, dist, world, rank, local, backend):
                                    res.ctypes.data + e * (D + 1) * 8, 1)
             mt_reps, mt_secs = 0, 0.0
             with ThreadPoolExecutor(thr) as ex:
-                while mt_secs < 5.0:
+                while mt_secs < tgt:
                     t1 = time.perf_counter()
                     list(ex.map(one, range(Es)))
                     mt_secs += time.perf_counter() - t1
@@ -1306,14 +1366,15 @@ def gst_main(a, torch, dist, world, rank, local, backend):
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src, "kernel_src_sha16": kernel_src_sha16(5),
                          "kernel_ms": kern_ms,
-                         "kernel": "agn_gst_min over 256 epochs (k_gst_init + k_gst_cols), HIP events",
+                         "kernel": "k_gst_cols",
+                         "timed": "agn_gst_min over 256 epochs (k_gst_init + k_gst_cols), HIP events",
                          "algorithmic_bytes": bytes_launch},
             "cpu_baseline": cpu, "exchange_verified": ok, "epoch_latency_us": lat_us,
         }
-        print(json.dumps(line), flush=True)
+    del clocks, out
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    torch.cuda.empty_cache()
+    return line
 
 
 if __name__ == "__main__":
