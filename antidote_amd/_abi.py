@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK = 0
 EINVAL, EHIP, ENOMEM, ECAPACITY, ENOTSUP, ERCCL, ENODEV = -1, -2, -3, -4, -5, -6, -7
@@ -18,6 +18,8 @@ EFFECT_INVALID = -(1 << 63)
 TAG_INVALID = 0xFFFFFFFF
 
 F_NEWSS, F_CT_IGNORE, F_ERR_UNEXPECTED, F_ERR_CORRUPTED, F_ERR_CAPACITY = 0x1, 0x2, 0x4, 0x8, 0x10
+F_CT_FULL = 0x20          # ABI v5: LastOpCt has every column (mask not written)
+HINT_R_FULL, HINT_CT_FLAG = 0x1, 0x2
 OPS_THRESHOLD = 50  # src/materializer_vnode.erl:41
 RESIZE_THRESHOLD = 5  # :44
 GC_ALL_PRUNED = 0x1
@@ -52,7 +54,7 @@ class AgnRead(C.Structure):
     _fields_ = [
         ("n_req", C.c_uint64), ("keys", P), ("R", P), ("R_mask", P),
         ("sct", P), ("sct_mask", P), ("sct_ignore", P), ("txid", P),
-        ("req_type", C.c_uint32), ("_pad", C.c_uint32),
+        ("req_type", C.c_uint32), ("hints", C.c_uint32),
         ("base_value", P), ("base_off", P), ("base_tag", P), ("base_tok", P),
     ]
 
@@ -173,6 +175,9 @@ PROTOTYPES = {
     "agn_batcher_destroy": (C.c_int, [P]),
     "agn_batcher_read": (C.c_int, [P, C.POINTER(AgnKeyRead), C.POINTER(AgnKeyResult)]),
     "agn_batcher_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "agn_batcher_state_bound": (C.c_int, [P, C.c_uint64, C.POINTER(C.c_uint32)]),
+    "agn_batcher_store": (C.c_int, [P, C.c_uint64, P, P, C.c_int64, C.c_uint32, C.c_int64,
+                                    C.c_uint32, P, P, C.c_uint32]),
     "agn_batcher_create_cached": (C.c_int, [P, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(P)]),
     "agn_oplog_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                   C.POINTER(C.c_uint64)]),

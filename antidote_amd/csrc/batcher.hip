@@ -31,6 +31,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_set>
@@ -45,8 +46,19 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// agn_batcher_store's request: a snapshot the caller materialized itself
+struct StoreReq {
+    uint64_t key;
+    const uint64_t *clock, *clock_mask;  // LastOpCt row [D] (+ [W]) (host)
+    int64_t last_op, value;
+    uint32_t count, n_pairs, flags;
+    const uint32_t *tags;
+    const uint64_t *toks;
+};
+
 struct Pending {
     const agn_key_read *rd;
+    const StoreReq *st = nullptr;  // a store instead of a read (rd is null)
     agn_key_result *out;
     Clock::time_point t;
     int rc = AGN_OK;
@@ -91,7 +103,12 @@ struct agn_batcher {
     // of the pairs of any state the cache holds for it (the largest result
     // seen: every cached state is a result's), which sizes a batch's output
     uint64_t *ctl_h = nullptr;  // pinned [4]
-    std::vector<uint32_t> kbound;
+    // written by the worker only; read by agn_batcher_state_bound's callers
+    std::unique_ptr<std::atomic<uint32_t>[]> kbound;
+    uint32_t bound_of(uint64_t k) const { return kbound[k].load(std::memory_order_relaxed); }
+    void raise_bound(uint64_t k, uint32_t m) {
+        if (m > bound_of(k)) kbound[k].store(m, std::memory_order_relaxed);
+    }
     // the fused set/register read's scratch (tags_serve.hpp): 3 n + 4 words,
     // the first 4 zero between batches
     uint32_t *tscr = nullptr;
@@ -119,6 +136,23 @@ int grow(agn_batcher *B, size_t bytes) {
 // profiles/r02/serve/.)
 int wait_batch(agn_batcher *B) {
     AGN_HIP(hipStreamSynchronize(B->stream));
+    return AGN_OK;
+}
+
+// agn_key_result.err_pos is the failing op's id (its key's op counter value,
+// what the caller's error term names): the kernels report the entry's slot in
+// the log, meaningful only while the log is held, so it is translated through
+// the log's op_id column here (one 4-byte read per failed read: rare).
+int errs_to_op_ids(agn_batcher *B, const agn_log &view, std::vector<Pending *> &b) {
+    for (Pending *p : b) {
+        agn_key_result *o = p->out;
+        if (!(o->flags & AGN_F_ERR_UNEXPECTED) || o->err_pos == 0xffffffffu || !view.op_id)
+            continue;
+        uint32_t id = 0;
+        AGN_HIP(hipMemcpyAsync(&id, view.op_id + o->err_pos, 4, hipMemcpyDeviceToHost, B->stream));
+        AGN_HIP(hipStreamSynchronize(B->stream));
+        o->err_pos = id;
+    }
     return AGN_OK;
 }
 
@@ -219,6 +253,8 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
             o->out_n = 0;
             any_prune = any_prune || ((const uint8_t *)(h + o_pr))[i] != 0;
         }
+        rc = errs_to_op_ids(B, view, b);
+        if (rc) return rc;
         if (!any_prune) return AGN_OK;
     }  // the shared hold ends: the GC takes the log exclusively
     return oplog_prune_keys(B->log, n, keys.data(), (const uint64_t *)(B->dbuf + d_keys),
@@ -228,28 +264,62 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
 // The state arena must hold `need` more pairs: re-pack the live states into a
 // fresh arena of max(capacity, 2 x (live + need)) pairs (agn_ss_state_compact's
 // kernel) and free the old one.  Between batches, on the batcher's stream.
+// A store that did not fit (state_ctl[2]) still advanced state_ctl[0] past
+// the capacity (its pairs counted as released), so the room is clamped at 0
+// and an overflow always re-packs (which clears it).  The re-pack commits all
+// or nothing: the slots' new references go to scratch and replace the cache's
+// only when every live state fit; otherwise the old arena, references and
+// state_ctl stay as they were.
 int ensure_state_room(agn_batcher *B, uint64_t need) {
-    if (B->ss.state_cap - B->ctl_h[0] >= need) return AGN_OK;
+    const uint64_t used = B->ctl_h[0];
+    const uint64_t room = used >= B->ss.state_cap ? 0 : B->ss.state_cap - used;
+    if (room >= need && !B->ctl_h[2]) return AGN_OK;
+    // the exact counters (the host copy may be a sum of per-store deltas)
+    uint64_t ctl[4];
+    AGN_HIP(hipMemcpyAsync(ctl, B->ss.state_ctl, sizeof ctl, hipMemcpyDeviceToHost, B->stream));
     AGN_HIP(hipStreamSynchronize(B->stream));
-    const uint64_t live = B->ctl_h[0] - B->ctl_h[1];
+    std::memcpy(B->ctl_h, ctl, sizeof ctl);
+    const uint64_t live = ctl[0] - ctl[1];
     const uint64_t cap = std::max<uint64_t>(B->ss.state_cap, 2 * (live + need));
+    const uint64_t nval = B->ss.n_keys * B->ss.slots;
     uint32_t *nt = nullptr;
     uint64_t *nk = nullptr;
-    if (hipMalloc((void **)&nt, cap * 4) != hipSuccess || hipMalloc((void **)&nk, cap * 8) != hipSuccess) {
+    int64_t *nv = nullptr;
+    if (hipMalloc((void **)&nt, cap * 4) != hipSuccess || hipMalloc((void **)&nk, cap * 8) != hipSuccess ||
+        hipMalloc((void **)&nv, std::max<uint64_t>(nval, 1) * 8) != hipSuccess) {
         if (nt) (void)hipFree(nt);
+        if (nk) (void)hipFree(nk);
         return fail(AGN_ENOMEM, "batcher: state arena of %llu pairs", (unsigned long long)cap);
     }
-    int rc = launch_ss_compact(B->ss, nt, nk, cap, B->ss.state_ctl + 2, B->stream);
-    if (rc == AGN_OK && hipMemcpyAsync(B->ctl_h, B->ss.state_ctl, 4 * 8, hipMemcpyDeviceToHost,
+    int rc = launch_ss_compact(B->ss, nt, nk, cap, B->ss.state_ctl + 2, B->stream, nv);
+    uint64_t after[4] = {0, 0, 0, 0};
+    if (rc == AGN_OK && hipMemcpyAsync(after, B->ss.state_ctl, sizeof after, hipMemcpyDeviceToHost,
                                        B->stream) != hipSuccess)
         rc = fail(AGN_EHIP, "batcher: state_ctl copy");
     if (rc == AGN_OK && hipStreamSynchronize(B->stream) != hipSuccess)
         rc = fail(AGN_EHIP, "batcher: state compaction");
+    if (rc == AGN_OK && after[2]) {
+        // did not fit (the live count disagreed with the slots): keep the old
+        // arena and references, restore its counters
+        if (hipMemcpyAsync(B->ss.state_ctl, ctl, sizeof ctl, hipMemcpyHostToDevice, B->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(B->stream) != hipSuccess)
+            rc = fail(AGN_EHIP, "batcher: state_ctl restore");
+        else
+            rc = fail(AGN_ECAPACITY, "batcher: state re-pack overflowed %llu pairs",
+                      (unsigned long long)cap);
+    }
+    if (rc == AGN_OK && nval &&
+        (hipMemcpyAsync(B->ss.value, nv, nval * 8, hipMemcpyDeviceToDevice, B->stream) != hipSuccess ||
+         hipStreamSynchronize(B->stream) != hipSuccess))
+        rc = fail(AGN_EHIP, "batcher: state references commit");
+    (void)hipFree(nv);
     if (rc) {
         (void)hipFree(nt);
         (void)hipFree(nk);
         return rc;
     }
+    std::memcpy(B->ctl_h, after, sizeof after);
     (void)hipFree(B->ss.state_tag);
     (void)hipFree(B->ss.state_tok);
     B->ss.state_tag = nt;
@@ -278,7 +348,7 @@ int run_batch_tags_fused(agn_batcher *B, std::vector<Pending *> &b, bool sparse)
         if (rc) return rc;
         std::vector<uint64_t> co(n + 1);
         co[0] = 0;
-        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + B->kbound[keys[i]];
+        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + B->bound_of(keys[i]);
         const uint64_t ncap = co[n];
         rc = ensure_state_room(B, ncap);
         if (rc) return rc;
@@ -390,7 +460,9 @@ int run_batch_tags_fused(agn_batcher *B, std::vector<Pending *> &b, bool sparse)
                 if (((const uint8_t *)H(o_pr))[i] & 2u) B->ctl_h[2] = 1;
             }
         }
-        if (B->ctl_h[2]) return fail(AGN_ECAPACITY, "batcher: state arena overflow");
+        // ctl_h[2]: a store did not fit the arena and was not made (its
+        // snapshot is simply not cached: the results stand); the next batch's
+        // ensure_state_room re-packs
         bool any_prune = false;
         for (uint64_t i = 0; i < n; ++i) {
             agn_key_result *o = b[i]->out;
@@ -408,7 +480,7 @@ int run_batch_tags_fused(agn_batcher *B, std::vector<Pending *> &b, bool sparse)
             const bool ok = !(o->flags & (AGN_F_ERR_CORRUPTED | AGN_F_ERR_UNEXPECTED |
                                           AGN_F_ERR_CAPACITY));
             o->out_n = ok ? m : 0;
-            if (ok) B->kbound[keys[i]] = std::max(B->kbound[keys[i]], m);
+            if (ok) B->raise_bound(keys[i], m);
             if (!ok || o->status == AGN_SS_LOG) continue;
             if (m > o->out_cap) {  // the caller retries with out_cap >= out_n
                 b[i]->rc = AGN_ECAPACITY;
@@ -421,6 +493,8 @@ int run_batch_tags_fused(agn_batcher *B, std::vector<Pending *> &b, bool sparse)
                 std::memcpy(o->out_tok, H(o_otok) + co[i] * 8, m * 8);
             }
         }
+        rc = errs_to_op_ids(B, view, b);
+        if (rc) return rc;
         if (!any_prune) return AGN_OK;
     }  // the shared hold ends: the GC takes the log exclusively
     return oplog_prune_keys(B->log, n, keys.data(), (const uint64_t *)(B->dbuf + d_keys),
@@ -456,7 +530,7 @@ int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
         // one pair) + the bound of its cached states
         std::vector<uint64_t> co(n + 1);
         co[0] = 0;
-        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + B->kbound[keys[i]];
+        for (uint64_t i = 0; i < n; ++i) co[i + 1] = co[i] + lens[i] + B->bound_of(keys[i]);
         const uint64_t ncap = co[n];
         rc = ensure_state_room(B, ncap);
         if (rc) return rc;
@@ -538,7 +612,9 @@ int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
         AGN_HIP(hipMemcpyAsync(B->ctl_h, B->ss.state_ctl, 4 * 8, hipMemcpyDeviceToHost, B->stream));
         rc = wait_batch(B);
         if (rc) return rc;
-        if (B->ctl_h[2]) return fail(AGN_ECAPACITY, "batcher: state arena overflow");
+        // ctl_h[2]: a store did not fit the arena and was not made (its
+        // snapshot is simply not cached: the results stand); the next batch's
+        // ensure_state_room re-packs
         bool any_prune = false;
         for (uint64_t i = 0; i < n; ++i) {
             agn_key_result *o = b[i]->out;
@@ -556,7 +632,7 @@ int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
             const bool ok = !(o->flags & (AGN_F_ERR_CORRUPTED | AGN_F_ERR_UNEXPECTED |
                                           AGN_F_ERR_CAPACITY));
             o->out_n = ok ? m : 0;
-            if (ok) B->kbound[keys[i]] = std::max(B->kbound[keys[i]], m);
+            if (ok) B->raise_bound(keys[i], m);
             if (!ok || o->status == AGN_SS_LOG) continue;
             if (m > o->out_cap) {  // the caller retries with out_cap >= out_n
                 b[i]->rc = AGN_ECAPACITY;
@@ -569,6 +645,8 @@ int run_batch_cached_tags(agn_batcher *B, std::vector<Pending *> &b) {
                 std::memcpy(o->out_tok, H(o_otok) + co[i] * 8, m * 8);
             }
         }
+        rc = errs_to_op_ids(B, view, b);
+        if (rc) return rc;
         if (!any_prune) return AGN_OK;
     }  // the shared hold ends: the GC takes the log exclusively
     return oplog_prune_keys(B->log, n, keys.data(), (const uint64_t *)(B->dbuf + o_keys_saved),
@@ -681,6 +759,8 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
             o->out_n = 0;
             any_prune = any_prune || ((const uint8_t *)H(o_pr))[i] != 0;
         }
+        rc = errs_to_op_ids(B, view, b);
+        if (rc) return rc;
         if (!any_prune) return AGN_OK;
     }  // the shared hold ends: the GC takes the log exclusively
     // prune_ops of the batch's selected keys (in place, over the batch's key
@@ -781,6 +861,16 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
     }
     req.txid = (const uint64_t *)(d + o_txid);
     req.req_type = B->crdt;
+    if (sparse) {
+        // the batch's promises (agn_read.hints): every R mask carries all D
+        // DCs, and LastOpCt masks over every column come back as a flag
+        bool rfull = true;
+        for (uint64_t i = 0; i < n && rfull; ++i) {
+            const uint64_t *m = b[i]->rd->R_mask;
+            for (uint32_t x = 0; m && x < W && rfull; ++x) rfull = (m[x] & full[x]) == full[x];
+        }
+        req.hints = AGN_HINT_CT_FLAG | (rfull ? AGN_HINT_R_FULL : 0u);
+    }
     if (tags) {
         req.base_off = (const uint64_t *)(d + o_boff);
         req.base_tag = (const uint32_t *)(d + o_btag);
@@ -816,9 +906,13 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
         o->value = tags ? 0 : ((const int64_t *)H(o_val))[i];
         o->hole = ((const int64_t *)H(o_hole))[i];
         std::memcpy(o->lastct, H(o_ct) + i * D * 8, D * 8);
-        if (o->lastct_mask) std::memcpy(o->lastct_mask, sparse ? H(o_ctm) + i * W * 8 : (char *)full, W * 8);
         o->count = ((const uint32_t *)H(o_cnt))[i];
         o->flags = ((const uint32_t *)H(o_flg))[i];
+        const bool ct_full = (o->flags & AGN_F_CT_FULL) != 0u;  // AGN_HINT_CT_FLAG
+        o->flags &= ~AGN_F_CT_FULL;
+        if (o->lastct_mask)
+            std::memcpy(o->lastct_mask, (sparse && !ct_full) ? H(o_ctm) + i * W * 8 : (char *)full,
+                        W * 8);
         o->err_pos = ((const uint32_t *)H(o_epos))[i];
         o->status = 0;
         if (tags) {
@@ -838,7 +932,94 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
             }
         }
     }
-    return AGN_OK;
+    return errs_to_op_ids(B, view, b);
+}
+
+// agn_batcher_store: materialize_snapshot's store (:466-509) of a snapshot
+// the caller materialized from get_from_snapshot_log's response (IsNewest =
+// false: only a GC read stores it) -> internal_store_ss / insert_bigger /
+// snapshot_insert_gc (:341-364, 513-563) on the device cache, then prune_ops
+// of the key when the policy collects -- the same kernels a read's store runs.
+int run_store(agn_batcher *B, const StoreReq &s) {
+    const uint32_t D = B->D, W = B->W;
+    const bool tags = B->crdt != AGN_COUNTER_PN;
+    const bool msk = B->ss.clock_mask != nullptr;
+    uint64_t key = s.key;
+    uint32_t len = 0;
+    size_t d_keys = 0, d_pr = 0;
+    bool collect = false;
+    {
+        std::shared_lock<std::shared_mutex> hold;
+        int rc = oplog_begin_read(B->log, B->stream, 1, &key, &len, hold);
+        if (rc) return rc;
+        if (tags) {
+            rc = ensure_state_room(B, s.n_pairs);
+            if (rc) return rc;
+        }
+        size_t off = 0;
+        auto slot = [&](size_t bytes) { size_t o = off; off = al(off + bytes); return o; };
+        const size_t o_first = slot(1), o_st = slot(1), o_gc = slot(1), o_ct = slot(D * 8),
+                     o_ctm = slot(W * 8), o_hole = slot(8), o_val = slot(8), o_cnt = slot(4),
+                     o_flg = slot(4), o_off = slot(16), o_n = slot(4),
+                     o_tag = slot(std::max<uint32_t>(s.n_pairs, 1) * 4),
+                     o_tok = slot(std::max<uint32_t>(s.n_pairs, 1) * 8), o_pr = slot(1);
+        d_keys = 0;
+        d_pr = al(8);
+        rc = grow(B, std::max(off, d_pr + 1));
+        if (rc) return rc;
+        char *h = B->hbuf, *x = B->hdev;
+        ((uint8_t *)(h + o_first))[0] = 0;            // a log response: not the newest
+        ((uint8_t *)(h + o_st))[0] = AGN_SS_HIT;       // (anything but LOG)
+        ((uint8_t *)(h + o_gc))[0] = (s.flags & AGN_READ_GC) ? 1 : 0;
+        std::memcpy(h + o_ct, s.clock, D * 8);
+        uint64_t full[4] = {0, 0, 0, 0};
+        for (uint32_t c = 0; c < D; ++c) full[c >> 6] |= 1ull << (c & 63);
+        std::memcpy(h + o_ctm, s.clock_mask ? s.clock_mask : full, W * 8);
+        ((int64_t *)(h + o_hole))[0] = s.last_op;
+        ((int64_t *)(h + o_val))[0] = s.value;
+        ((uint32_t *)(h + o_cnt))[0] = s.count;
+        ((uint32_t *)(h + o_flg))[0] = s.count ? AGN_F_NEWSS : 0u;
+        ((uint64_t *)(h + o_off))[0] = 0;
+        ((uint64_t *)(h + o_off))[1] = s.n_pairs;
+        ((uint32_t *)(h + o_n))[0] = s.n_pairs;
+        if (s.n_pairs) {
+            std::memcpy(h + o_tag, s.tags, (size_t)s.n_pairs * 4);
+            std::memcpy(h + o_tok, s.toks, (size_t)s.n_pairs * 8);
+        }
+        AGN_HIP(hipMemcpyAsync(B->dbuf + d_keys, &key, 8, hipMemcpyHostToDevice, B->stream));
+        agn_result res;
+        std::memset(&res, 0, sizeof res);
+        res.lastct = (uint64_t *)(x + o_ct);
+        res.lastct_mask = msk ? (uint64_t *)(x + o_ctm) : nullptr;
+        res.hole = (int64_t *)(x + o_hole);
+        res.value = (int64_t *)(x + o_val);
+        res.count = (uint32_t *)(x + o_cnt);
+        res.flags = (uint32_t *)(x + o_flg);
+        if (tags) {
+            res.out_off = (const uint64_t *)(x + o_off);
+            res.out_n = (uint32_t *)(x + o_n);
+            res.out_tag = (uint32_t *)(x + o_tag);
+            res.out_tok = (uint64_t *)(x + o_tok);
+        }
+        agn_log view;
+        oplog_view(B->log, &view);
+        rc = launch_ss_store_req(B->ss, view.key_off, view.key_len, 1,
+                                 (const uint64_t *)(B->dbuf + d_keys), (const uint8_t *)(x + o_first),
+                                 (const uint8_t *)(x + o_st), (const uint8_t *)(x + o_gc), res,
+                                 (uint8_t *)(B->dbuf + d_pr), B->thr, B->thrm, B->stream);
+        if (rc) return rc;
+        AGN_HIP(hipMemcpyAsync(h + o_pr, B->dbuf + d_pr, 1, hipMemcpyDeviceToHost, B->stream));
+        if (tags)
+            AGN_HIP(hipMemcpyAsync(B->ctl_h, B->ss.state_ctl, 4 * 8, hipMemcpyDeviceToHost,
+                                   B->stream));
+        rc = wait_batch(B);
+        if (rc) return rc;
+        if (tags && !B->ctl_h[2]) B->raise_bound(key, s.n_pairs);
+        collect = ((const uint8_t *)(h + o_pr))[0] != 0;
+    }  // the shared hold ends: the GC takes the log exclusively
+    if (!collect) return AGN_OK;
+    return oplog_prune_keys(B->log, 1, &key, (const uint64_t *)(B->dbuf + d_keys),
+                            (const uint8_t *)(B->dbuf + d_pr), B->thr, B->thrm, B->stream);
 }
 
 void worker_main(agn_batcher *B) {
@@ -855,21 +1036,30 @@ void worker_main(agn_batcher *B) {
             const size_t n = std::min<size_t>(B->q.size(), B->max_batch);
             batch.assign(B->q.begin(), B->q.begin() + n);
             B->q.erase(B->q.begin(), B->q.begin() + n);
+        } else if (B->q.front()->st) {
+            // a caller-computed snapshot (agn_batcher_store): alone, in order
+            batch.push_back(B->q.front());
+            B->q.pop_front();
         } else {
-            // distinct keys, in arrival order; a repeated key waits for the next batch
+            // distinct keys, in arrival order; a repeated key waits for the next
+            // batch, and nothing queued after a store joins this one
             std::unordered_set<uint64_t> in;
             std::deque<Pending *> rest;
+            bool barrier = false;
             for (Pending *p : B->q) {
-                if (batch.size() < B->max_batch && in.insert(p->rd->key).second)
+                barrier = barrier || p->st != nullptr;
+                if (!barrier && batch.size() < B->max_batch && in.insert(p->rd->key).second)
                     batch.push_back(p);
                 else
                     rest.push_back(p);
             }
             B->q.swap(rest);
         }
-        const size_t n = batch.size();
+        const size_t n = batch[0]->st ? 0 : batch.size();
         lk.unlock();
-        int rc = B->cached ? run_batch_cached(B, batch) : run_batch(B, batch);
+        int rc = !B->cached        ? run_batch(B, batch)
+                 : batch[0]->st ? run_store(B, *batch[0]->st)
+                                : run_batch_cached(B, batch);
         if (rc)
             for (Pending *p : batch) {
                 p->rc = rc;
@@ -978,6 +1168,9 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     uint64_t *ctl_h = nullptr;
     if (crdt != AGN_COUNTER_PN) {
         c.state_cap = std::max<uint64_t>(16 * K1, 1u << 16);
+        // test knob: a small first arena, so re-packs and growth happen early
+        const char *ai = getenv("AGN_SS_ARENA_INIT");
+        if (ai && std::strtoull(ai, nullptr, 10) > 0) c.state_cap = std::strtoull(ai, nullptr, 10);
         if (e == hipSuccess) e = hipMalloc((void **)&c.state_tag, c.state_cap * 4);
         if (e == hipSuccess) e = hipMalloc((void **)&c.state_tok, c.state_cap * 8);
         if (e == hipSuccess) e = hipMalloc((void **)&c.state_ctl, 4 * 8);
@@ -985,13 +1178,11 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
         if (e == hipSuccess) e = hipHostMalloc((void **)&ctl_h, 4 * 8, hipHostMallocDefault);
         if (e == hipSuccess) std::memset(ctl_h, 0, 4 * 8);
     }
-    std::vector<uint32_t> kb;  // set/register: per-key state bounds
+    std::unique_ptr<std::atomic<uint32_t>[]> kb;  // set/register: per-key state bounds
     if (e == hipSuccess && crdt != AGN_COUNTER_PN) {
-        try {
-            kb.assign(K1, 0);
-        } catch (...) {
-            e = hipErrorOutOfMemory;
-        }
+        kb.reset(new (std::nothrow) std::atomic<uint32_t>[K1]);
+        if (!kb) e = hipErrorOutOfMemory;
+        else for (uint64_t k = 0; k < K1; ++k) kb[k].store(0, std::memory_order_relaxed);
     }
     if (e == hipSuccess) rc = agn_batcher_create(log, max_batch, max_wait_us, out);
     if (e != hipSuccess || rc != AGN_OK) {
@@ -1013,7 +1204,7 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     (*out)->thr = thr;
     (*out)->thrm = thrm;
     (*out)->ctl_h = ctl_h;
-    (*out)->kbound.swap(kb);
+    (*out)->kbound = std::move(kb);
     return AGN_OK;
 }
 
@@ -1039,6 +1230,39 @@ int agn_batcher_read(agn_batcher *B, const agn_key_read *rd, agn_key_result *out
     if (B->q.size() == 1 || B->q.size() >= B->max_batch) B->cv_work.notify_one();
     p.cv.wait(lk, [&] { return p.done; });
     if (p.rc) return fail(p.rc, "%s", p.err);
+    return AGN_OK;
+}
+
+int agn_batcher_store(agn_batcher *B, uint64_t key, const uint64_t *clock,
+                      const uint64_t *clock_mask, int64_t last_op, uint32_t count, int64_t value,
+                      uint32_t n_pairs, const uint32_t *tags, const uint64_t *toks, uint32_t flags) {
+    if (!B || !clock) return fail(AGN_EINVAL, "batcher_store: null argument");
+    if (!B->cached) return fail(AGN_EINVAL, "batcher_store: the batcher has no snapshot cache");
+    if (key >= B->K) return fail(AGN_EINVAL, "batcher_store: key %llu >= n_keys",
+                                 (unsigned long long)key);
+    if (flags & ~(uint32_t)AGN_READ_GC) return fail(AGN_EINVAL, "batcher_store: unknown flags");
+    if (B->crdt == AGN_COUNTER_PN ? n_pairs != 0 : (n_pairs && (!tags || !toks)))
+        return fail(AGN_EINVAL, "batcher_store: state pairs do not match the type");
+    if (n_pairs > AGN_SS_STATE_MAX_PAIRS) return fail(AGN_ECAPACITY, "batcher_store: %u pairs", n_pairs);
+    StoreReq s{key, clock, clock_mask, last_op, value, count, n_pairs, flags, tags, toks};
+    Pending p;
+    p.rd = nullptr;
+    p.st = &s;
+    p.t = Clock::now();
+    std::unique_lock<std::mutex> lk(B->mu);
+    if (B->stop) return fail(AGN_EINVAL, "batcher_store: batcher is shutting down");
+    B->q.push_back(&p);
+    B->cv_work.notify_one();
+    p.cv.wait(lk, [&] { return p.done; });
+    if (p.rc) return fail(p.rc, "%s", p.err);
+    return AGN_OK;
+}
+
+int agn_batcher_state_bound(agn_batcher *B, uint64_t key, uint32_t *pairs) {
+    if (!B || !pairs) return fail(AGN_EINVAL, "batcher_state_bound: null argument");
+    if (key >= B->K) return fail(AGN_EINVAL, "batcher_state_bound: key %llu >= n_keys",
+                                 (unsigned long long)key);
+    *pairs = B->kbound ? B->bound_of(key) : 0u;
     return AGN_OK;
 }
 

@@ -112,10 +112,13 @@ int store_g(const agn_ss_cache &c, const uint64_t *key_off, const uint64_t *key_
 
 // agn_ss_state_compact: one wave per key; the key's live slots' states are
 // copied into the fresh arena at one atomically reserved range, and their
-// references rewritten.  ctl[0] (reset to 0 before) ends as the live pairs.
+// references rewritten (into nv when given, else in place).  ctl[0] (reset to
+// 0 before) ends as the live pairs.
 __global__ __launch_bounds__(256) void k_ss_compact(agn_ss_cache c, uint32_t *__restrict__ nt,
                                                    uint64_t *__restrict__ nk, uint64_t ncap,
-                                                   uint64_t *__restrict__ ovf) {
+                                                   uint64_t *__restrict__ ovf,
+                                                   int64_t *__restrict__ nv) {
+    int64_t *const out = nv ? nv : c.value;
     const uint64_t k = uniform_u64((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6));
     if (k >= c.n_keys) return;
     const int lane = lane_id();
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(256) void k_ss_compact(agn_ss_cache c, uint32_t *__
     for (uint32_t j = 0; j < n; ++j) tot += AGN_SS_STATE_PAIRS(c.value[k * S + j]);
     if (tot == 0) {
         if (lane == 0)
-            for (uint32_t j = 0; j < n; ++j) c.value[k * S + j] = AGN_SS_STATE(0, 0);
+            for (uint32_t j = 0; j < n; ++j) out[k * S + j] = AGN_SS_STATE(0, 0);
         return;
     }
     uint64_t base = 0;
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(256) void k_ss_compact(agn_ss_cache c, uint32_t *__
             nk[base + x] = c.state_tok[s0 + x];
         }
         __builtin_amdgcn_wave_barrier();
-        if (lane == 0) c.value[k * S + j] = AGN_SS_STATE(p ? base : 0, p);
+        if (lane == 0) out[k * S + j] = AGN_SS_STATE(p ? base : 0, p);
         base += p;
     }
 }
@@ -151,13 +154,13 @@ __global__ __launch_bounds__(256) void k_ss_compact(agn_ss_cache c, uint32_t *__
 }  // namespace
 
 int launch_ss_compact(const agn_ss_cache &c, uint32_t *new_tag, uint64_t *new_tok, uint64_t new_cap,
-                      uint64_t *ovf, hipStream_t st) {
+                      uint64_t *ovf, hipStream_t st, int64_t *new_value) {
     AGN_HIP(hipMemsetAsync(c.state_ctl, 0, 4 * sizeof(uint64_t), st));
     if (c.n_keys == 0) return AGN_OK;
     const uint64_t nb = (c.n_keys + 3) / 4;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "ss_state_compact: too many keys");
     hipLaunchKernelGGL(k_ss_compact, dim3((unsigned)nb), dim3(256), 0, st, c, new_tag, new_tok,
-                       new_cap, ovf);
+                       new_cap, ovf, new_value);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }

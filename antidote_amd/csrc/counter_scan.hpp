@@ -310,12 +310,16 @@ __device__ __forceinline__ Q8Chunk q8_load(const uint64_t *__restrict__ oc,
     return c;
 }
 
+// noR: R lacks one of the DCs every op of the key carries -- every op is
+// excluded (is_op_in_snapshot's missing-DC branch, :245-247); the SCT compare
+// (notInPrev) still decides which exclusions count.
 template <bool WARM>
 __device__ __forceinline__ void q8_fold(const Q8Chunk &c, const uint64_t *__restrict__ txid,
                                         uint64_t txr, uint64_t off, uint64_t b, uint64_t n,
                                         uint64_t n_entries, uint64_t rA, uint64_t rB, uint64_t sA,
                                         uint64_t sB, uint64_t &ctA, uint64_t &ctB, int64_t &sum,
-                                        uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+                                        uint32_t &cnt, int64_t &first_excl, int64_t &first_err,
+                                        bool noR = false) {
     const int lane = lane_id();
     const int q = lane >> 2;
     const uint64_t valid = (n - b >= (uint64_t)AGN_WAVE) ? ~0ull : ((1ull << (n - b)) - 1ull);
@@ -331,6 +335,7 @@ __device__ __forceinline__ void q8_fold(const Q8Chunk &c, const uint64_t *__rest
         e = e < n_entries - 1u ? e : n_entries - 1u;
         nip |= ballot(txid[e] == txr);
     }
+    if (noR) bad = ~0ull;
     const uint64_t incl = valid & nip & ~bad, excl = valid & nip & bad;
     if (first_excl < 0 && excl) first_excl = (int64_t)b + (int64_t)__builtin_ctzll(excl);
     cnt += (uint32_t)__builtin_popcountll(incl);
@@ -365,7 +370,8 @@ __device__ __forceinline__ void scan_key_q8(
     const uint64_t *__restrict__ oc, const int64_t *__restrict__ eff,
     const uint64_t *__restrict__ txid, uint64_t txr, uint64_t off, uint64_t n,
     uint64_t n_entries, uint64_t rA, uint64_t rB, uint64_t sA, uint64_t sB, uint64_t &ctA,
-    uint64_t &ctB, int64_t &sum, uint32_t &cnt, int64_t &first_excl, int64_t &first_err) {
+    uint64_t &ctB, int64_t &sum, uint32_t &cnt, int64_t &first_excl, int64_t &first_err,
+    bool noR = false) {
     for (uint64_t b = FROM1 ? AGN_WAVE : 0; b < n; b += AGN_WAVE) {
         const Q8Chunk c = q8_load<NT, EFF_NT>(oc, eff, off, b, n_entries);
         // every load of the chunk is in flight before the first verdict (left
@@ -373,7 +379,7 @@ __device__ __forceinline__ void scan_key_q8(
         // waits for each row load in turn)
         __builtin_amdgcn_sched_barrier(0);
         q8_fold<WARM>(c, txid, txr, off, b, n, n_entries, rA, rB, sA, sB, ctA, ctB, sum, cnt,
-                      first_excl, first_err);
+                      first_excl, first_err, noR);
     }
 }
 

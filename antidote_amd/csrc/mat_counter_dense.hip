@@ -43,6 +43,7 @@ struct DenseArgs {
     uint32_t xcd;  // 1: XCD-aware block order (xcd_block)
     uint32_t pair; // 1: D <= 4 keys longer than a chunk walk two chunks per step
     uint32_t qnt;  // quad rows, non-temporal loads: bit 0 rows, bit 1 effects (AGN_COUNTER_QUAD_NT)
+    uint32_t hints;  // agn_read.hints (k_counter_q8e / k_counter_quad2)
 };
 
 // Presence masks of a sparse batch (the MSK instantiations; one word per
@@ -457,10 +458,88 @@ inline const uint32_t *id0_index(const agn_log &log) {
 struct Q2Key {
     uint64_t i, key, off, n, txr;
     uint32_t id0;
-    bool corrupt, sct_ign, uni;
+    bool corrupt, sct_ign;
+    bool uni;  // the dense scan serves the key: its DC set U is known (MSK) or the batch is dense
+    bool noR;  // MSK: U is known but R lacks one of its DCs -- every op excluded (:245-247)
     uint64_t rA, rB, sA, sB, eA, eB;  // per lane: DCs 2p, 2p+1 (p = lane & 3)
     uint64_t U, Sm, Rm;               // MSK (Presence)
 };
+
+// agn_log.key_mask of a key (an in-bounds dummy when the log has none).
+__device__ __forceinline__ uint64_t key_word(const MaskArgs &mk, uint64_t key,
+                                             const uint64_t *__restrict__ key_off) {
+    return uniform_u64(*(mk.key_mask ? mk.key_mask + key : key_off));
+}
+
+// The key's segment (the metadata the row loads depend on).
+__device__ __forceinline__ void q2_meta(Q2Key &k, uint64_t i, const uint64_t *__restrict__ keys,
+                                        const uint64_t *__restrict__ key_off,
+                                        const uint64_t *__restrict__ key_len,
+                                        const uint32_t *__restrict__ key_id0) {
+    k.i = i;
+    k.key = keys ? uniform_u64(keys[i]) : i;
+    const KeyMeta km = key_meta(k.key, key_off, key_len, key_id0);
+    k.off = km.off;
+    k.n = km.n;
+    k.id0 = km.id0;
+}
+
+// The rest of a request's prologue: key_type, SCT and its ignore byte, TxId,
+// R, the presence words of a sparse batch.
+template <bool ANY_WARM, bool MSK>
+__device__ __forceinline__ void q2_side(Q2Key &k, const DenseArgs &a, const MaskArgs &mk,
+                                        uint64_t kmw, const uint64_t *__restrict__ key_off,
+                                        const uint8_t *__restrict__ key_type,
+                                        const uint64_t *__restrict__ R,
+                                        const uint64_t *__restrict__ sct,
+                                        const uint8_t *__restrict__ sct_ignore,
+                                        const uint64_t *__restrict__ req_txid) {
+    constexpr int D = 8;
+    const uint64_t i = k.i;
+    const uint32_t kty =
+        byte_of(key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off), k.key);
+    k.corrupt = k.n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu);
+    const uint32_t sib =
+        ANY_WARM ? byte_of(sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R), i) : 0u;
+    k.sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
+    const uint64_t txv = uniform_u64((req_txid ? req_txid : R)[i]);
+    k.txr = req_txid ? txv : 0ull;
+    uint64_t rmw = 0, smw = 0;
+    if constexpr (MSK) {
+        // AGN_HINT_R_FULL: every R mask carries all D DCs (not read)
+        const bool rfull = (a.hints & AGN_HINT_R_FULL) != 0u;
+        rmw = uniform_u64(*((mk.R_mask && !rfull) ? mk.R_mask + i : R));
+        if (rfull) rmw = ~0ull;
+        smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
+    }
+    const Presence<D> pr = presence<D, MSK>(mk, kmw, rmw, smw, k.n);
+    k.U = pr.U;
+    k.Rm = pr.Rm;
+    k.Sm = pr.Sm;
+    // a known DC set U is served by the dense scan whether or not R covers it:
+    // when R lacks one of U's DCs, every op (all carry U) is excluded
+    const bool known = !MSK || pr.uni || pr.U != 0ull;
+    k.uni = known;
+    k.noR = MSK && known && !pr.uni;
+    uint64_t r[D], sv[D], ev[D];
+    const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const bool inU = ((pr.U >> j) & 1ull) != 0ull;
+        r[j] = uniform_u64(R[i * D + j]);
+        sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
+        ev[j] = (k.sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : sv[j];  // dict read of SCT
+        sv[j] = (MSK && known && !inU) ? ~0ull : ev[j];                // compare value
+        r[j] = (MSK && known && !inU) ? ~0ull : r[j];
+    }
+    const int p = lane_id() & 3;
+    k.rA = p == 0 ? r[0] : p == 1 ? r[2] : p == 2 ? r[4] : r[6];
+    k.rB = p == 0 ? r[1] : p == 1 ? r[3] : p == 2 ? r[5] : r[7];
+    k.sA = p == 0 ? sv[0] : p == 1 ? sv[2] : p == 2 ? sv[4] : sv[6];
+    k.sB = p == 0 ? sv[1] : p == 1 ? sv[3] : p == 2 ? sv[5] : sv[7];
+    k.eA = p == 0 ? ev[0] : p == 1 ? ev[2] : p == 2 ? ev[4] : ev[6];
+    k.eB = p == 0 ? ev[1] : p == 1 ? ev[3] : p == 2 ? ev[5] : ev[7];
+}
 
 template <bool ANY_WARM, bool MSK>
 __device__ __forceinline__ Q2Key q2_prologue(const DenseArgs &a, const MaskArgs &mk, uint64_t i,
@@ -473,51 +552,10 @@ __device__ __forceinline__ Q2Key q2_prologue(const DenseArgs &a, const MaskArgs 
                                              const uint64_t *__restrict__ sct,
                                              const uint8_t *__restrict__ sct_ignore,
                                              const uint64_t *__restrict__ req_txid) {
-    constexpr int D = 8;
     Q2Key k;
-    k.i = i;
-    k.key = keys ? uniform_u64(keys[i]) : i;
-    const KeyMeta km = key_meta(k.key, key_off, key_len, key_id0);
-    k.off = km.off;
-    k.n = km.n;
-    k.id0 = km.id0;
-    const uint32_t kty =
-        byte_of(key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off), k.key);
-    k.corrupt = k.n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu);
-    const uint32_t sib =
-        ANY_WARM ? byte_of(sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R), i) : 0u;
-    k.sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
-    const uint64_t txv = uniform_u64((req_txid ? req_txid : R)[i]);
-    k.txr = req_txid ? txv : 0ull;
-    uint64_t kmw = 0, rmw = 0, smw = 0;
-    if constexpr (MSK) {
-        kmw = uniform_u64(*(mk.key_mask ? mk.key_mask + k.key : R));
-        rmw = uniform_u64(*(mk.R_mask ? mk.R_mask + i : R));
-        smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
-    }
-    const Presence<D> pr = presence<D, MSK>(mk, kmw, rmw, smw, k.n);
-    k.U = pr.U;
-    k.Rm = pr.Rm;
-    k.Sm = pr.Sm;
-    k.uni = pr.uni;
-    uint64_t r[D], sv[D], ev[D];
-    const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const bool inU = ((pr.U >> j) & 1ull) != 0ull;
-        r[j] = uniform_u64(R[i * D + j]);
-        sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
-        ev[j] = (k.sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : sv[j];  // dict read of SCT
-        sv[j] = (MSK && pr.uni && !inU) ? ~0ull : ev[j];              // compare value
-        r[j] = (MSK && pr.uni && !inU) ? ~0ull : r[j];
-    }
-    const int p = lane_id() & 3;
-    k.rA = p == 0 ? r[0] : p == 1 ? r[2] : p == 2 ? r[4] : r[6];
-    k.rB = p == 0 ? r[1] : p == 1 ? r[3] : p == 2 ? r[5] : r[7];
-    k.sA = p == 0 ? sv[0] : p == 1 ? sv[2] : p == 2 ? sv[4] : sv[6];
-    k.sB = p == 0 ? sv[1] : p == 1 ? sv[3] : p == 2 ? sv[5] : sv[7];
-    k.eA = p == 0 ? ev[0] : p == 1 ? ev[2] : p == 2 ? ev[4] : ev[6];
-    k.eB = p == 0 ? ev[1] : p == 1 ? ev[3] : p == 2 ? ev[5] : ev[7];
+    q2_meta(k, i, keys, key_off, key_len, key_id0);
+    const uint64_t kmw = MSK ? key_word(mk, k.key, key_off) : 0ull;
+    q2_side<ANY_WARM, MSK>(k, a, mk, kmw, key_off, key_type, R, sct, sct_ignore, req_txid);
     return k;
 }
 
@@ -535,10 +573,10 @@ __device__ __forceinline__ void q2_fold(const Q2Key &k, const Q8Chunk &c, uint64
     const uint64_t *tx = k.txr ? log_txid : nullptr;
     if (ANY_WARM && !k.sct_ign)
         q8_fold<true>(c, tx, k.txr, k.off, b, k.n, n_entries, k.rA, k.rB, k.sA, k.sB, s.ctA, s.ctB,
-                      s.sum, s.cnt, s.first_excl, s.first_err);
+                      s.sum, s.cnt, s.first_excl, s.first_err, k.noR);
     else
         q8_fold<false>(c, tx, k.txr, k.off, b, k.n, n_entries, k.rA, k.rB, k.sA, k.sB, s.ctA,
-                       s.ctB, s.sum, s.cnt, s.first_excl, s.first_err);
+                       s.ctB, s.sum, s.cnt, s.first_excl, s.first_err, k.noR);
 }
 
 template <bool ANY_WARM>
@@ -551,11 +589,11 @@ __device__ __forceinline__ void q2_rest(const Q2Key &k, const uint64_t *__restri
     if (ANY_WARM && !k.sct_ign)
         scan_key_q8<true, true, false, true>(oc, eff, tx, k.txr, k.off, k.n, n_entries, k.rA, k.rB,
                                              k.sA, k.sB, s.ctA, s.ctB, s.sum, s.cnt, s.first_excl,
-                                             s.first_err);
+                                             s.first_err, k.noR);
     else
         scan_key_q8<false, true, false, true>(oc, eff, tx, k.txr, k.off, k.n, n_entries, k.rA,
                                               k.rB, k.sA, k.sB, s.ctA, s.ctB, s.sum, s.cnt,
-                                              s.first_excl, s.first_err);
+                                              s.first_excl, s.first_err, k.noR);
 }
 
 // A mixed key of a sparse batch (MSK, !uni): the per-entry-mask scan, lane =
@@ -579,7 +617,7 @@ __device__ __forceinline__ void q2_msk(const Q2Key &k, const uint64_t *__restric
 }
 
 template <bool MSK>
-__device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
+__device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s, uint32_t hints,
                                             const uint32_t *__restrict__ op_id,
                                             const int64_t *__restrict__ base_value,
                                             int64_t *__restrict__ o_value,
@@ -638,9 +676,13 @@ __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s,
         o_value[i] = (int64_t)((uint64_t)base + (uint64_t)total);
         o_hole[i] = hole;
         o_count[i] = s.cnt;
-        o_flags[i] = fl;
         o_err[i] = s.first_err >= 0 ? (uint32_t)(k.off + (uint64_t)s.first_err) : 0xffffffffu;
-        if (MSK && o_mask) o_mask[i] = mo;
+        // AGN_HINT_CT_FLAG: a LastOpCt over every column is a flag bit, not a
+        // mask word (one store stream less per request)
+        const bool full = MSK && (hints & AGN_HINT_CT_FLAG) && mo == 0xFFull;
+        if (full) fl |= AGN_F_CT_FULL;
+        o_flags[i] = fl;
+        if (MSK && o_mask && !full) o_mask[i] = mo;
     }
 }
 
@@ -688,11 +730,115 @@ __global__ __launch_bounds__(64) void k_counter_quad2(
                 q2_msk<ANY_WARM>(k1, oc, mk.oc_mask, eff, log_txid, a.n_entries, s1);
         }
     }
-    q2_epilogue<MSK>(k0, s0, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err,
+    q2_epilogue<MSK>(k0, s0, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags, o_err,
                      mk.o_mask);
     if (two)
-        q2_epilogue<MSK>(k1, s1, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags,
+        q2_epilogue<MSK>(k1, s1, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags,
                          o_err, mk.o_mask);
+}
+
+// ROWS_QUAD with the first chunk EARLY (D = 8, one request per wave; the
+// sparse batches, MSK): the key's segment metadata (key_off, key_len,
+// key_id0) is the only scalar round trip before the rows -- chunk 0's quad
+// rows and effects are issued as soon as it lands, and R, SCT, the side
+// bytes, the TxId and the mask words load under them.  In k_counter_key all
+// of those share the metadata's round trip, and scalar loads return out of
+// order, so the first row load waits for the slowest of them (lgkmcnt(0)).
+// A key whose DC set U is known (agn_log.key_mask) is served by the dense
+// scan, also when R lacks one of U's DCs (every op excluded, :245-247); a key
+// whose entries carry different DC sets is appended to `list` for
+// k_counter_q8m, so this kernel holds no per-entry-mask scan (inlined, it
+// cost 73-98 VGPRs: 4-6 waves per SIMD, or spills at a 7-wave cap;
+// profiles/r04/ab_masked_*.log).  KM: the key's DC set loads with the
+// segment metadata (1) or under the chunk (0).  Same results as
+// k_counter_key.
+template <bool ANY_WARM, bool KEYS, int KM>
+__global__ __launch_bounds__(64) void k_counter_q8e(
+    DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
+    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
+    const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
+    const uint64_t *__restrict__ oc, const uint32_t *__restrict__ op_id,
+    const int64_t *__restrict__ eff, const uint64_t *__restrict__ log_txid,
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ sct,
+    const uint8_t *__restrict__ sct_ignore, const uint64_t *__restrict__ req_txid,
+    const int64_t *__restrict__ base_value, int64_t *__restrict__ o_value,
+    int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
+    uint32_t *__restrict__ o_err, uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
+    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint64_t i = uniform_u64((uint64_t)blk);
+    if (i >= a.n_req) return;
+    Q2Key k;
+    q2_meta(k, i, KEYS ? keys : nullptr, key_off, key_len, key_id0);
+    // a key whose entries carry different DC sets: k_counter_q8m's
+    auto mixed = [&](uint64_t kmw) {
+        return !(mk.oc_mask == nullptr || (mk.key_mask && (kmw & 0xFFull)) || k.n == 0);
+    };
+    auto hand_on = [&]() {
+        if (lane_id() == 0) list[atomicAdd(list_n, 1u)] = (uint32_t)i;
+    };
+    uint64_t kmw = 0;
+    if constexpr (KM == 1) {
+        kmw = key_word(mk, k.key, key_off);
+        if (mixed(kmw)) {
+            hand_on();
+            return;
+        }
+    }
+    const bool any = a.n_entries != 0;
+    Q8Chunk c0{};
+    if (any) c0 = q8_load<true, false>(oc, eff, k.off, 0, a.n_entries);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KM == 0) kmw = key_word(mk, k.key, key_off);
+    q2_side<ANY_WARM, true>(k, a, mk, kmw, key_off, key_type, R, sct, sct_ignore, req_txid);
+    if (KM == 0 && mixed(kmw)) {
+        hand_on();
+        return;
+    }
+    Q2Acc s;
+    s.ctA = k.eA;
+    s.ctB = k.eB;
+    if (any && !k.corrupt) {
+        q2_fold<ANY_WARM>(k, c0, 0, log_txid, a.n_entries, s);
+        q2_rest<ANY_WARM>(k, oc, eff, log_txid, a.n_entries, s);
+    }
+    q2_epilogue<true>(k, s, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count, o_flags,
+                      o_err, mk.o_mask);
+}
+
+// The keys k_counter_q8e handed on (entries with different DC sets): the
+// per-entry-mask quad scan (scan_key_q8_msk), one request per wave, the
+// waves striding over the list -- the grid does not know the list's length,
+// and an empty list costs one short launch.
+template <bool ANY_WARM, bool KEYS>
+__global__ __launch_bounds__(64) void k_counter_q8m(
+    DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
+    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
+    const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
+    const uint64_t *__restrict__ oc, const uint32_t *__restrict__ op_id,
+    const int64_t *__restrict__ eff, const uint64_t *__restrict__ log_txid,
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ sct,
+    const uint8_t *__restrict__ sct_ignore, const uint64_t *__restrict__ req_txid,
+    const int64_t *__restrict__ base_value, int64_t *__restrict__ o_value,
+    int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
+    uint32_t *__restrict__ o_err, const uint32_t *__restrict__ list,
+    const uint32_t *__restrict__ list_n) {
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(*list_n);
+    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
+        const uint64_t i = __builtin_amdgcn_readfirstlane(list[j]);
+        const Q2Key k = q2_prologue<ANY_WARM, true>(a, mk, i, KEYS ? keys : nullptr, key_off,
+                                                    key_len, key_type, key_id0, R, sct, sct_ignore,
+                                                    req_txid);
+        Q2Acc s;
+        s.ctA = k.eA;
+        s.ctB = k.eB;
+        if (a.n_entries != 0 && !k.corrupt)
+            q2_msk<ANY_WARM>(k, oc, mk.oc_mask, eff, log_txid, a.n_entries, s);
+        q2_epilogue<true>(k, s, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count,
+                          o_flags, o_err, mk.o_mask);
+    }
 }
 
 MaskArgs mask_args(const agn_log &log, const agn_read &req, const agn_result &out) {
@@ -710,7 +856,7 @@ inline bool sparse_batch(const agn_log &log, const agn_read &req, const agn_resu
 }
 
 int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u};
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u, req.hints};
     const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + 1) / 2;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
@@ -732,6 +878,60 @@ int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out,
 #undef AGN_Q2L
     AGN_HIP(hipGetLastError());
     return AGN_OK;
+}
+
+// Sparse batches (D = 8, quad rows) run k_counter_q8e + k_counter_q8m,
+// unless AGN_COUNTER_EARLY=0 (A/B knob: k_counter_key).  AGN_Q8E_KM=0 loads
+// the key's DC set under the first chunk instead of with the metadata.
+inline bool early_chunk() {
+    const char *v = getenv("AGN_COUNTER_EARLY");
+    return !(v && v[0] == '0');
+}
+
+int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u, req.hints};
+    const MaskArgs mk = mask_args(log, req, out);
+    if (req.n_req > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
+                                               (unsigned long long)req.n_req);
+    const char *kv = getenv("AGN_Q8E_KM");
+    const bool km0 = kv && kv[0] == '0';
+    uint32_t *lst = nullptr;  // [0] = count, then the handed-on request indices
+    AGN_HIP(pool_malloc(&lst, (req.n_req + 1) * sizeof(uint32_t), st));
+    int rc = AGN_OK;
+    if (hipMemsetAsync(lst, 0, sizeof(uint32_t), st) != hipSuccess)
+        rc = fail(AGN_EHIP, "counter q8e: list reset");
+#define AGN_ARGS                                                                                \
+    a, mk, req.keys, log.key_off, log.key_len, log.key_type, id0_index(log), log.oc, log.op_id,  \
+        log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,  \
+        out.hole, out.lastct, out.count, out.flags, out.err_pos, lst + 1, lst
+#define AGN_Q8E_(W, K, KM)                                                                      \
+    hipLaunchKernelGGL((k_counter_q8e<W, K, KM>), dim3((unsigned)req.n_req), dim3(64), 0, st,   \
+                       AGN_ARGS)
+#define AGN_Q8E(W, K)                                                                           \
+    do {                                                                                        \
+        if (km0) AGN_Q8E_(W, K, 0);                                                             \
+        else AGN_Q8E_(W, K, 1);                                                                 \
+    } while (0)
+    const unsigned mb = (unsigned)(req.n_req < 16384 ? req.n_req : 16384);
+#define AGN_Q8M(W, K)                                                                           \
+    hipLaunchKernelGGL((k_counter_q8m<W, K>), dim3(mb), dim3(64), 0, st, AGN_ARGS)
+    if (rc == AGN_OK) {
+        if (req.sct) {
+            if (req.keys) { AGN_Q8E(true, true); AGN_Q8M(true, true); }
+            else { AGN_Q8E(true, false); AGN_Q8M(true, false); }
+        } else {
+            if (req.keys) { AGN_Q8E(false, true); AGN_Q8M(false, true); }
+            else { AGN_Q8E(false, false); AGN_Q8M(false, false); }
+        }
+        if (hipGetLastError() != hipSuccess) rc = fail(AGN_EHIP, "counter q8e: launch");
+    }
+#undef AGN_Q8M
+#undef AGN_Q8E
+#undef AGN_Q8E_
+#undef AGN_ARGS
+    const hipError_t ef = hipFreeAsync(lst, st);
+    if (rc == AGN_OK && ef != hipSuccess) rc = fail(AGN_EHIP, "hipFreeAsync: %s", hipGetErrorString(ef));
+    return rc;
 }
 
 // Two chunks per step for D <= 4 (scan_key PAIR), unless AGN_COUNTER_PAIR=0
@@ -832,8 +1032,10 @@ int launch_var(int v, const agn_log &log, const agn_read &req, const agn_result 
     if constexpr (D % 2 == 0 && !MSK)
         if (v == ROWS_GLDS) return launch_key_g<D, WPB, ROWS_GLDS, false>(log, req, out, st);
     if constexpr (D == 8)
-        if (v == ROWS_QUAD || (MSK && v == ROWS_GLDS))
+        if (v == ROWS_QUAD || (MSK && v == ROWS_GLDS)) {
+            if (MSK && WPB == 1 && early_chunk()) return launch_q8e(log, req, out, st);
             return launch_key_g<D, WPB, ROWS_QUAD, MSK>(log, req, out, st);
+        }
     return launch_key_g<D, WPB, ROWS_VGPR, MSK>(log, req, out, st);
 }
 

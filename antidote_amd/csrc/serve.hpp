@@ -15,9 +15,11 @@ int launch_ss_store_req(const agn_ss_cache &c, const uint64_t *key_off, const ui
                         uint8_t *prune_req, uint64_t *thr, uint64_t *thrm, hipStream_t st);
 
 // agn_ss_state_compact's kernel: the live states into new_tag / new_tok
-// (state_ctl reset, then the live pairs; *ovf = 1 if they do not fit).
+// (state_ctl reset, then the live pairs; *ovf = 1 if they do not fit).  The
+// slots' rewritten references go to c.value, or -- new_value given, [n_keys
+// * slots] -- there, for the caller to commit only when *ovf stayed 0.
 int launch_ss_compact(const agn_ss_cache &c, uint32_t *new_tag, uint64_t *new_tok, uint64_t new_cap,
-                      uint64_t *ovf, hipStream_t st);
+                      uint64_t *ovf, hipStream_t st, int64_t *new_value = nullptr);
 
 // prune_ops in place over a key list (entry i: key keys[i], GC'd iff
 // flags[i] != 0); meta[6][n] per entry.

@@ -224,7 +224,21 @@ class Engine:
         return d
 
     def fetch_result(self, d: DeviceArrays, stream=None) -> ResultArrays:
+        """The results in host arrays; a request flagged AGN_F_CT_FULL (a
+        batch with AGN_HINT_CT_FLAG) gets its LastOpCt mask back -- every
+        column -- and the flag is cleared, so results compare as without the
+        hint."""
         get = {n: self.download(d.bufs[n], *d.shapes[n], stream=stream) for n in d.shapes}
+        full = (get["flags"] & _abi.F_CT_FULL) != 0
+        if full.any():
+            D = get["lastct"].shape[1]
+            if get.get("lastct_mask") is not None:
+                row = np.zeros(get["lastct_mask"].shape[1], np.uint64)
+                for w in range(row.size):
+                    bits = min(64, D - 64 * w)
+                    row[w] = np.uint64((1 << bits) - 1) if bits > 0 else np.uint64(0)
+                get["lastct_mask"][full] = row
+            get["flags"] &= np.uint32(~_abi.F_CT_FULL & 0xFFFFFFFF)
         return ResultArrays(value=get["value"], hole=get["hole"], lastct=get["lastct"],
                             lastct_mask=get.get("lastct_mask"), count=get["count"],
                             flags=get["flags"], err_pos=get["err_pos"], out_off=get.get("out_off"),
@@ -442,8 +456,10 @@ class Batcher:
         self.close()
 
     def read(self, key, R, R_mask=None, sct=None, sct_mask=None, txid=0, base_value=0,
-             base_tag=None, base_tok=None, out_cap=0, gc=False):
-        """One read/6; returns a dict of the key's result."""
+             base_tag=None, base_tok=None, out_cap=0, gc=False, capacity_ok=False):
+        """One read/6; returns a dict of the key's result.  capacity_ok: an
+        AGN_ECAPACITY (the state did not fit out_cap) returns the result with
+        "ecapacity": True and out_n = the pairs needed, instead of raising."""
         D = self.oplog.n_dcs
         W = n_words(D)
         arr = lambda a: None if a is None else np.ascontiguousarray(a, np.uint64)  # noqa: E731
@@ -462,7 +478,10 @@ class Batcher:
         o = _abi.AgnKeyResult()
         o.lastct, o.lastct_mask, o.out_cap = ct.ctypes.data, ctm.ctypes.data, out_cap
         o.out_tag, o.out_tok = otag.ctypes.data, otok.ctypes.data
-        check(self.lib.agn_batcher_read(self.h, C.byref(rd), C.byref(o)), "agn_batcher_read")
+        rc = self.lib.agn_batcher_read(self.h, C.byref(rd), C.byref(o))
+        if rc == _abi.ECAPACITY and capacity_ok:
+            return {"ecapacity": True, "out_n": o.out_n, "status": o.status}
+        check(rc, "agn_batcher_read")
         return {"value": o.value, "hole": o.hole, "lastct": ct, "lastct_mask": ctm,
                 "count": o.count, "flags": o.flags, "err_pos": o.err_pos, "out_n": o.out_n,
                 "status": o.status,
@@ -472,6 +491,27 @@ class Batcher:
         b, r = C.c_uint64(), C.c_uint64()
         check(self.lib.agn_batcher_stats(self.h, C.byref(b), C.byref(r)))
         return {"batches": b.value, "reads": r.value}
+
+    def state_bound(self, key) -> int:
+        """agn_batcher_state_bound: pairs of the largest cached state of key."""
+        n = C.c_uint32()
+        check(self.lib.agn_batcher_state_bound(self.h, key, C.byref(n)), "agn_batcher_state_bound")
+        return n.value
+
+    def store(self, key, clock, clock_mask=None, last_op=0, count=0, value=0, tags=None,
+              toks=None, gc=True):
+        """agn_batcher_store: materialize_snapshot's store of a snapshot the
+        caller materialized from the log (get_from_snapshot_log)."""
+        clock = np.ascontiguousarray(clock, np.uint64)
+        cm = None if clock_mask is None else np.ascontiguousarray(np.atleast_1d(clock_mask),
+                                                                   np.uint64)
+        tg = None if tags is None else np.ascontiguousarray(tags, np.uint32)
+        tk = None if toks is None else np.ascontiguousarray(toks, np.uint64)
+        n = 0 if tg is None else len(tg)
+        check(self.lib.agn_batcher_store(self.h, key, _ptr(clock), _ptr(cm), int(last_op),
+                                         int(count), int(value), n, _ptr(tg) if n else None,
+                                         _ptr(tk) if n else None,
+                                         _abi.READ_GC if gc else 0), "agn_batcher_store")
 
 
 def gen_host(cfg: _abi.AgnGenCfg):

@@ -172,20 +172,21 @@ def algorithmic_bytes_survey(cfg, n_keys, n_rem=0, n_live=0):
     return ops * (8 * D + 20) + 8 * n_rem + 12 * n_live + n_keys * (32 + 16 * D)
 
 
-def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0, mask_keys=0, mask_ops=0):
+def algorithmic_bytes(cfg, n_keys, n_rem=0, n_live=0, mask_words=0, mask_ops=0):
     """HBM bytes one materialize launch must move.
-    Presence masks (--sparse) add per request its key's DC set, R's mask word
-    and the LastOpCt mask word (mask_keys requests), and the per-entry mask
-    word of the keys whose entries differ (mask_ops entries)."""
+    Presence masks (--sparse) add the per-request mask words (mask_words: the
+    key's DC set, R's mask word, the LastOpCt mask word -- the latter two
+    unless a hint spares them) and the per-entry mask word of the keys whose
+    entries differ (mask_ops entries)."""
     D, N = cfg["n_dcs"], cfg["ops_per_key"]
     ops = n_keys * N
     if cfg["crdt_type"] == 1:
         per_op = 8 * D + 8                    # OpSSCommit row + effect
         per_key = 8 + 8 * D + 8 * D + 32      # key_off, R, LastOpCt, value/hole/count/flags/err/op_id
-        return ops * per_op + n_keys * per_key + 24 * mask_keys + 8 * mask_ops
+        return ops * per_op + n_keys * per_key + 8 * mask_words + 8 * mask_ops
     per_op = 8 * D + 4 + 4 + 8 + 4            # oc, op_id, tag, add_tok, rem_off
     per_key = 8 + 8 * D + 8 * D + 24 + 8 + 4  # key_off, R, LastOpCt, hole/count/flags/err, out_off, out_n
-    return (ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key + 24 * mask_keys +
+    return (ops * per_op + 8 * n_rem + 12 * n_live + n_keys * per_key + 8 * mask_words +
             8 * mask_ops)
 
 
@@ -384,12 +385,19 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
         kmask = eng.index_masks(dl, sp)
         km = eng.download(kmask, np.uint64, (n_keys,), stream=sp)
         mixed = int((km == 0).sum())
+        # the promises the read batcher makes for such a batch (agn_read.hints):
+        # R masks that carry every DC are not read, a LastOpCt over every
+        # column comes back as AGN_F_CT_FULL instead of a mask word
+        r_full = not a.sparse.startswith("subset")
+        dr.hints = _abi.HINT_CT_FLAG | (_abi.HINT_R_FULL if r_full else 0)
         # counter_pn reads a mask per entry only for the keys whose entries
         # differ (agn_log.key_mask); the set/register kernel reads every one
         per_entry = mixed if cfg["crdt_type"] == 1 else n_keys
         presence = {"mode": a.sparse, "key_mask": "agn_log_index_masks",
                     "uniform_keys": n_keys - mixed, "mixed_keys": mixed,
-                    "mask_ops": per_entry * cfg["ops_per_key"]}
+                    "mask_ops": per_entry * cfg["ops_per_key"],
+                    "hints": ["AGN_HINT_CT_FLAG"] + (["AGN_HINT_R_FULL"] if r_full else []),
+                    "r_full": r_full}
     res = eng.alloc_result(n_keys, cfg["n_dcs"], sparse=bool(a.sparse), cap_off=cap)
 
     def barrier():
@@ -453,8 +461,16 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
 
     ops_step = n_keys * cfg["ops_per_key"] * world
     value = ops_step * a.steps / elapsed
-    bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live,
-                                     n_keys if presence else 0,
+    mask_words = 0
+    if presence:
+        # per request: the key's DC set; R's mask word unless AGN_HINT_R_FULL
+        # (the general kernel over the mixed keys reads it anyway); the
+        # LastOpCt mask word unless the result carries AGN_F_CT_FULL
+        ct_full = int(((flags & np.uint32(_abi.F_CT_FULL)) != 0).sum())
+        presence["ct_full_keys"] = ct_full
+        mask_words = n_keys + (presence["mixed_keys"] if presence["r_full"] else n_keys) + \
+            (n_keys - ct_full)
+    bytes_launch = algorithmic_bytes(cfg, n_keys, n_rem, n_live, mask_words,
                                      presence["mask_ops"] if presence else 0)
     bytes_survey = algorithmic_bytes_survey(cfg, n_keys, n_rem, n_live)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9

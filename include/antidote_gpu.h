@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AGN_ABI_VERSION 4
+#define AGN_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 #define AGN_OK 0
@@ -74,6 +74,10 @@ extern "C" {
 #define AGN_F_ERR_UNEXPECTED 0x4u /* {error,{unexpected_operation,Op,Type}}      */
 #define AGN_F_ERR_CORRUPTED 0x8u  /* erlang:error(corrupted_ops_cache)           */
 #define AGN_F_ERR_CAPACITY 0x10u  /* a per-key device table overflowed            */
+/* ABI v5: LastOpCt carries every column of the partition (its dict has all n_dcs
+ * DCs); set only for requests of a batch with AGN_HINT_CT_FLAG, and then
+ * lastct_mask[i] is NOT written (the mask is the n_dcs low bits) */
+#define AGN_F_CT_FULL 0x20u
 
 /* ---- op log (device or host pointers, same layout) -------------------- */
 typedef struct agn_log {
@@ -132,7 +136,9 @@ typedef struct agn_read {
     const uint8_t *sct_ignore;  /* [n_req] 1 = ignore (with sct != NULL), NULL = none ignored */
     const uint64_t *txid;       /* [n_req] reading TxId (0 = ignore) or NULL = all ignore */
     uint32_t req_type;          /* Type argument of materialize/4 */
-    uint32_t _pad;
+    uint32_t hints;             /* ABI v5 (was padding; 0 = none): AGN_HINT_* promises
+                                   about this batch that let a kernel skip loads /
+                                   stores of presence words */
     /* base snapshot value (#materialized_snapshot.value) */
     const int64_t *base_value;  /* counter: [n_req] or NULL (= 0, Type:new());
                                    set/register with base_off NULL: [n_req]
@@ -144,12 +150,23 @@ typedef struct agn_read {
     const uint64_t *base_tok;   /* token */
 } agn_read;
 
+/* agn_read.hints.  AGN_HINT_R_FULL: every R_mask[i] carries all n_dcs DCs (the
+ * caller checked; the masks are then not read).  AGN_HINT_CT_FLAG: the caller
+ * reads lastct_mask through AGN_F_CT_FULL (a request whose LastOpCt carries
+ * every column gets the flag instead of its mask word; see agn_result).  The
+ * read batcher sets both from the requests it packs.  Kernels may ignore a
+ * hint (then the mask is loaded / written as without it). */
+#define AGN_HINT_R_FULL 0x1u
+#define AGN_HINT_CT_FLAG 0x2u
+
 /* ---- results ----------------------------------------------------------- */
 typedef struct agn_result {
     int64_t *value;           /* counter: [n_req] materialized value */
     int64_t *hole;            /* [n_req] NewLastOp (1 - id of the oldest excluded op) */
     uint64_t *lastct;         /* [n_req * D] LastOpCt */
-    uint64_t *lastct_mask;    /* [n_req * W] or NULL when inputs are dense */
+    uint64_t *lastct_mask;    /* [n_req * W] or NULL when inputs are dense; with
+                                 AGN_HINT_CT_FLAG not written for a request whose
+                                 flags carry AGN_F_CT_FULL */
     uint32_t *count;          /* [n_req] number of effects applied */
     uint32_t *flags;          /* [n_req] AGN_F_* */
     uint32_t *err_pos;        /* [n_req] entry index (global) of the failing op, or UINT32_MAX */
@@ -351,7 +368,11 @@ typedef struct agn_key_result { /* caller-owned host memory */
     int64_t value, hole;
     uint64_t *lastct;           /* [D] */
     uint64_t *lastct_mask;      /* [W] or NULL (then the batch must be dense) */
-    uint32_t count, flags, err_pos;
+    uint32_t count, flags;
+    uint32_t err_pos;           /* AGN_F_ERR_UNEXPECTED: the op id (agn_oplog_append's
+                                   out_op_id) of the failing op -- the op whose effect
+                                   {error,{unexpected_operation,Op,Type}} names -- else
+                                   UINT32_MAX (ABI v5; was its slot in the log) */
     uint32_t out_cap;           /* set/register: room in out_tag / out_tok */
     uint32_t out_n;             /* live pairs (> out_cap => AGN_ECAPACITY) */
     uint32_t status;            /* cached mode: AGN_SS_HIT / AGN_SS_NEW, or AGN_SS_LOG (no
@@ -377,6 +398,33 @@ int agn_batcher_stats(agn_batcher *b, uint64_t *batches, uint64_t *reads);
  * LOG.  Reads of one key are applied in arrival order. */
 int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch,
                               uint32_t max_wait_us, agn_batcher **out);
+/* ABI v5, cached set_aw / register_mv batchers: *pairs = an upper bound of the
+ * pairs of any state the partition's snapshot cache holds for `key` (the
+ * largest state the batcher has returned for it; 0 otherwise).  A read whose
+ * out_cap is the key's length (agn_oplog_key_meta) + this bound cannot get
+ * AGN_ECAPACITY from its cached base.  Not part of the reference's API (the
+ * ETS read copies terms of any size). */
+int agn_batcher_state_bound(agn_batcher *b, uint64_t key, uint32_t *pairs);
+/* ABI v5, cached batchers: materialize_snapshot's store (:466-509) of a
+ * snapshot the caller materialized itself -- the read whose cache held no
+ * snapshot <= its clock (agn_key_result.status AGN_SS_LOG) and which the
+ * caller served from the log (get_from_snapshot_log :416-419 ->
+ * logging_vnode:get_up_to_time -> materialize/4, e.g. agn_materialize_host).
+ * Such a response is never the newest snapshot (is_newest_snapshot = false,
+ * src/logging_vnode.erl:538-540), so only a GC read stores it: flags =
+ * AGN_READ_GC (op_insert_gc's GC read, :640) runs internal_store_ss /
+ * insert_bigger / snapshot_insert_gc (:341-364, 513-563) on the device cache
+ * and prune_ops of the key when it collects, exactly as a GC read served from
+ * the cache does; flags = 0 stores nothing (the reference's ShouldRefreshCache
+ * is false for it).  Call it only when the materialize returned ok with a
+ * LastOpCt other than ignore and the log response had ops (:466-484).  clock
+ * [D] (+ clock_mask [W], NULL = every DC) = LastOpCt, last_op = NewLastOp,
+ * count = ops applied, value = counter_pn value, or n_pairs / tags / toks =
+ * the set_aw / register_mv state (host arrays, the result layout).  Runs in
+ * arrival order with the batcher's reads; blocks. */
+int agn_batcher_store(agn_batcher *b, uint64_t key, const uint64_t *clock,
+                      const uint64_t *clock_mask, int64_t last_op, uint32_t count, int64_t value,
+                      uint32_t n_pairs, const uint32_t *tags, const uint64_t *toks, uint32_t flags);
 
 /* ---- exact term interning (the Erlang binding's term <-> integer maps) ----
  * Host-only.  The device log holds DC ids, keys, TxIds, set elements /

@@ -31,6 +31,9 @@
  *       before the insert as the reference does
  *   part_gc(Part, Key, ThresholdPairs) -> ok
  *       snapshot_insert_gc's prune_ops + resize for one key (agn_oplog_prune)
+ *   part_store(Part, Key, CommitTimePairs, NewLastOp, Count, Value, Gc) -> ok
+ *       materialize_snapshot's store of a snapshot served from the log
+ *       (agn_batcher_store; Gc = true: op_insert_gc's GC read)
  *   part_stats(Part) -> {Entries, Slots, Tokens}
  *   part_key_meta(Part, Key) -> {Length, ListLen, OpId}
  *   Keys, DC ids, TxIds, elements / values and tokens are interned exactly
@@ -94,7 +97,65 @@ typedef struct {
     pthread_mutex_t gc_mu;
     uint8_t *d_prune;
     uint64_t *d_thr, *d_thrm;
+    /* the original effect term (external format) of every op whose effect the
+     * engine could not encode (an invalid entry), by (key, op id): a read that
+     * includes it returns {error, {unexpected_operation, Effect, Type}} with
+     * that term, as materializer:update_snapshot/3 (src/materializer.erl:51-58) */
+    pthread_mutex_t inv_mu;
+    struct inv_op {
+        uint64_t key;
+        uint32_t id;
+        ErlNifBinary eff;
+    } *inv;
+    size_t n_inv, cap_inv;
 } part_res;
+
+static const char *type_name(uint32_t type) {
+    switch (type) {
+        case AGN_COUNTER_PN: return "antidote_crdt_counter_pn";
+        case AGN_SET_AW: return "antidote_crdt_set_aw";
+        case AGN_REGISTER_MV: return "antidote_crdt_register_mv";
+    }
+    return "undefined";
+}
+
+/* keep the effect term of an invalid op (one writer: the vnode) */
+static int inv_put(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t id, ERL_NIF_TERM eff) {
+    ErlNifBinary b;
+    if (!enif_term_to_binary(env, eff, &b)) return AGN_ENOMEM;
+    pthread_mutex_lock(&p->inv_mu);
+    if (p->n_inv == p->cap_inv) {
+        const size_t c = p->cap_inv ? 2 * p->cap_inv : 16;
+        struct inv_op *n = enif_realloc(p->inv, c * sizeof *n);
+        if (!n) {
+            pthread_mutex_unlock(&p->inv_mu);
+            enif_release_binary(&b);
+            return AGN_ENOMEM;
+        }
+        p->inv = n;
+        p->cap_inv = c;
+    }
+    p->inv[p->n_inv].key = key;
+    p->inv[p->n_inv].id = id;
+    p->inv[p->n_inv].eff = b;
+    p->n_inv++;
+    pthread_mutex_unlock(&p->inv_mu);
+    return AGN_OK;
+}
+
+/* the effect term of op `id` of `key`, or 'undefined' */
+static ERL_NIF_TERM inv_get(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t id) {
+    ERL_NIF_TERM out = enif_make_atom(env, "undefined");
+    pthread_mutex_lock(&p->inv_mu);
+    for (size_t i = p->n_inv; i-- > 0;)
+        if (p->inv[i].key == key && p->inv[i].id == id) {
+            if (!enif_binary_to_term(env, p->inv[i].eff.data, p->inv[i].eff.size, &out, 0))
+                out = enif_make_atom(env, "undefined");
+            break;
+        }
+    pthread_mutex_unlock(&p->inv_mu);
+    return out;
+}
 
 static void part_dtor(ErlNifEnv *env, void *obj) {
     (void)env;
@@ -112,6 +173,9 @@ static void part_dtor(ErlNifEnv *env, void *obj) {
     agn_interner_destroy(p->tags);
     agn_interner_destroy(p->toks);
     pthread_mutex_destroy(&p->gc_mu);
+    for (size_t i = 0; i < p->n_inv; ++i) enif_release_binary(&p->inv[i].eff);
+    enif_free(p->inv);
+    pthread_mutex_destroy(&p->inv_mu);
     if (p->ctx) enif_release_resource(p->ctx);
 }
 
@@ -394,6 +458,7 @@ static ERL_NIF_TERM nif_part_open(ErlNifEnv *env, int argc, const ERL_NIF_TERM a
     part_res *p = enif_alloc_resource(PART_RES, sizeof *p);
     memset(p, 0, sizeof *p);
     pthread_mutex_init(&p->gc_mu, NULL);
+    pthread_mutex_init(&p->inv_mu, NULL);
     p->type = type;
     p->D = D;
     p->W = (D + 63) / 64;
@@ -562,7 +627,7 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     enif_free(E);
     enif_free(oc);
     enif_free(ocm);
-    (void)invalid;
+    if (!rc && invalid) rc = inv_put(env, p, k, ids[0], argv[4]);
     if (rc) return error_tuple(env, rc);
     return enif_make_tuple3(env, atom(env, "ok"), enif_make_uint(env, ids[0]),
                             atom(env, due[0] ? "true" : "false"));
@@ -592,14 +657,18 @@ static ERL_NIF_TERM state_term(ErlNifEnv *env, part_res *p, uint32_t n, const ui
     return l;
 }
 
-static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, const agn_key_result *o,
-                                const uint64_t *ct, const uint64_t *ctm) {
-    if (o->flags & AGN_F_ERR_CORRUPTED) return enif_make_tuple2(env, atom(env, "error"), atom(env, "corrupted_ops_cache"));
+static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, uint64_t key,
+                                const agn_key_result *o, const uint64_t *ct, const uint64_t *ctm) {
+    /* erlang:error(corrupted_ops_cache) (src/clocksi_materializer.erl:190-191) */
+    if (o->flags & AGN_F_ERR_CORRUPTED)
+        return enif_raise_exception(env, atom(env, "corrupted_ops_cache"));
+    /* {error, {unexpected_operation, Op, Type}} (src/materializer.erl:51-58),
+     * Op = the effect term the vnode was given; err_pos = the op's id */
     if (o->flags & AGN_F_ERR_UNEXPECTED)
         return enif_make_tuple2(env, atom(env, "error"),
                                 enif_make_tuple3(env, atom(env, "unexpected_operation"),
-                                                 atom(env, "invalid_effect"),
-                                                 enif_make_uint(env, p->type)));
+                                                 inv_get(env, p, key, o->err_pos),
+                                                 atom(env, type_name(p->type))));
     ERL_NIF_TERM v = p->type == AGN_COUNTER_PN ? enif_make_int64(env, o->value)
                                                : state_term(env, p, o->out_n, o->out_tag, o->out_tok);
     ERL_NIF_TERM lct = (o->flags & AGN_F_CT_IGNORE) ? atom(env, "ignore") : clock_pairs(env, p, ct, ctm);
@@ -607,6 +676,68 @@ static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, const agn_key_resul
                            atom(env, (o->flags & AGN_F_NEWSS) ? "true" : "false"),
                            enif_make_uint(env, o->count)};
     return enif_make_tuple_from_array(env, res, 6);
+}
+
+/* a set_aw orddict [{Elem, [Tok]}] / register_mv [{V, Tok}] -> interned
+ * (tag, token) pairs in the result layout (enif_alloc'ed; NULL when empty);
+ * AGN_EINVAL for a malformed term */
+static int state_pairs(ErlNifEnv *env, part_res *p, ERL_NIF_TERM st, uint32_t *n_out,
+                       uint32_t **tags_out, uint64_t **toks_out) {
+    unsigned nl = 0;
+    *n_out = 0;
+    *tags_out = NULL;
+    *toks_out = NULL;
+    if (!enif_get_list_length(env, st, &nl)) return AGN_EINVAL;
+    ERL_NIF_TERM h, t = st;
+    uint32_t cap = 0;
+    while (enif_get_list_cell(env, t, &h, &t)) {
+        int ar;
+        const ERL_NIF_TERM *tp;
+        unsigned m = 1;
+        if (!enif_get_tuple(env, h, &ar, &tp) || ar != 2) return AGN_EINVAL;
+        if (p->type == AGN_SET_AW && !enif_get_list_length(env, tp[1], &m)) return AGN_EINVAL;
+        cap += m;
+    }
+    uint32_t *tg = enif_alloc(4 * (cap + 1));
+    uint64_t *tk = enif_alloc(8 * (cap + 1));
+    if (!tg || !tk) {
+        enif_free(tg);
+        enif_free(tk);
+        return AGN_ENOMEM;
+    }
+    uint32_t n = 0;
+    for (t = st; enif_get_list_cell(env, t, &h, &t);) {
+        int ar;
+        const ERL_NIF_TERM *tp;
+        uint64_t id_tag, id_tok;
+        enif_get_tuple(env, h, &ar, &tp);
+        int rc = term_id(env, p->tags, tp[0], &id_tag);
+        if (p->type == AGN_REGISTER_MV) {
+            if (!rc) rc = term_id(env, p->toks, tp[1], &id_tok);
+            if (!rc) {
+                tg[n] = (uint32_t)id_tag;
+                tk[n++] = id_tok;
+            }
+        } else {
+            ERL_NIF_TERM th, tt = tp[1];
+            while (!rc && enif_get_list_cell(env, tt, &th, &tt)) {
+                rc = term_id(env, p->toks, th, &id_tok);
+                if (!rc) {
+                    tg[n] = (uint32_t)id_tag;
+                    tk[n++] = id_tok;
+                }
+            }
+        }
+        if (rc) {
+            enif_free(tg);
+            enif_free(tk);
+            return rc;
+        }
+    }
+    *n_out = n;
+    *tags_out = tg;
+    *toks_out = tk;
+    return AGN_OK;
 }
 
 /* one read through the partition's batcher */
@@ -645,49 +776,20 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     } else if (!p->cached) {
         /* base state pairs: set_aw orddict [{Elem, [Tok]}], register_mv [{V, Tok}]
          * (a cached partition's base state is the device snapshot cache's) */
-        unsigned nl = 0;
-        if (!enif_get_list_length(env, base, &nl)) return enif_make_badarg(env);
-        ERL_NIF_TERM h, t = base;
-        uint32_t cap = 0;
-        while (enif_get_list_cell(env, t, &h, &t)) {
-            int ar;
-            const ERL_NIF_TERM *tp;
-            unsigned m = 1;
-            if (!enif_get_tuple(env, h, &ar, &tp) || ar != 2) return enif_make_badarg(env);
-            if (p->type == AGN_SET_AW && !enif_get_list_length(env, tp[1], &m)) return enif_make_badarg(env);
-            cap += m;
-        }
-        btag = enif_alloc(4 * (cap + 1));
-        btok = enif_alloc(8 * (cap + 1));
-        if (!btag || !btok) goto oom;
-        for (t = base; enif_get_list_cell(env, t, &h, &t);) {
-            int ar;
-            const ERL_NIF_TERM *tp;
-            uint64_t tg, tk;
-            enif_get_tuple(env, h, &ar, &tp);
-            if (term_id(env, p->tags, tp[0], &tg)) goto oom;
-            if (p->type == AGN_REGISTER_MV) {
-                if (term_id(env, p->toks, tp[1], &tk)) goto oom;
-                btag[nb] = (uint32_t)tg;
-                btok[nb++] = tk;
-            } else {
-                ERL_NIF_TERM th, tt = tp[1];
-                while (enif_get_list_cell(env, tt, &th, &tt)) {
-                    if (term_id(env, p->toks, th, &tk)) goto oom;
-                    btag[nb] = (uint32_t)tg;
-                    btok[nb++] = tk;
-                }
-            }
-        }
+        const int src = state_pairs(env, p, base, &nb, &btag, &btok);
+        if (src == AGN_EINVAL) return enif_make_badarg(env);
+        if (src) goto oom;
         rd.n_base = nb;
         rd.base_tag = btag;
         rd.base_tok = btok;
     }
     if (p->type != AGN_COUNTER_PN) {
-        /* room for the state: the key's entries + the base (a cached base is
-         * sized by the retry below) */
+        /* room for the state: the key's entries + the base (a cached base:
+         * the largest state the partition's cache holds for the key) */
+        uint32_t bound = 0;
         if (agn_oplog_key_meta(p->log, 1, &k, &len, NULL, NULL)) goto oom;
-        o.out_cap = len + nb + (p->cached ? 16u : 0u);
+        if (p->cached && agn_batcher_state_bound(p->bt, k, &bound)) goto oom;
+        o.out_cap = len + nb + bound + (p->cached ? 16u : 0u);
         otag = enif_alloc(4 * (o.out_cap + 1));
         otok = enif_alloc(8 * (o.out_cap + 1));
         if (!otag || !otok) goto oom;
@@ -696,9 +798,12 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     }
     rc = agn_batcher_read(p->bt, &rd, &o);
     if (rc == AGN_ECAPACITY && p->type != AGN_COUNTER_PN && o.out_n > o.out_cap) {
-        /* the state outgrew the buffer (an update landed after key_meta, or a
-         * larger cached base): read again with room for it (a read/6 is
-         * repeatable: the second one is served from what the first stored) */
+        /* the state outgrew the buffer (updates landed after key_meta): read
+         * again with room for it (a read/6 is repeatable: the second one is
+         * served from what the first stored).  The first pass already ran a GC
+         * read's store and prune, so the retry is a plain read: running
+         * op_insert_gc's GC twice would resize ListLen twice (:540-558). */
+        rd.flags &= ~AGN_READ_GC;
         enif_free(otag);
         enif_free(otok);
         o.out_cap = o.out_n + 16u;
@@ -713,7 +818,7 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     if (rc) r = error_tuple(env, rc);
     else if (p->cached && o.status == AGN_SS_LOG)
         r = enif_make_tuple2(env, atom(env, "error"), atom(env, "no_snapshot"));
-    else r = read_result(env, p, &o, ct, ctm);
+    else r = read_result(env, p, k, &o, ct, ctm);
     enif_free(btag);
     enif_free(btok);
     enif_free(otag);
@@ -742,6 +847,40 @@ static ERL_NIF_TERM nif_part_materialize(ErlNifEnv *env, int argc, const ERL_NIF
     part_res *p;
     if (argc != 6 || !get_part(env, argv[0], &p) || p->cached) return enif_make_badarg(env);
     return part_read_common(env, p, argv[1], argv[2], argv[3], argv[4], argv[5], 0);
+}
+
+/* part_store(Part, Key, CommitTimePairs, NewLastOp, Count, Value, Gc) -> ok:
+ * materialize_snapshot's store (:466-509) of a snapshot the vnode
+ * materialized from the log (get_from_snapshot_log, :416-419), on the
+ * partition's device cache (agn_batcher_store); Gc = true for op_insert_gc's
+ * GC read (a log response is never the newest, so only it stores) */
+static ERL_NIF_TERM nif_part_store(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
+    part_res *p;
+    if (argc != 7 || !get_part(env, argv[0], &p) || !p->cached) return enif_make_badarg(env);
+    uint64_t k, row[256], mask[4];
+    ErlNifSInt64 last_op = 0, value = 0;
+    unsigned count = 0;
+    int rc = key_index(env, p, argv[1], &k);
+    if (!rc) rc = clock_row(env, p, argv[2], row, mask);
+    if (rc == AGN_EINVAL || !enif_get_int64(env, argv[3], &last_op) ||
+        !enif_get_uint(env, argv[4], &count))
+        return enif_make_badarg(env);
+    if (rc) return error_tuple(env, rc);
+    uint32_t n = 0, *tags = NULL;
+    uint64_t *toks = NULL;
+    if (p->type == AGN_COUNTER_PN) {
+        if (!enif_get_int64(env, argv[5], &value)) return enif_make_badarg(env);
+    } else {
+        rc = state_pairs(env, p, argv[5], &n, &tags, &toks);
+        if (rc == AGN_EINVAL) return enif_make_badarg(env);
+        if (rc) return error_tuple(env, rc);
+    }
+    const int gc = enif_is_identical(argv[6], atom(env, "true"));
+    rc = agn_batcher_store(p->bt, k, row, mask, last_op, count, value, n, tags, toks,
+                           gc ? AGN_READ_GC : 0u);
+    enif_free(tags);
+    enif_free(toks);
+    return rc ? error_tuple(env, rc) : atom(env, "ok");
 }
 
 static ERL_NIF_TERM nif_part_gc(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
@@ -805,6 +944,7 @@ static ErlNifFunc funcs[] = {
     {"part_read", 5, nif_part_read, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_materialize", 6, nif_part_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_gc", 3, nif_part_gc, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_store", 7, nif_part_store, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_gc_due", 2, nif_part_gc_due, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_stats", 1, nif_part_stats, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_key_meta", 2, nif_part_key_meta, ERL_NIF_DIRTY_JOB_IO_BOUND},

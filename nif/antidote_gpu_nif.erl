@@ -17,8 +17,8 @@
 -export([new/1, materialize_eager/3, update_snapshot/3]).
 %% engine-owned partition (one per materializer_vnode)
 -export([part_open/5, part_update/5, part_read/5, part_materialize/6, part_gc/3,
-         part_gc_due/2, part_stats/1, part_key_meta/2]).
--export([new_partition/3, update/3, read/4, read_from/6, gc/3]).
+         part_gc_due/2, part_stats/1, part_key_meta/2, part_store/7]).
+-export([new_partition/3, update/3, read/4, read/5, read_from/6, gc/3]).
 
 -on_load(init/0).
 
@@ -50,6 +50,7 @@ part_update(_Part, _Key, _OcPairs, _TxId, _Effect) -> erlang:nif_error(not_loade
 part_read(_Part, _Key, _RPairs, _TxId, _Gc) -> erlang:nif_error(not_loaded).
 part_materialize(_Part, _Key, _RPairs, _Sct, _TxId, _Base) -> erlang:nif_error(not_loaded).
 part_gc(_Part, _Key, _ThresholdPairs) -> erlang:nif_error(not_loaded).
+part_store(_Part, _Key, _CommitTimePairs, _NewLastOp, _Count, _Value, _Gc) -> erlang:nif_error(not_loaded).
 part_gc_due(_Part, _Key) -> erlang:nif_error(not_loaded).
 part_stats(_Part) -> erlang:nif_error(not_loaded).
 part_key_meta(_Part, _Key) -> erlang:nif_error(not_loaded).
@@ -352,7 +353,7 @@ new_partition(Type, NKeys, Cached) ->
 %% reference's ETS snapshot cache, the vnode checks part_gc_due/2 itself, runs
 %% its own internal_read(..., true) -- whose snapshot_insert_gc calls gc/3 --
 %% and then part_update/5.)
-update(Part, Key, #clocksi_payload{snapshot_time = SS, commit_time = {Dc, Ct},
+update(Part, Key, #clocksi_payload{type = Type, snapshot_time = SS, commit_time = {Dc, Ct},
                                    txid = TxId, op_param = Effect}) ->
     GcRan = case part_gc_due(Part, Key) of
                 true ->
@@ -361,6 +362,14 @@ update(Part, Key, #clocksi_payload{snapshot_time = SS, commit_time = {Dc, Ct},
                             %% an uncached partition's GC read is the vnode's own
                             %% (its ETS snapshot cache): use part_update/5 there
                             erlang:error({update_needs_cached_partition, Key});
+                        {error, no_snapshot} ->
+                            %% no cached snapshot <= the op's snapshot time: the GC
+                            %% read goes to the log, and its result is stored with
+                            %% the GC on the device cache (internal_read(..., true),
+                            %% :640 -> get_from_snapshot_log :416-419 ->
+                            %% materialize_snapshot :466-509)
+                            _ = read_from_log(Part, Key, Type, SS, ignore, true),
+                            true;
                         _ -> true
                     end;
                 false -> false
@@ -371,11 +380,47 @@ update(Part, Key, #clocksi_payload{snapshot_time = SS, commit_time = {Dc, Ct},
     end.
 
 %% read/6 on a cached partition: {ok, Value} | {error, no_snapshot} (the
-%% caller reads the log: get_from_snapshot_log, :416-419) | {error, Reason}.
+%% caller reads the log: get_from_snapshot_log, :416-419; read/5 below does
+%% it) | {error, Reason}.
 read(Part, Key, MinSnapshotTime, TxId) ->
     case part_read(Part, Key, dict:to_list(MinSnapshotTime), TxId, false) of
         {ok, Value, _NewLastOp, _LastOpCt, _IsNewSS, _Count} -> {ok, Value};
         Other -> Other
+    end.
+
+%% read/6 with the log fallback (internal_read/7, :371-376, ShouldGc = false).
+read(Part, Key, Type, MinSnapshotTime, TxId) ->
+    case read(Part, Key, MinSnapshotTime, TxId) of
+        {error, no_snapshot} -> read_from_log(Part, Key, Type, MinSnapshotTime, TxId, false);
+        Other -> Other
+    end.
+
+%% get_from_snapshot_log (:416-419) + materialize_snapshot (:466-509) for a
+%% cached partition: the key's ops from the partition's log
+%% (logging_vnode:get_up_to_time), materialize/4 over them on the device
+%% (per-call path), and -- for a GC read -- the result stored with its GC on
+%% the device cache (part_store/7).  A log response is never the newest
+%% snapshot (src/logging_vnode.erl:538-540), so a plain read stores nothing.
+read_from_log(Part, Key, Type, SnapshotTime, TxId, ShouldGc) ->
+    LogId = log_utilities:get_logid_from_key(Key),
+    Partition = log_utilities:get_key_partition(Key),
+    case logging_vnode:get_up_to_time(Partition, LogId, SnapshotTime, Type, Key) of
+        {error, Reason} -> {error, Reason};
+        #snapshot_get_response{number_of_ops = 0, materialized_snapshot = Snapshot} ->
+            {ok, Snapshot#materialized_snapshot.value};
+        Resp ->
+            case materialize(Type, TxId, SnapshotTime, Resp) of
+                {error, Reason} -> {error, Reason};
+                {ok, Value, _NewLastOp, ignore, _WasUpdated, _Count} -> {ok, Value};
+                {ok, Value, NewLastOp, CommitTime, _WasUpdated, Count} ->
+                    case ShouldGc of
+                        true ->
+                            ok = part_store(Part, Key, dict:to_list(CommitTime), NewLastOp,
+                                            Count, Value, true);
+                        false -> ok
+                    end,
+                    {ok, Value}
+            end
     end.
 
 %% materialize/4 over the partition's resident ops from a base snapshot the

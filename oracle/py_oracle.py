@@ -336,11 +336,15 @@ class VectorOrddict:
 # ---------------------------------------------------------------- materializer_vnode
 class MaterializerVnode:
     """ETS-backed state of one partition: ops_cache (key -> ops tuple as a
-    1-indexed Python list) and snapshot_cache (key -> VectorOrddict)."""
+    1-indexed Python list) and snapshot_cache (key -> VectorOrddict).
+    disk_log=True also models the partition's logging_vnode disk log (every
+    committed payload, commit order), which get_from_snapshot_log reads;
+    without it that fallback raises NotImplementedError."""
 
-    def __init__(self):
+    def __init__(self, disk_log: bool = False):
         self.ops_cache: dict = {}
         self.snapshot_cache: dict = {}
+        self.disk_log: list | None = [] if disk_log else None
 
     # -- reads
     def internal_read(self, key, typ, min_snapshot_time, txid, should_gc):
@@ -357,8 +361,23 @@ class MaterializerVnode:
             return self.update_snapshot_from_cache(((IGNORE, empty), True), key)
         found, is_first = self.snapshot_cache[key].get_smaller(min_snapshot_time)
         if found is None:
-            raise NotImplementedError("get_from_snapshot_log (logging_vnode fallback)")
+            return self.get_from_snapshot_log(key, typ, min_snapshot_time)
         return self.update_snapshot_from_cache((found, is_first), key)
+
+    def get_from_snapshot_log(self, key, typ, snapshot_time):
+        """get_from_snapshot_log (:416-419) -> logging_vnode:get_up_to_time
+        (src/logging_vnode.erl:185-190) -> {get, LogId, undefined, Max, Type,
+        Key} (:522-549): the key's committed ops whose transaction snapshot
+        passes check_max_time (vectorclock:le(SnapshotTime, Max), :778-779),
+        in log order, then reverse_and_add_op_id (:586-591): newest first,
+        ids from 0 at the oldest; base {last_op_id 0, Type:new()},
+        snapshot_time vectorclock:new(), is_newest_snapshot false."""
+        if self.disk_log is None:
+            raise NotImplementedError("get_from_snapshot_log (logging_vnode fallback)")
+        ops = [p for p in self.disk_log if p.key == key and vc_le(p.snapshot_time, snapshot_time)]
+        newest_first = [(i, p) for i, p in enumerate(ops)][::-1]
+        return SnapshotGetResponse(newest_first, len(ops), MaterializedSnapshot(0, crdt_new(typ)),
+                                   {}, False)
 
     def store_snapshot(self, txid, key, snapshot, time, should_gc):
         self.internal_store_ss(key, snapshot, time, should_gc)
@@ -457,6 +476,11 @@ class MaterializerVnode:
 
     # -- writes
     def update(self, key, op: Payload):
+        # the commit is logged before the materializer sees the op
+        # (clocksi_vnode:commit -> logging_vnode:append_commit, then
+        # update_materializer, src/clocksi_vnode.erl:499-528,636-656)
+        if self.disk_log is not None:
+            self.disk_log.append(op)
         return self.op_insert_gc(key, op)
 
     def op_insert_gc(self, key, op: Payload):

@@ -5,6 +5,15 @@ batch's extra inputs / outputs costs what, on uniform keys and on mixed ones
 8 waves per SIMD for cold masked batches ("_w8" variants: 8.51 vs 8.49 ms,
 mixed 9.57 vs 9.46; profiles/r03/ab_masked_w8.log) -- not kept.
 
+Round 4: each variant also carries environment knobs (AGN_COUNTER_EARLY=0:
+k_counter_key, the prologue with every scalar load before the rows; default:
+k_counter_q8e + k_counter_q8m over the keys whose entries differ, chunk 0's
+rows issued right after the segment metadata and the key's DC set;
+AGN_Q8E_KM=0: the DC set loaded under the chunk instead) and agn_read.hints
+(AGN_HINT_CT_FLAG / AGN_HINT_R_FULL).  Every variant's results (value, hole,
+LastOpCt + its mask, count, flags) are compared with its input class's first
+variant.
+
   python scripts/ab_masked.py [rounds]
 """
 import ctypes as C
@@ -16,12 +25,29 @@ import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
+HINTS = 0x1 | 0x2  # AGN_HINT_R_FULL | AGN_HINT_CT_FLAG
+# name: (inputs, env, hints)
+VARIANTS = {
+    "dense": ("dense", {}, 0),
+    "masked_old": ("masked", {"AGN_COUNTER_EARLY": "0"}, 0),
+    "masked": ("masked", {}, 0),
+    "masked_km0": ("masked", {"AGN_Q8E_KM": "0"}, 0),
+    "masked_ctflag": ("masked", {}, 0x2),
+    "masked_ctflag_km0": ("masked", {"AGN_Q8E_KM": "0"}, 0x2),
+    "masked_hints": ("masked", {}, HINTS),
+    "mixed_old": ("mixed", {"AGN_COUNTER_EARLY": "0"}, 0),
+    "mixed": ("mixed", {}, 0),
+    "mixed_km0": ("mixed", {"AGN_Q8E_KM": "0"}, 0),
+}
+KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM")
+
 
 def main():
     import torch
     from antidote_amd import _abi
     from antidote_amd.engine import Engine
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    only = [x for x in os.environ.get("AB_ONLY", "").split(",") if x]
     torch.cuda.set_device(0)
     eng = Engine(0)
     st = torch.cuda.current_stream()
@@ -34,62 +60,69 @@ def main():
     rm = torch.full((K,), 255, dtype=torch.int64, device="cuda")
     from bench import presence_masks
     ocm_x, _ = presence_masks("mixed", D, K * N, K, torch=torch)
-    kbx = eng.empty(8 * K)
-    res_d = eng.alloc_result(K, D, sparse=False)
-    res_s = eng.alloc_result(K, D, sparse=True)
-    res_x = eng.alloc_result(K, D, sparse=True)
-    kb = eng.empty(8 * K)
+    kb, kbx = eng.empty(8 * K), eng.empty(8 * K)
+    res = {"dense": eng.alloc_result(K, D, sparse=False),
+           "masked": eng.alloc_result(K, D, sparse=True),
+           "mixed": eng.alloc_result(K, D, sparse=True)}
 
-    def variant(name):
+    def structs(inputs, hints):
         ls, rs = _abi.AgnLog(), _abi.AgnRead()
         C.memmove(C.addressof(ls), C.addressof(dl), C.sizeof(ls))
         C.memmove(C.addressof(rs), C.addressof(dr), C.sizeof(rs))
-        res = res_d
-        if name != "dense":
-            ls.oc_mask = ocm.data_ptr()
-            ls.key_mask = kb.ptr
+        if inputs != "dense":
+            ls.oc_mask = (ocm if inputs == "masked" else ocm_x).data_ptr()
+            ls.key_mask = (kb if inputs == "masked" else kbx).ptr
             rs.R_mask = rm.data_ptr()
-            res = res_s
-        if name == "masked_no_out_mask":
-            res = res_d
-        if name == "masked_no_R_mask":
-            rs.R_mask = None
-        if name.startswith("mixed"):
-            ls.oc_mask = ocm_x.data_ptr()
-            ls.key_mask = kbx.ptr
-            res = res_x
-        if name == "out_mask_only":
-            ls.oc_mask = None
-            ls.key_mask = None
-            rs.R_mask = None
-            res = res_s
-        return ls, rs, res
-    names = ["dense", "masked", "masked_no_out_mask", "masked_no_R_mask", "out_mask_only",
-             "mixed"]
-    args = {n: variant(n) for n in names}
-    check = eng.lib.agn_log_index_masks(eng.ctx, C.byref(args["masked"][0]), kb.ptr, sp)
-    assert check == 0
-    check = eng.lib.agn_log_index_masks(eng.ctx, C.byref(args["mixed"][0]), kbx.ptr, sp)
-    assert check == 0
+        rs.hints = hints
+        return ls, rs
+    names = [n for n in VARIANTS if not only or n in only]
+    args = {n: structs(VARIANTS[n][0], VARIANTS[n][2]) for n in names}
+    for inputs, buf in (("masked", kb), ("mixed", kbx)):
+        ls, _ = structs(inputs, 0)
+        assert eng.lib.agn_log_index_masks(eng.ctx, C.byref(ls), buf.ptr, sp) == 0
+
+    def setenv(env):
+        for k in KNOBS:
+            if k in env:
+                os.environ[k] = env[k]
+            else:
+                os.environ.pop(k, None)
     ms = {n: [] for n in names}
+    ref, same = {}, {}
     for r in range(rounds + 1):
         for n in (names if r % 2 == 0 else names[::-1]):
-            ls, rs, res = args[n]
+            inputs, env, _ = VARIANTS[n]
+            ls, rs = args[n]
+            setenv(env)
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             b.record(st)
-            eng.materialize(ls, rs, res, stream=sp)
+            eng.materialize(ls, rs, res[inputs], stream=sp)
             e.record(st)
             torch.cuda.synchronize()
             if r:
                 ms[n].append(b.elapsed_time(e))
-    v = {n: eng.download(args[n][2].bufs["value"], np.int64, (K,)) for n in names}
-    # uniform masks give the dense values; the mixed log's own pair must agree
-    same = {n: bool(np.array_equal(v[n], v["mixed" if n.startswith("mixed") else "dense"]))
-            for n in names}
+            if r == 0:  # results of every variant vs its input class's first
+                got = eng.fetch_result(res[inputs])
+                key = "dense" if inputs in ("dense", "masked") else "mixed"
+                fields = ("value", "hole", "lastct", "count", "flags") + \
+                    (("lastct_mask",) if inputs != "dense" else ())
+                if key not in ref:
+                    ref[key] = got
+                    same[n] = True
+                else:
+                    same[n] = all(np.array_equal(getattr(got, f), getattr(ref[key], f))
+                                  for f in fields if getattr(ref[key], f) is not None)
+                if inputs == "masked" and "masked" not in ref:
+                    ref["masked"] = got
+                if inputs == "masked":
+                    same[n] = same[n] and np.array_equal(got.lastct_mask, ref["masked"].lastct_mask)
+    setenv({})
+    med = {n: float(np.median(x)) for n, x in ms.items()}
+    base = med.get("dense")
     print(json.dumps({"warm": int(os.environ.get("WARM", "0")),
-                      "variant": os.environ.get("AGN_COUNTER_VARIANT", "default"),
-                      "ms_median": {n: float(np.median(x)) for n, x in ms.items()},
-                      "values_equal_dense": same}), flush=True)
+                      "ms_median": med,
+                      "vs_dense": {n: (v / base if base else None) for n, v in med.items()},
+                      "results_equal": same}), flush=True)
     dl.oc_mask = dr.R_mask = None
     eng.free_gen(dl, dr)
     eng.close()

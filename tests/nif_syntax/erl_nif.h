@@ -66,7 +66,9 @@ int enif_get_resource(ErlNifEnv *env, ERL_NIF_TERM term, ErlNifResourceType *typ
 void enif_release_resource(void *obj);
 void enif_keep_resource(void *obj);
 void *enif_alloc(size_t size);
+void *enif_realloc(void *ptr, size_t size);
 void enif_free(void *ptr);
+ERL_NIF_TERM enif_raise_exception(ErlNifEnv *env, ERL_NIF_TERM reason);
 
 #define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                 \
     static const void *agn_nif_syntax_check_##NAME[] = {(const void *)FUNCS,      \

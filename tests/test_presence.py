@@ -76,8 +76,9 @@ def oracle_result(oracle_lib, log, req, cap=None):
     return res
 
 
-def device_result(eng, log, req, index):
+def device_result(eng, log, req, index, hints=0):
     dl, dr = eng.upload_log(log), eng.upload_read(req, sparse=True)
+    dr.struct.hints = hints
     if index:
         eng.index_masks(dl)
     dres = eng.alloc_result(req.n_req, log.n_dcs, sparse=True)
@@ -85,26 +86,33 @@ def device_result(eng, log, req, index):
     return eng.fetch_result(dres)
 
 
-IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3"}
+IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "split": "2", "split_ctflag": "2"}
 
 
 @pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
-@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general"])
+@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "split", "split_ctflag"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
 def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
+    """split: the early-chunk kernel with its hand-ons to the general kernel
+    (AGN_COUNTER_SPLIT=1: from one request; D = 8), _ctflag with
+    AGN_HINT_CT_FLAG (LastOpCt masks over every column as AGN_F_CT_FULL)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
+    monkeypatch.setenv("AGN_COUNTER_SPLIT", "1" if impl.startswith("split") else "0")
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
     else:
         monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
+    if impl.startswith("split") and path == "host":
+        pytest.skip("the host path has no hints; split covered on the device paths")
     log, req = presence_case(1000 * D + len(impl) + len(path), 260, D, 150, txid=0.3,
                              invalid=0.02, corrupt=0.03, identity=(D % 2 == 0))
     want = oracle_result(oracle_lib, log, req)
     if path == "host":
         got = eng.materialize_host(log, req, sparse=True)
     else:
-        got = device_result(eng, log, req, index=(path == "device_indexed"))
+        got = device_result(eng, log, req, index=(path == "device_indexed"),
+                            hints=_abi.HINT_CT_FLAG if impl == "split_ctflag" else 0)
     bad = compare(_abi.COUNTER_PN, D, got, want, True, req.n_req)
     assert not bad, bad[:10]
     # absent LastOpCt columns are 0, as the oracle writes them (a corrupted
@@ -163,13 +171,16 @@ def test_index_masks_vs_numpy(eng, D):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2"])
+@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "split_hints"])
 @pytest.mark.parametrize("D", [3, 8])
 def test_full_masks_equal_dense(eng, monkeypatch, D, impl):
     """Every DC present everywhere: the masked batch equals the dense one, and
-    LastOpCt's DC set is all of them (or empty when LastOpCt is ignore)."""
+    LastOpCt's DC set is all of them (or empty when LastOpCt is ignore).
+    split_hints: the early-chunk kernel with AGN_HINT_R_FULL (R masks unread)
+    and AGN_HINT_CT_FLAG, over device arrays."""
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
-    monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS[impl])
+    monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "2"))
+    monkeypatch.setenv("AGN_COUNTER_SPLIT", "1" if impl == "split_hints" else "0")
     log, req, _ = random_case(515 + D, _abi.COUNTER_PN, 400, D, 200, sparse=True, warm=0.5,
                               txid=0.3, invalid=0.02, corrupt=0.03)
     full = np.uint64((1 << D) - 1)
@@ -177,7 +188,11 @@ def test_full_masks_equal_dense(eng, monkeypatch, D, impl):
     req.R_mask[:] = full
     req.sct_mask[:] = full
     dense = eng.materialize_host(log, req, sparse=False)
-    masked = eng.materialize_host(log, req, sparse=True)
+    if impl == "split_hints":
+        masked = device_result(eng, log, req, index=True,
+                               hints=_abi.HINT_R_FULL | _abi.HINT_CT_FLAG)
+    else:
+        masked = eng.materialize_host(log, req, sparse=True)
     assert not compare(_abi.COUNTER_PN, D, masked, dense, False, req.n_req)
     ign = (masked.flags & _abi.F_CT_IGNORE) != 0
     corrupt = (masked.flags & _abi.F_ERR_CORRUPTED) != 0
