@@ -156,8 +156,9 @@ int errs_to_op_ids(agn_batcher *B, const agn_log &view, std::vector<Pending *> &
     return AGN_OK;
 }
 
-// Cached mode, counter_pn with D <= 8 (dense clocks, or presence masks: the
-// Erlang NIF's partitions): the whole batch is one fused kernel (read6.hip)
+// Cached mode, counter_pn with D <= 64 (dense clocks, or presence masks: the
+// Erlang NIF's partitions): the whole batch is one fused kernel (read6.hip;
+// k_read6 for D <= 8, k_read6w above)
 // reading the requests from, and writing the results to, the pinned block
 // directly; its GC follows in stream order from the batch's device key list.
 int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
@@ -179,11 +180,17 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
                      o_Rm = slot(sparse ? n * 8 : 0), o_ctm = slot(sparse ? n * 8 : 0);
         d_keys = 0;
         d_pr = al(n * 8);
-        rc = grow(B, std::max(off, d_pr + n));
+        // D > 8 (k_read6w): the lookup's SCT rows / masks, ignore bytes and the
+        // LastOpCt rows / masks, in device memory
+        const bool wide = D > 8;
+        const size_t d_sct = al(d_pr + n), d_sctm = al(d_sct + (wide ? n * D * 8 : 0)),
+                     d_ct = al(d_sctm + (wide ? n * 8 : 0)), d_ctm = al(d_ct + (wide ? n * D * 8 : 0)),
+                     d_ign = al(d_ctm + (wide ? n * 8 : 0)), d_end = d_ign + (wide ? n : 0);
+        rc = grow(B, std::max(off, d_end));
         if (rc) return rc;
         char *h = B->hbuf;
         bool any_tx = false;
-        const uint64_t full = (1ull << D) - 1ull;
+        const uint64_t full = D >= 64 ? ~0ull : (1ull << D) - 1ull;
         for (uint64_t i = 0; i < n; ++i) {
             const agn_key_read *r = b[i]->rd;
             ((uint64_t *)(h + o_keys))[i] = r->key;
@@ -225,6 +232,13 @@ int run_batch_read6(agn_batcher *B, std::vector<Pending *> &b, bool sparse) {
         a.dkeys = (uint64_t *)(B->dbuf + d_keys);
         a.dprune = (uint8_t *)(B->dbuf + d_pr);
         a.thr = B->thr;
+        if (wide) {
+            a.sct_scr = (uint64_t *)(B->dbuf + d_sct);
+            a.sctm_scr = (uint64_t *)(B->dbuf + d_sctm);
+            a.ct_scr = (uint64_t *)(B->dbuf + d_ct);
+            a.ctm_scr = (uint64_t *)(B->dbuf + d_ctm);
+            a.ign_scr = (uint8_t *)(B->dbuf + d_ign);
+        }
         if (sparse) {
             a.key_mask = view.key_mask;
             a.oc_mask = view.oc_mask;
@@ -660,7 +674,7 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
     if (B->crdt != AGN_COUNTER_PN) return run_batch_cached_tags(B, b);
     bool sparse = B->sparse_log != 0;
     for (Pending *p : b) sparse = sparse || p->rd->R_mask;
-    if (D <= 8 && B->read6) return run_batch_read6(B, b, sparse);
+    if (D <= 64 && B->read6) return run_batch_read6(B, b, sparse);
     std::vector<uint64_t> keys(n);
     for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
     int rc;

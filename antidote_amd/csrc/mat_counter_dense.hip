@@ -36,6 +36,10 @@
 namespace agn {
 namespace {
 
+// k_counter_q8e's hand-on sub-lists: count, and the stride of their counters
+// (uint32 words: one 128-byte line each)
+constexpr uint32_t QL_S = 1024, QL_STRIDE = 32;
+
 struct DenseArgs {
     uint64_t n_req;
     uint64_t n_entries;
@@ -44,6 +48,7 @@ struct DenseArgs {
     uint32_t pair; // 1: D <= 4 keys longer than a chunk walk two chunks per step
     uint32_t qnt;  // quad rows, non-temporal loads: bit 0 rows, bit 1 effects (AGN_COUNTER_QUAD_NT)
     uint32_t hints;  // agn_read.hints (k_counter_q8e / k_counter_quad2)
+    uint32_t ql_cap; // k_counter_q8e / q8m: entries per hand-on sub-list
 };
 
 // Presence masks of a sparse batch (the MSK instantiations; one word per
@@ -775,8 +780,14 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
     auto mixed = [&](uint64_t kmw) {
         return !(mk.oc_mask == nullptr || (mk.key_mask && (kmw & 0xFFull)) || k.n == 0);
     };
+    // QL_S sub-lists (request i -> i mod QL_S), each with its own counter in
+    // its own 128-byte line: one shared counter serialised every hand-on of
+    // a batch of mixed keys at one L2 channel (10M atomics, 16x the scan)
     auto hand_on = [&]() {
-        if (lane_id() == 0) list[atomicAdd(list_n, 1u)] = (uint32_t)i;
+        if (lane_id() == 0) {
+            const uint32_t sl = (uint32_t)(i % QL_S);
+            list[(uint64_t)sl * a.ql_cap + atomicAdd(list_n + sl * QL_STRIDE, 1u)] = (uint32_t)i;
+        }
     };
     uint64_t kmw = 0;
     if constexpr (KM == 1) {
@@ -809,8 +820,8 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
 
 // The keys k_counter_q8e handed on (entries with different DC sets): the
 // per-entry-mask quad scan (scan_key_q8_msk), one request per wave, the
-// waves striding over the list -- the grid does not know the list's length,
-// and an empty list costs one short launch.
+// waves striding over the sub-lists -- the grid does not know their
+// lengths, and empty lists cost one short launch.
 template <bool ANY_WARM, bool KEYS>
 __global__ __launch_bounds__(64) void k_counter_q8m(
     DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
@@ -825,9 +836,11 @@ __global__ __launch_bounds__(64) void k_counter_q8m(
     uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
     uint32_t *__restrict__ o_err, const uint32_t *__restrict__ list,
     const uint32_t *__restrict__ list_n) {
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(*list_n);
-    for (uint32_t j = blockIdx.x; j < cnt; j += gridDim.x) {
-        const uint64_t i = __builtin_amdgcn_readfirstlane(list[j]);
+    // block b walks sub-list b mod QL_S, entries b / QL_S, + gridDim.x / QL_S
+    const uint32_t sl = blockIdx.x % QL_S, per = gridDim.x / QL_S;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(list_n[sl * QL_STRIDE]);
+    for (uint32_t j = blockIdx.x / QL_S; j < cnt; j += per) {
+        const uint64_t i = __builtin_amdgcn_readfirstlane(list[(uint64_t)sl * a.ql_cap + j]);
         const Q2Key k = q2_prologue<ANY_WARM, true>(a, mk, i, KEYS ? keys : nullptr, key_off,
                                                     key_len, key_type, key_id0, R, sct, sct_ignore,
                                                     req_txid);
@@ -893,17 +906,23 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     const MaskArgs mk = mask_args(log, req, out);
     if (req.n_req > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                                (unsigned long long)req.n_req);
+    // the key's DC set loaded under the first chunk (default; cold masked
+    // cfg2 1.047x dense vs 1.107x with the metadata, profiles/r04/), or with
+    // the segment metadata (AGN_Q8E_KM=1)
     const char *kv = getenv("AGN_Q8E_KM");
-    const bool km0 = kv && kv[0] == '0';
-    uint32_t *lst = nullptr;  // [0] = count, then the handed-on request indices
-    AGN_HIP(pool_malloc(&lst, (req.n_req + 1) * sizeof(uint32_t), st));
+    const bool km0 = !(kv && kv[0] == '1');
+    // QL_S counters (QL_STRIDE apart), then QL_S sub-lists of ql_cap indices
+    a.ql_cap = (uint32_t)((req.n_req + QL_S - 1) / QL_S);
+    const size_t hdr = (size_t)QL_S * QL_STRIDE;
+    uint32_t *lst = nullptr;
+    AGN_HIP(pool_malloc(&lst, (hdr + (size_t)QL_S * a.ql_cap) * sizeof(uint32_t), st));
     int rc = AGN_OK;
-    if (hipMemsetAsync(lst, 0, sizeof(uint32_t), st) != hipSuccess)
+    if (hipMemsetAsync(lst, 0, hdr * sizeof(uint32_t), st) != hipSuccess)
         rc = fail(AGN_EHIP, "counter q8e: list reset");
 #define AGN_ARGS                                                                                \
     a, mk, req.keys, log.key_off, log.key_len, log.key_type, id0_index(log), log.oc, log.op_id,  \
         log.eff, log.txid, req.R, req.sct, req.sct_ignore, req.txid, req.base_value, out.value,  \
-        out.hole, out.lastct, out.count, out.flags, out.err_pos, lst + 1, lst
+        out.hole, out.lastct, out.count, out.flags, out.err_pos, lst + hdr, lst
 #define AGN_Q8E_(W, K, KM)                                                                      \
     hipLaunchKernelGGL((k_counter_q8e<W, K, KM>), dim3((unsigned)req.n_req), dim3(64), 0, st,   \
                        AGN_ARGS)
@@ -912,7 +931,7 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
         if (km0) AGN_Q8E_(W, K, 0);                                                             \
         else AGN_Q8E_(W, K, 1);                                                                 \
     } while (0)
-    const unsigned mb = (unsigned)(req.n_req < 16384 ? req.n_req : 16384);
+    const unsigned mb = QL_S * 16u;  // a multiple of QL_S
 #define AGN_Q8M(W, K)                                                                           \
     hipLaunchKernelGGL((k_counter_q8m<W, K>), dim3(mb), dim3(64), 0, st, AGN_ARGS)
     if (rc == AGN_OK) {

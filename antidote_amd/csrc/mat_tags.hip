@@ -220,11 +220,12 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     constexpr int OPI = S::OPI;
     static_assert(!CT || (DPL == 4 && FULL && !SPARSE), "CT: dense rows, 4 DCs per lane");
     static_assert(!MSK || (FULL && !SPARSE), "MSK: the dense row scans");
-    static_assert(!SV || (WARM && !SLOW && DPL * LPO <= 8), "SV: the fast pass, D <= 8");
+    static_assert(!SV || (WARM && !SLOW && DPL * LPO <= 64), "SV: the fast pass, D <= 64");
+    constexpr int SVD = DPL * LPO;  // SV: the LastOpCt stash's row width (>= D), mask word after it
     constexpr int P = CT ? DPL * LPO / 2 : 1;  // 16-byte parts per op
     constexpr int OPH = AGN_WAVE / P;          // ops per 1 KiB load (OPI / 2)
     __shared__ CandLds<CAP> Lall[WPB];
-    __shared__ uint64_t Sct[WPB][SV ? 9 : 1];  // SV: LastOpCt row + mask word for the store
+    __shared__ uint64_t Sct[WPB][SV ? SVD + 1 : 1];  // SV: LastOpCt row + mask word for the store
     const int w = (WPB == 1) ? 0 : (int)(threadIdx.x >> 6);
     CandLds<CAP> &L = Lall[w];
     const int lane = lane_id();
@@ -643,7 +644,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             }
             const uint64_t ctm = ct_ign ? 0ull : ((sct_ign ? 0ull : mS) | (cnt ? mU : 0ull));
             if (out.lastct_mask != nullptr && lane == 0) out.lastct_mask[i] = ctm;
-            if (SV && lane == 0) Sct[w][SV ? 8 : 0] = ctm;
+            if (SV && lane == 0) Sct[w][SV ? SVD : 0] = ctm;
         }
         if constexpr (CT) {
 #pragma unroll
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
 #pragma unroll
                 for (int x = 1; x < AGN_WAVE; x <<= 1) v |= shfl_xor_u64(v, x);
                 if (lane == 0) out.lastct_mask[i * W + wd] = v;
-                if (SV && lane == 0 && wd == 0) Sct[w][SV ? 8 : 0] = v;
+                if (SV && lane == 0 && wd == 0) Sct[w][SV ? SVD : 0] = v;
             }
         }
 
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
             uint64_t dl[3] = {0ull, 0ull, 0ull};
             const bool pr = ss_store_one<AGN_WAVE>(
                 g, sv.c, key, n, lk.status, lk.first, sv.gc != nullptr && sv.gc[i] != 0, Sct[w],
-                ((MSK || SPARSE) && out.lastct_mask != nullptr) ? &Sct[w][SV ? 8 : 0] : nullptr,
+                ((MSK || SPARSE) && out.lastct_mask != nullptr) ? &Sct[w][SV ? SVD : 0] : nullptr,
                 hole, 0, cnt,
                 fl, sv.thr, sv.thrm, L.tag, L.tok, n_live, dl);
             if (lane == 0) {
@@ -909,31 +910,34 @@ int dispatch_masked(const agn_log &log, const agn_read &req, const agn_result &o
 // Shapes (as launch_tags picks them for D <= 8): FULL dense rows (even D;
 // D = 4 the CT form), the MSK form (masked, even D), non-FULL dense rows or
 // the per-entry-mask (SPARSE) form for odd D.
-template <int D, bool SET, bool SPARSE, bool FULL, bool MSK, bool CT>
+// DPL x LPO: the pass's shape (D <= 8: one lane per op; 16, 32, 64: 4 DCs
+// per lane, the CT rows); SDPL x SLPO: the per-entry-mask pass's for the keys
+// the MSK form hands on.
+template <int DPL, int LPO, int SDPL, int SLPO, bool SET, bool SPARSE, bool FULL, bool MSK, bool CT>
 int serve_fast(const agn_log &log, const agn_read &req, const agn_result &out, const TagServe &sv,
                uint32_t *scr, hipStream_t st) {
     TagScratch w;
     w.base = scr;
     w.n = req.n_req;
     const TagLists fast{nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n()};
-    hipLaunchKernelGGL((k_tags<D, 1, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, true, false, CT,
-                               MSK, true>),
+    hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, true, false,
+                               CT, MSK, true>),
                        dim3(grid_for(req.n_req, FAST_WPB, 0x7fffffffu)), dim3(64 * FAST_WPB), 0, st,
                        log, req, out, fast, 0u, sv);
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }
 
-template <int D, bool SET, bool SPARSE, bool FULL, bool MSK, bool CT>
+template <int DPL, int LPO, int SDPL, int SLPO, bool SET, bool SPARSE, bool FULL, bool MSK, bool CT>
 int serve_rest(const agn_log &log, const agn_read &req, const agn_result &out, const TagServe &sv,
                uint32_t *scr, hipStream_t st) {
     TagScratch w;
     w.base = scr;
     w.n = req.n_req;
-    hipError_t e = tags_passes<D, 1, SPARSE, FULL, SET, true, CT, MSK>(
+    hipError_t e = tags_passes<DPL, LPO, SPARSE, FULL, SET, true, CT, MSK>(
         log, req, out, nullptr, nullptr, w.ovf(), w.ovf_n(), w.mix(), w.mix_n(), st, false);
     if (MSK && e == hipSuccess)
-        e = tags_passes<D, 1, true, false, SET, true, false, false>(
+        e = tags_passes<SDPL, SLPO, true, false, SET, true, false, false>(
             log, req, out, w.mix(), w.mix_n(), w.ovf2(), w.ovf2_n(), nullptr, nullptr, st);
     if (e != hipSuccess) return fail(AGN_EHIP, "k_tags launch: %s", hipGetErrorString(e));
     // the store for both lists (the mixed keys' overflow list is part of mix)
@@ -950,9 +954,10 @@ int serve_rest(const agn_log &log, const agn_read &req, const agn_result &out, c
 template <bool REST, bool SET>
 int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &out,
                    const TagServe &sv, uint32_t *scr, bool msk, hipStream_t st) {
-#define AGN_S(D, SPV, FULLV, MSKV, CTV)                                                    \
-    return REST ? serve_rest<D, SET, SPV, FULLV, MSKV, CTV>(log, req, out, sv, scr, st)     \
-                : serve_fast<D, SET, SPV, FULLV, MSKV, CTV>(log, req, out, sv, scr, st)
+#define AGN_SW(DPL, LPO, SD, SL, SPV, FULLV, MSKV, CTV)                                              \
+    return REST ? serve_rest<DPL, LPO, SD, SL, SET, SPV, FULLV, MSKV, CTV>(log, req, out, sv, scr, st) \
+                : serve_fast<DPL, LPO, SD, SL, SET, SPV, FULLV, MSKV, CTV>(log, req, out, sv, scr, st)
+#define AGN_S(D, SPV, FULLV, MSKV, CTV) AGN_SW(D, 1, D, 1, SPV, FULLV, MSKV, CTV)
     if (msk) {
         switch (log.n_dcs) {
             case 1: AGN_S(1, true, false, false, false);
@@ -963,6 +968,11 @@ int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &ou
             case 6: AGN_S(6, false, true, true, false);
             case 7: AGN_S(7, true, false, false, false);
             case 8: AGN_S(8, false, true, true, false);
+            // the masked shapes launch_tags picks (dispatch_masked): CT rows,
+            // the per-entry-mask pass at 8 DCs per lane
+            case 16: AGN_SW(4, 4, 8, 2, false, true, true, true);
+            case 32: AGN_SW(4, 8, 8, 4, false, true, true, true);
+            case 64: AGN_SW(4, 16, 8, 8, false, true, true, true);
             default: break;
         }
     } else {
@@ -975,10 +985,15 @@ int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &ou
             case 6: AGN_S(6, false, true, false, false);
             case 7: AGN_S(7, false, false, false, false);
             case 8: AGN_S(8, false, true, false, false);
+            // dense wide clocks: 4 DCs per lane, contiguous (CT) rows (dispatch)
+            case 16: AGN_SW(4, 4, 4, 4, false, true, false, true);
+            case 32: AGN_SW(4, 8, 4, 8, false, true, false, true);
+            case 64: AGN_SW(4, 16, 4, 16, false, true, false, true);
             default: break;
         }
     }
 #undef AGN_S
+#undef AGN_SW
     return AGN_ENOTSUP;
 }
 
@@ -986,9 +1001,15 @@ int serve_dispatch(const agn_log &log, const agn_read &req, const agn_result &ou
 
 // D <= 8 in the shape launch_tags picks: even D with the MSK form for masked
 // logs (not with AGN_TAGS_MSK=0) and, dense, D = 4 in the CT form (not with
-// AGN_TAGS_CT=0); odd D with the per-entry-mask or non-FULL dense rows
+// AGN_TAGS_CT=0); odd D with the per-entry-mask or non-FULL dense rows;
+// D = 16, 32, 64 in the CT form (4 DCs per lane), dense or MSK
 bool tags_serve_supported(const agn_log &log, bool sparse) {
     const uint32_t D = log.n_dcs;
+    if (D == 16 || D == 32 || D == 64) {  // the CT shapes, dense or MSK
+        if (!tags_ct()) return false;
+        const char *v = getenv("AGN_TAGS_MSK");
+        return !sparse || !(v && v[0] == '0');
+    }
     if (D == 0 || D > 8) return false;
     if (D % 2) return true;
     if (sparse) {
@@ -1023,6 +1044,10 @@ int launch_tags_serve_rest(const agn_log &log, const agn_read &req, const agn_re
 int launch_tags(const agn_log &log, const agn_read &req, const agn_result &out,
                 hipStream_t st) {
     if (req.n_req == 0) return AGN_OK;
+    // base_value without base_off names AGN_SS_STATE references into
+    // base_tag / base_tok (ABI v4): both arrays are required for them
+    if (!req.base_off && req.base_value && (!req.base_tag || !req.base_tok))
+        return fail(AGN_EINVAL, "set/register read: base_value (state references) without base_tag/base_tok");
     const bool sparse = log.oc_mask || req.R_mask || req.sct_mask || out.lastct_mask;
     const bool set = log.crdt_type == AGN_SET_AW;
     if (sparse) {

@@ -16,7 +16,9 @@
 // of three kernels and two copies: for the read batcher requests are read
 // from, and results written to, device-visible pinned host memory;
 // agn_read_cached runs it over device arrays below 2^15 requests.
+#include "cache_dev.hpp"
 #include "counter_scan.hpp"
+#include "filter.hpp"
 #include "serve.hpp"
 
 namespace agn {
@@ -412,6 +414,133 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     }
 }
 
+// read/6 for clocks of 9 .. 64 DCs (D > 8 has no register-resident dense
+// scan): one wave per request runs get_from_snapshot_cache on all 64 lanes
+// (cache_dev.hpp ss_lookup_one, the SCT row into device scratch), the general
+// per-key filter + counter fold from that base (filter.hpp KeyFilter, as
+// mat_counter.hip's k_counter: DPL DCs per lane, LPO lanes per op, per-entry
+// masks when SPARSE) and materialize_snapshot's store (ss_store_one) -- one
+// launch where the batcher otherwise runs lookup -> materialize -> store as
+// three kernels around two copies.  Same results as that sequence.
+template <int DPL, int LPO, bool SPARSE>
+__global__ __launch_bounds__(64) void k_read6w(agn_ss_cache c, Read6Args a) {
+    using F = KeyFilter<DPL, LPO, SPARSE>;
+    __shared__ uint64_t stage[DPL][AGN_WAVE];
+    const uint64_t i = blockIdx.x;
+    if (i >= a.n_req) return;
+    const int lane = lane_id();
+    const uint32_t D = a.n_dcs, W = n_words(D);
+    const uint64_t key = uniform_u64(a.keys[i]);
+    agn_log log;
+    __builtin_memset(&log, 0, sizeof log);
+    log.crdt_type = AGN_COUNTER_PN;
+    log.n_dcs = D;
+    log.n_entries = a.n_entries;
+    log.key_off = a.key_off;
+    log.key_len = a.key_len;
+    log.key_type = a.key_type;
+    log.oc = a.oc;
+    log.oc_mask = SPARSE ? a.oc_mask : nullptr;
+    log.op_id = a.op_id;
+    log.txid = a.log_txid;
+    log.eff = a.eff;
+    agn_read rq;
+    __builtin_memset(&rq, 0, sizeof rq);
+    rq.n_req = a.n_req;
+    rq.keys = a.keys;
+    rq.R = a.R;
+    rq.R_mask = SPARSE ? a.R_mask : nullptr;
+    rq.sct = a.sct_scr;
+    rq.sct_mask = SPARSE ? a.sctm_scr : nullptr;
+    rq.sct_ignore = a.ign_scr;
+    rq.txid = a.txid;
+    rq.req_type = a.req_type;
+    // 1. get_from_snapshot_cache (:384-413, vector_orddict:get_smaller)
+    const Grp<AGN_WAVE> g;
+    const LookupOut lk = ss_lookup_one<AGN_WAVE>(
+        g, c, key, a.R + i * D, (SPARSE && a.R_mask) ? a.R_mask + i * W : nullptr,
+        a.sct_scr + i * D, (SPARSE && a.sctm_scr) ? a.sctm_scr + i * W : nullptr);
+    if (lane == 0) a.ign_scr[i] = lk.ign;
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the filter reads them back
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t off = uniform_u64(a.key_off[key]);
+    const uint64_t n = uniform_u64(key_n(a.key_off, a.key_len, key));
+    const uint32_t kty = a.key_type ? __builtin_amdgcn_readfirstlane((uint32_t)a.key_type[key]) : 0u;
+    if (n != 0 && a.key_type != nullptr && kty != (a.req_type & 0xffu)) {
+        // erlang:error(corrupted_ops_cache) (:190-191): no store
+        for (uint32_t d = lane; d < D; d += AGN_WAVE) a.lastct[i * D + d] = 0ull;
+        if (lane == 0) {
+            a.value[i] = 0;
+            a.hole[i] = 0;
+            a.count[i] = 0;
+            a.flags[i] = AGN_F_ERR_CORRUPTED;
+            a.err_pos[i] = 0xffffffffu;
+            a.status[i] = (uint8_t)lk.status;
+            a.prune[i] = 0;
+            if (SPARSE && a.lastct_mask) a.lastct_mask[i] = 0ull;
+            if (a.dkeys) a.dkeys[i] = key;
+            if (a.dprune) a.dprune[i] = 0;
+        }
+        return;
+    }
+    // 2. materialize/4 from the base (mat_counter.hip k_counter's body)
+    F f;
+    f.init(log, rq, i);
+    int64_t sum = 0;
+    uint32_t cnt = 0;
+    int64_t first_err = -1;
+    for (uint64_t b = 0; b < n; b += F::S::OPI) {
+        bool valid;
+        const bool incl = f.step(log, off, n, b, valid);
+        const bool lead = incl && f.sub == 0;
+        int64_t ev = 0;
+        if (lead) ev = a.eff[off + b + (uint64_t)f.slot];
+        const bool bad = lead && ev == AGN_EFFECT_INVALID;
+        cnt += (uint32_t)__builtin_popcountll(ballot(lead));
+        if (first_err < 0) {
+            const uint64_t be = ballot(bad);
+            if (be) first_err = (int64_t)b + (int64_t)(__builtin_ctzll(be) / LPO);
+        }
+        sum += bad ? 0 : ev;
+    }
+    const int64_t total = wave_sum_i64(sum);
+    const bool ct_ign = f.sct_ign && cnt == 0u;
+    agn_result o;
+    __builtin_memset(&o, 0, sizeof o);
+    o.lastct = a.ct_scr;
+    o.lastct_mask = SPARSE ? a.ctm_scr : nullptr;
+    f.write_ct(stage, o, i, ct_ign);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the store reads the row back
+    __builtin_amdgcn_wave_barrier();
+    int64_t hid;
+    if (f.first_excl >= 0) hid = (int64_t)a.op_id[uniform_u64(off + (uint64_t)f.first_excl)];
+    else hid = n ? (int64_t)a.op_id[uniform_u64(off + n - 1)] : 0;
+    const int64_t hole = f.first_excl >= 0 ? hid - 1 : hid;
+    uint32_t fl = 0;
+    if (cnt) fl |= AGN_F_NEWSS;
+    if (ct_ign) fl |= AGN_F_CT_IGNORE;
+    if (first_err >= 0) fl |= AGN_F_ERR_UNEXPECTED;
+    const int64_t value = (int64_t)((uint64_t)lk.base + (uint64_t)total);
+    // 3. internal_store_ss / insert_bigger / snapshot_insert_gc (:341-364, 466-563)
+    const bool gc = a.gc != nullptr && a.gc[i] != 0;
+    const bool pr = ss_store_one<AGN_WAVE>(g, c, key, n, lk.status, lk.first, gc, a.ct_scr + i * D,
+                                           SPARSE ? a.ctm_scr + i * W : nullptr, hole, value, cnt,
+                                           fl, a.thr, SPARSE ? a.thrm : nullptr);
+    for (uint32_t d = lane; d < D; d += AGN_WAVE) a.lastct[i * D + d] = a.ct_scr[i * D + d];
+    if (lane == 0) {
+        a.value[i] = value;
+        a.hole[i] = hole;
+        a.count[i] = cnt;
+        a.flags[i] = fl;
+        a.err_pos[i] = first_err >= 0 ? (uint32_t)(off + (uint64_t)first_err) : 0xffffffffu;
+        a.status[i] = (uint8_t)lk.status;
+        a.prune[i] = pr ? 1 : 0;
+        if (SPARSE && a.lastct_mask) a.lastct_mask[i] = a.ctm_scr[i * W];
+        if (a.dkeys) a.dkeys[i] = key;
+        if (a.dprune) a.dprune[i] = pr ? 1 : 0;
+    }
+}
+
 }  // namespace
 
 bool read6_supported(const agn_log &view, uint32_t D) {
@@ -427,6 +556,12 @@ int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     if (msk) hipLaunchKernelGGL((k_read6<DV, true>), grid, block, 0, st, c, a);                \
     else hipLaunchKernelGGL((k_read6<DV, false>), grid, block, 0, st, c, a);                   \
     break
+#define AGN_R6W(DPL, LPO)                                                                      \
+    if (msk) hipLaunchKernelGGL((k_read6w<DPL, LPO, true>), grid, block, 0, st, c, a);          \
+    else hipLaunchKernelGGL((k_read6w<DPL, LPO, false>), grid, block, 0, st, c, a);             \
+    break
+    if (a.n_dcs > 8 && (!a.sct_scr || !a.ign_scr || !a.ct_scr || (msk && (!a.sctm_scr || !a.ctm_scr))))
+        return fail(AGN_EINVAL, "read6: D > 8 needs the device scratch");
     switch (a.n_dcs) {
         case 1: AGN_R6(1);
         case 2: AGN_R6(2);
@@ -436,8 +571,13 @@ int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
         case 6: AGN_R6(6);
         case 7: AGN_R6(7);
         case 8: AGN_R6(8);
-        default: return fail(AGN_ENOTSUP, "read6: n_dcs=%u", a.n_dcs);
+        default:
+            if (a.n_dcs <= 16) { AGN_R6W(8, 2); }
+            if (a.n_dcs <= 32) { AGN_R6W(8, 4); }
+            if (a.n_dcs <= 64) { AGN_R6W(8, 8); }
+            return fail(AGN_ENOTSUP, "read6: n_dcs=%u", a.n_dcs);
     }
+#undef AGN_R6W
 #undef AGN_R6
     AGN_HIP(hipGetLastError());
     return AGN_OK;

@@ -76,6 +76,11 @@ struct Read6Args {
     // carries clock_mask)
     const uint64_t *key_mask, *oc_mask, *R_mask;
     uint64_t *lastct_mask, *thrm;
+    // D = 9 .. 64 (k_read6w): device scratch of the batch -- the lookup's SCT
+    // rows [n][D] and mask words [n], its ignore bytes [n], and the LastOpCt
+    // rows [n][D] / mask words [n] the store reads back
+    uint64_t *sct_scr, *sctm_scr, *ct_scr, *ctm_scr;
+    uint8_t *ign_scr;
 };
 // agn_read_cached's fused path: dense logs (its cache has no clock masks)
 bool read6_supported(const agn_log &view, uint32_t D);

@@ -144,7 +144,12 @@ typedef struct agn_read {
                                    set/register with base_off NULL: [n_req]
                                    AGN_SS_STATE(start, pairs) references into
                                    base_tag / base_tok (a cache's state arena,
-                                   as agn_ss_lookup writes them) */
+                                   as agn_ss_lookup writes them; both arrays
+                                   required, else AGN_EINVAL).  Device memory
+                                   for the device calls; host memory for the
+                                   host helpers agn_state_capacity and
+                                   agn_materialize_host, which read the pair
+                                   counts out of the references */
     const uint64_t *base_off;   /* set/register: CSR [n_req+1] or NULL (= empty) */
     const uint32_t *base_tag;   /* set: elem, register: value */
     const uint64_t *base_tok;   /* token */
@@ -253,7 +258,11 @@ int agn_log_index_masks(agn_ctx *ctx, const agn_log *log, uint64_t *out, void *s
 
 /* Upper bound of live pairs per request for set/register types:
  * writes cap_off[n_req+1] (host pointers): cap = #adding entries of the key
- * + #base pairs.  Host-side helper (the bound is static per log). */
+ * + #base pairs.  Host-side helper (the bound is static per log): every
+ * array of host_log / host_req it reads -- key_off / key_len, the adding
+ * flags, base_off, or base_value's AGN_SS_STATE references when base_off is
+ * NULL -- must be host memory (copy a device agn_ss_lookup's base_value
+ * back first). */
 int agn_state_capacity(const agn_log *host_log, const agn_read *host_req,
                        uint64_t *cap_off);
 

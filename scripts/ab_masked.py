@@ -9,7 +9,8 @@ Round 4: each variant also carries environment knobs (AGN_COUNTER_EARLY=0:
 k_counter_key, the prologue with every scalar load before the rows; default:
 k_counter_q8e + k_counter_q8m over the keys whose entries differ, chunk 0's
 rows issued right after the segment metadata and the key's DC set;
-AGN_Q8E_KM=0: the DC set loaded under the chunk instead) and agn_read.hints
+AGN_Q8E_KM=1: the DC set loaded with the metadata instead of under the
+chunk) and agn_read.hints
 (AGN_HINT_CT_FLAG / AGN_HINT_R_FULL).  Every variant's results (value, hole,
 LastOpCt + its mask, count, flags) are compared with its input class's first
 variant.
@@ -31,13 +32,12 @@ VARIANTS = {
     "dense": ("dense", {}, 0),
     "masked_old": ("masked", {"AGN_COUNTER_EARLY": "0"}, 0),
     "masked": ("masked", {}, 0),
-    "masked_km0": ("masked", {"AGN_Q8E_KM": "0"}, 0),
+    "masked_km1": ("masked", {"AGN_Q8E_KM": "1"}, 0),
     "masked_ctflag": ("masked", {}, 0x2),
-    "masked_ctflag_km0": ("masked", {"AGN_Q8E_KM": "0"}, 0x2),
     "masked_hints": ("masked", {}, HINTS),
     "mixed_old": ("mixed", {"AGN_COUNTER_EARLY": "0"}, 0),
     "mixed": ("mixed", {}, 0),
-    "mixed_km0": ("mixed", {"AGN_Q8E_KM": "0"}, 0),
+    "mixed_km1": ("mixed", {"AGN_Q8E_KM": "1"}, 0),
 }
 KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM")
 

@@ -501,3 +501,22 @@ def test_rccl_single_rank_min_allreduce(eng):
     eng.gst_allreduce(b.ptr, 4)
     eng.sync()
     assert np.array_equal(eng.download(b, np.uint64, (4,)), v)
+
+
+@pytest.mark.parametrize("crdt", [_abi.SET_AW, _abi.REGISTER_MV])
+def test_tags_state_refs_need_their_arrays(eng, crdt):
+    """agn_read.base_value without base_off names AGN_SS_STATE references into
+    base_tag / base_tok: with either array missing the call fails with
+    AGN_EINVAL before any kernel reads them (not an out-of-bounds read)."""
+    from antidote_amd._lib import EngineError
+    log, req, cap = random_case(9 + crdt, crdt, 40, 3, 20)
+    dl, dr = eng.upload_log(log), eng.upload_read(req, sparse=False)
+    refs = eng.empty(8 * req.n_req)
+    dr.struct.base_off = None
+    dr.struct.base_tag = None
+    dr.struct.base_tok = None
+    dr.struct.base_value = refs.ptr
+    dres = eng.alloc_result(req.n_req, log.n_dcs, sparse=False, cap_off=cap)
+    with pytest.raises(EngineError) as ei:
+        eng.materialize(dl, dr, dres)
+    assert ei.value.code == _abi.EINVAL

@@ -86,19 +86,24 @@ def device_result(eng, log, req, index, hints=0):
     return eng.fetch_result(dres)
 
 
-IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "split": "2", "split_ctflag": "2"}
+IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "split": "2", "split_km1": "2",
+         "split_ctflag": "2"}
 
 
 @pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
-@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "split", "split_ctflag"])
+@pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "split", "split_km1",
+                                  "split_ctflag"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
 def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
-    """split: the early-chunk kernel with its hand-ons to the general kernel
-    (AGN_COUNTER_SPLIT=1: from one request; D = 8), _ctflag with
-    AGN_HINT_CT_FLAG (LastOpCt masks over every column as AGN_F_CT_FULL)."""
+    """quad / quad2 / vgpr: k_counter_key (AGN_COUNTER_EARLY=0); split: the
+    default masked D = 8 path -- k_counter_q8e with its hand-ons (keys whose
+    entries differ) to the list pass k_counter_q8m; _km1 with the key's DC set
+    loaded with the segment metadata (AGN_Q8E_KM=1), _ctflag with AGN_HINT_CT_FLAG
+    (LastOpCt masks over every column as AGN_F_CT_FULL)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
-    monkeypatch.setenv("AGN_COUNTER_SPLIT", "1" if impl.startswith("split") else "0")
+    monkeypatch.setenv("AGN_COUNTER_EARLY", "1" if impl.startswith("split") else "0")
+    monkeypatch.setenv("AGN_Q8E_KM", "1" if impl == "split_km1" else "0")
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
     else:
@@ -180,7 +185,7 @@ def test_full_masks_equal_dense(eng, monkeypatch, D, impl):
     and AGN_HINT_CT_FLAG, over device arrays."""
     monkeypatch.delenv("AGN_COUNTER_IMPL", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "2"))
-    monkeypatch.setenv("AGN_COUNTER_SPLIT", "1" if impl == "split_hints" else "0")
+    monkeypatch.setenv("AGN_COUNTER_EARLY", "1" if impl == "split_hints" else "0")
     log, req, _ = random_case(515 + D, _abi.COUNTER_PN, 400, D, 200, sparse=True, warm=0.5,
                               txid=0.3, invalid=0.02, corrupt=0.03)
     full = np.uint64((1 << D) - 1)

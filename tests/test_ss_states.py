@@ -11,7 +11,7 @@ appends the result's state.  Checked against the reference's transcription
 resize) read for read:
 
   * the cached read batcher (the NIF's read/4 on a Cached partition), with
-    update/2's GC reads, dense and presence-masked logs; for D <= 8
+    update/2's GC reads, dense and presence-masked logs; for D <= 64
     the batch is the fused read (lookup -> fast tags pass -> store in one
     kernel, tags_serve.hpp), with its hand-on path for states past the fast
     table; AGN_READ6=0 runs the kernel sequence on the same workload;
@@ -194,7 +194,11 @@ def placeholder(vn, key):
 BATCHER_CASES = [
     (d, lg, r6) for d in (3, 4, 8) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
 ] + [(1, "sparse", "1"), (2, "sparse", "1"), (5, "sparse", "1"), (6, "dense", "1"),
-     (7, "dense", "1"), (7, "mixed", "1")]
+     (7, "dense", "1"), (7, "mixed", "1")] + [
+    # D > 8: the fused read's wide shapes (mat_tags.hip serve_dispatch, 4 DCs
+    # a lane) against the reference and the kernel sequence
+    (16, lg, r6) for lg in ("dense", "sparse", "mixed") for r6 in ("1", "0")
+] + [(64, "dense", "1"), (64, "sparse", "1"), (64, "mixed", "1"), (32, "mixed", "1")]
 
 
 @pytest.mark.parametrize("d,logk,read6", BATCHER_CASES)
@@ -251,7 +255,9 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
         ln, ll, ct = ol.key_meta()
     print(f"served={served} log_reads={part.log_reads} log_gc={part.log_gc} "
           f"quirk={len(quirk)}/{K}")
-    assert served > (150 if mixed else 500) and part.log_reads > 0, \
+    # (at D = 64 the clocks a read picks are rarely below every kept snapshot
+    # within the run: the log path is exercised at the narrower widths)
+    assert served > (150 if mixed else 500) and (part.log_reads > 0 or d > 16), \
         (served, part.log_reads, len(quirk))
     assert len(quirk) <= K // 4, (len(quirk), K)
     for k in range(K):
@@ -261,7 +267,11 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
         assert (int(ln[k]), int(ll[k])) == (length, list_len), k
 
 
-@pytest.mark.parametrize("d", [3, 4, 8])
+def rand_mask(rng, d):
+    return int(sum(int(b) << i for i, b in enumerate(rng.integers(0, 2, d))))
+
+
+@pytest.mark.parametrize("d", [3, 4, 8, 16, 64])
 @pytest.mark.parametrize("typ", [_abi.SET_AW, _abi.REGISTER_MV])
 def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
     """Entries with random DC sets (each holding its own DC; R with some DCs
@@ -286,7 +296,7 @@ def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
                 key = int(w.rng.integers(0, K))
                 if w.rng.random() < 0.7:
                     c, ss, ct, oc, eff, entry = w.op(key)
-                    mask = np.uint64(int(w.rng.integers(0, 1 << d)) | (1 << c))
+                    mask = np.uint64(rand_mask(w.rng, d) | (1 << c))
                     pay = po.Payload(key, PTYPE[typ], eff, vc(ss, int(mask)), (c, ct), s + 1)
                     try:
                         vn.update(key, pay)
@@ -298,7 +308,7 @@ def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
                         quirk.add(key)
                 else:
                     R = w.read_clock(lag=400 if w.rng.random() < 0.85 else 20000).astype(np.uint64)
-                    rm = full if w.rng.random() < 0.8 else int(w.rng.integers(1, 1 << d))
+                    rm = full if w.rng.random() < 0.8 else rand_mask(w.rng, d) | 1
                     (ra, ga), (rb, gb) = (p.read(key, R, np.array([rm], np.uint64)) for p in (pa, pb))
                     for f in ga:
                         assert np.array_equal(np.asarray(ga[f]), np.asarray(gb[f])), (s, key, f)

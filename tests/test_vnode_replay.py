@@ -28,8 +28,8 @@ D = 3
 BIG = 10 ** 15
 
 
-def vc(row):
-    return {d: int(row[d]) for d in range(D)}
+def vc(row, mask=None):
+    return {d: int(row[d]) for d in range(len(row)) if mask is None or (int(mask) >> d) & 1}
 
 
 class Workload:
@@ -37,13 +37,14 @@ class Workload:
     current times (its snapshot), so op clocks are causal and reads at any
     R <= the current clocks see exactly the ops already appended."""
 
-    def __init__(self, seed, K):
+    def __init__(self, seed, K, d=D):
         self.rng = np.random.default_rng(seed)
-        self.K = K
-        self.clk = np.full(D, 1000, np.int64)
+        self.K, self.D = K, d
+        self.clk = np.full(d, 1000, np.int64)
         self.ops = [[] for _ in range(K)]   # per key: (oc row, eff)
 
     def op(self, key):
+        D = self.D
         c = int(self.rng.integers(0, D))
         ss = self.clk - self.rng.integers(0, 40, D)
         ss = np.maximum(ss, 0)
@@ -55,7 +56,7 @@ class Workload:
         return c, ss, ct, oc, eff
 
     def read_clock(self, lag=400):
-        return np.maximum(self.clk - self.rng.integers(0, lag, D), 0)
+        return np.maximum(self.clk - self.rng.integers(0, lag, self.D), 0)
 
 
 def has_placeholder(vn, key):
@@ -69,25 +70,31 @@ def has_placeholder(vn, key):
     return any(tup[po.FIRST_OP - 1 + i] == 0 for i in range(length))
 
 
-def engine_update(ol, bt, key, ss, oc, eff, txid):
+def engine_update(ol, bt, key, ss, oc, eff, txid, mask=None):
     """op_insert_gc/3 (:621-647) in the reference's order: the GC read at the
-    op's snapshot time (:640) when due, then the insert."""
+    op's snapshot time (:640) when due, then the insert.  mask: the op's DC
+    set (a presence-masked log)."""
+    m = None if mask is None else np.array([mask], np.uint64)
     if ol.gc_due(key)[0]:
-        bt.read(key, R=ss.astype(np.uint64), gc=True)
-    ids, _ = ol.append(np.array([key], np.uint64), oc.reshape(1, D).astype(np.uint64),
+        bt.read(key, R=ss.astype(np.uint64), R_mask=m, gc=True)
+    ids, _ = ol.append(np.array([key], np.uint64), oc.reshape(1, len(oc)).astype(np.uint64),
+                       oc_mask=None if m is None else m.reshape(1, 1),
                        eff=np.array([eff], np.int64), txid=np.array([txid], np.uint64))
     return int(ids[0])
 
 
+# D <= 8: read6.hip k_read6 (register-resident clocks); D = 16 / 64: k_read6w
+# (the general per-key filter between the cache lookup and store)
+@pytest.mark.parametrize("d", [3, 16, 64])
 @pytest.mark.parametrize("read6", ["1", "0"])
-def test_vnode_replay_sequential_vs_reference(eng, monkeypatch, read6):
+def test_vnode_replay_sequential_vs_reference(eng, monkeypatch, read6, d):
     monkeypatch.setenv("AGN_READ6", read6)
     K, steps = 24, 4000
-    w = Workload(11, K)
+    w = Workload(11 + d, K, d)
     vn = po.MaterializerVnode()
     quirk = set()   # keys where the reference hit the all-pruned placeholder (:580-583)
     served = log_reads = 0
-    with OpLog(eng, _abi.COUNTER_PN, D, K) as ol, \
+    with OpLog(eng, _abi.COUNTER_PN, d, K) as ol, \
             Batcher(ol, max_batch=8, cached=True) as bt:
         for s in range(steps):
             key = int(w.rng.integers(0, K))
@@ -133,15 +140,16 @@ def test_vnode_replay_sequential_vs_reference(eng, monkeypatch, read6):
         assert (int(ln[k]), int(ll[k]), int(ct[k])) == (length, list_len, vn.ops_cache[k][2]), k
 
 
+@pytest.mark.parametrize("d", [3, 16, 64])
 @pytest.mark.parametrize("read6", ["1", "0"])
-def test_vnode_replay_threads_values(eng, monkeypatch, read6):
+def test_vnode_replay_threads_values(eng, monkeypatch, read6, d):
     """1 writer (the vnode: update/2 + GC reads) and 8 read servers."""
     monkeypatch.setenv("AGN_READ6", read6)
     K = 16
-    w = Workload(5, K)
+    w = Workload(5 + d, K, d)
     lock = threading.Lock()
     errs, stats = [], {"served": 0, "log": 0}
-    with OpLog(eng, _abi.COUNTER_PN, D, K, init_slots=8) as ol, \
+    with OpLog(eng, _abi.COUNTER_PN, d, K, init_slots=8) as ol, \
             Batcher(ol, max_batch=16, max_wait_us=100, cached=True) as bt:
         stop = threading.Event()
 
@@ -172,7 +180,7 @@ def test_vnode_replay_threads_values(eng, monkeypatch, read6):
                     key = int(rng.integers(0, K))
                     with lock:
                         # ops at or below the published clocks are all appended
-                        R = np.maximum(w.clk - rng.integers(0, 300, D), 0)
+                        R = np.maximum(w.clk - rng.integers(0, 300, d), 0)
                     g = bt.read(key, R=R.astype(np.uint64))
                     with lock:
                         ops = list(w.ops[key])
@@ -202,3 +210,82 @@ def test_vnode_replay_threads_values(eng, monkeypatch, read6):
         st = ol.stats()
     assert stats["served"] > 100, stats
     assert st["entries"] < sum(len(x) for x in w.ops)   # the GC ran
+
+
+def rand_mask(rng, d):
+    return int(sum(int(b) << i for i, b in enumerate(rng.integers(0, 2, d))))
+
+
+@pytest.mark.parametrize("d", [5, 8, 16, 64])
+def test_counter_fused_vs_sequence_masked(eng, d):
+    """Presence-masked counter partitions (the NIF's): entries with random DC
+    sets (each holding its own DC), R missing DCs now and then.  Two
+    partitions fed the same updates, one served by the fused read (k_read6,
+    D = 16 / 64: k_read6w), one by the kernel sequence: every result field,
+    the status and the ETS list sizes agree, and every served value equals the
+    reference transcription's."""
+    import os
+    K, steps = 16, 2500
+    w = Workload(71 + d, K, d)
+    full = (1 << d) - 1
+    vn = po.MaterializerVnode()
+    quirk = set()
+    served = compared = 0
+    with OpLog(eng, _abi.COUNTER_PN, d, K, sparse=True) as la, \
+            OpLog(eng, _abi.COUNTER_PN, d, K, sparse=True) as lb:
+        old = os.environ.get("AGN_READ6")
+        try:
+            os.environ["AGN_READ6"] = "1"
+            ba = Batcher(la, max_batch=8, cached=True)
+            os.environ["AGN_READ6"] = "0"
+            bb = Batcher(lb, max_batch=8, cached=True)
+        finally:
+            if old is None:
+                os.environ.pop("AGN_READ6", None)
+            else:
+                os.environ["AGN_READ6"] = old
+        with ba, bb:
+            for s in range(steps):
+                key = int(w.rng.integers(0, K))
+                if w.rng.random() < 0.7:
+                    c, ss, ct, oc, eff = w.op(key)
+                    mask = (rand_mask(w.rng, d) if w.rng.random() < 0.5 else full) | (1 << c)
+                    pay = po.Payload(key, po.COUNTER_PN, eff, vc(ss, mask), (c, ct), s + 1)
+                    try:
+                        vn.update(key, pay)
+                    except (po.BadMatch, TypeError, ValueError):
+                        quirk.add(key)
+                    for ol, bt in ((la, ba), (lb, bb)):
+                        engine_update(ol, bt, key, ss, oc, eff, s + 1, mask)
+                    if has_placeholder(vn, key):
+                        quirk.add(key)
+                else:
+                    R = w.read_clock(lag=400 if w.rng.random() < 0.85 else 20000)
+                    rm = full if w.rng.random() < 0.8 else rand_mask(w.rng, d) | 1
+                    m = np.array([rm], np.uint64)
+                    ga, gb = (bt.read(key, R=R.astype(np.uint64), R_mask=m) for bt in (ba, bb))
+                    for f in ("status", "value", "hole", "count", "flags", "err_pos"):
+                        assert ga[f] == gb[f], (s, key, f, ga[f], gb[f])
+                    assert np.array_equal(ga["lastct"], gb["lastct"]), (s, key)
+                    assert np.array_equal(ga["lastct_mask"], gb["lastct_mask"]), (s, key)
+                    compared += 1
+                    if key in quirk:
+                        continue
+                    try:
+                        want = vn.read(key, po.COUNTER_PN, vc(R, rm), po.IGNORE)
+                    except NotImplementedError:
+                        assert ga["status"] == _abi.SS_LOG, (s, key)
+                        continue
+                    except (po.BadMatch, TypeError, ValueError):
+                        quirk.add(key)
+                        continue
+                    assert ga["status"] in (_abi.SS_HIT, _abi.SS_NEW), (s, key, ga["status"])
+                    assert want == ("ok", ga["value"]), (s, key, want, ga["value"])
+                    served += 1
+                    if has_placeholder(vn, key):
+                        quirk.add(key)
+            print(f"compared={compared} served={served} quirk={len(quirk)}/{K}")
+            assert compared > 500 and served > 300, (compared, served)
+            assert len(quirk) <= K // 4
+            for a, b in zip(la.key_meta(), lb.key_meta()):
+                assert np.array_equal(a, b)
