@@ -19,7 +19,7 @@ TAG_INVALID = 0xFFFFFFFF
 
 F_NEWSS, F_CT_IGNORE, F_ERR_UNEXPECTED, F_ERR_CORRUPTED, F_ERR_CAPACITY = 0x1, 0x2, 0x4, 0x8, 0x10
 F_CT_FULL = 0x20          # ABI v5: LastOpCt has every column (mask not written)
-HINT_R_FULL, HINT_CT_FLAG = 0x1, 0x2
+HINT_R_FULL, HINT_CT_FLAG, HINT_MIXED = 0x1, 0x2, 0x4
 OPS_THRESHOLD = 50  # src/materializer_vnode.erl:41
 RESIZE_THRESHOLD = 5  # :44
 GC_ALL_PRUNED = 0x1

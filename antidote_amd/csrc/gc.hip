@@ -313,9 +313,6 @@ struct InplaceArgs {
     // set/register removal tokens of an iteration's kept entries copied by
     // the whole wave (lane = token) instead of by each entry's head lane
     int tcoop;
-    // TS kernels: each kept entry's source token start, at its destination
-    // slot ([n_entries] scratch), for k_prune_tokens to move the tokens after
-    uint32_t *tsrc;
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -334,13 +331,8 @@ constexpr int PT = 4;  // removal tokens a lane buffers per entry
 // iteration with each instruction and re-request it (the tags kernel's CT
 // rows, k_tags).  Verdicts are group-any folds of wave ballots; a kept row is
 // stored from the same registers (its parts' lanes fetch its destination).
-// TS (set/register): the removal tokens are not moved here -- each kept
-// entry's head lane records its source token start in a.tsrc at its
-// destination slot and k_prune_tokens moves the tokens afterwards, so an
-// iteration's chain is rows -> filter -> fields -> stores, without the
-// token loads that depend on the fields (and without their registers).
 template <int DPL, int LPO, bool SPARSE, bool FULL, bool TAGS, int WPB, bool CTL = false,
-          int PF = 0, int MINW = 1, bool TS = false>
+          int PF = 0, int MINW = 1>
 __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(InplaceArgs a,
                                                        const uint8_t *__restrict__ prune,
                                                        const uint64_t *__restrict__ thr,
@@ -568,8 +560,7 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
         // is never above its source and sources rise with the token index,
         // so a round's stores never reach a later round's sources
         constexpr int TM = 4;
-        constexpr bool TSP = TS && TAGS;
-        const bool coop = tags && !TSP && a.tcoop;
+        const bool coop = tags && a.tcoop;
         uint64_t cv[TM];
         auto coop_load = [&](uint32_t base) {
 #pragma unroll
@@ -596,8 +587,8 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             }
         };
         if (coop) coop_load(0u);
-        const bool long_list = tags && !TSP && !coop && ballot(head && rl_ > (uint32_t)PT) != 0ull;
-        if (tags && !TSP && !coop && !long_list && head) {
+        const bool long_list = tags && !coop && ballot(head && rl_ > (uint32_t)PT) != 0ull;
+        if (tags && !coop && !long_list && head) {
 #pragma unroll
             for (int x = 0; x < PT; ++x) tk[x] = (uint32_t)x < rl_ ? a.tok[r0 + x] : 0ull;
         }
@@ -647,9 +638,7 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             }
         }
         if (tags) {
-            if (TSP) {
-                if (head && rl_) a.tsrc[dst] = r0;
-            } else if (coop) {
+            if (coop) {
                 coop_store(0u);
                 for (uint32_t base = TM * AGN_WAVE; base < T; base += TM * AGN_WAVE) {
                     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1259,71 +1248,6 @@ __global__ __launch_bounds__(64, MINW) void k_prune_tail_q(InplaceArgs a,
     }
 }
 
-// Second pass of a TS prune: per key (one wave) its kept entries' removal
-// tokens, 64 entries at a time -- lane = entry: source start (a.tsrc),
-// destination start and length (the new rem_off) -- then the chunk's tokens
-// as one destination run, lane = token, its owner entry found by a binary
-// search over the lanes' inclusive counts, TM tokens per lane per round.
-// In place a token's destination is never above its source and sources rise
-// with the token index, so a round's stores never reach a later round's
-// sources (every load of a round precedes its stores).
-template <int TM>
-__global__ __launch_bounds__(64) void k_prune_tokens(const uint64_t *__restrict__ key_off,
-                                                     const uint64_t *__restrict__ new_len,
-                                                     const uint32_t *__restrict__ new_rem_off,
-                                                     const uint32_t *__restrict__ tsrc,
-                                                     const uint64_t *tok, uint64_t *d_tok,
-                                                     uint64_t n_keys, int xcd) {
-    const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint64_t k = blk;
-    if (k >= n_keys) return;
-    const int lane = lane_id();
-    const uint64_t off = uniform_u64(key_off[k]);
-    const uint64_t n = uniform_u64(new_len[k]);
-    for (uint64_t c = 0; c < n; c += AGN_WAVE) {
-        const bool in = c + (uint64_t)lane < n;
-        const uint64_t e = off + c + (in ? (uint64_t)lane : 0ull);
-        const uint32_t s0 = in ? tsrc[e] : 0u;
-        const uint32_t d0 = new_rem_off[e];
-        const uint32_t len = in ? new_rem_off[e + 1] - d0 : 0u;
-        uint32_t incl = len;
-#pragma unroll
-        for (int x = 1; x < AGN_WAVE; x <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)incl, x, AGN_WAVE);
-            if (lane >= x) incl += v;
-        }
-        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint32_t dbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)d0);
-        for (uint32_t t0 = 0; t0 < T; t0 += TM * AGN_WAVE) {
-            uint64_t v[TM];
-#pragma unroll
-            for (int m = 0; m < TM; ++m) {
-                const uint32_t t = t0 + (uint32_t)(m * AGN_WAVE + lane);
-                int lo = 0;  // first lane whose inclusive count exceeds t
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1) {
-                    const uint32_t w = (uint32_t)__shfl((int)incl, lo + step - 1, AGN_WAVE);
-                    lo = w <= t ? lo + step : lo;
-                }
-                const int ow = lo < AGN_WAVE ? lo : AGN_WAVE - 1;
-                const uint32_t os = (uint32_t)__shfl((int)s0, ow, AGN_WAVE);
-                const uint32_t oi = (uint32_t)__shfl((int)incl, ow, AGN_WAVE);
-                const uint32_t ol = (uint32_t)__shfl((int)len, ow, AGN_WAVE);
-                v[m] = t < T ? tok[os + (t - (oi - ol))] : 0ull;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int m = 0; m < TM; ++m) {
-                const uint32_t t = t0 + (uint32_t)(m * AGN_WAVE + lane);
-                if (t < T) d_tok[dbase + t] = v[m];
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-}
-
 template <int DPL, int LPO, bool SPARSE>
 int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *thr,
                   const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags, hipStream_t st) {
@@ -1388,30 +1312,6 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         }
 #undef AGN_T
         return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_tail launch");
-    }
-    // TS: tokens moved by a second pass (a.tsrc set by the caller: the
-    // segmented prune of a tag log, AGN_PRUNE_TSPLIT); AGN_PRUNE_PF=0 drops
-    // the next iteration's row prefetch
-    if (tags && a.tsrc && !a.key_list) {
-        const char *pv = getenv("AGN_PRUNE_PF");
-        const bool pf = !(pv && pv[0] == '0');
-#define AGN_S(FULLV, PFV)                                                                          \
-    hipLaunchKernelGGL((k_prune_inplace<DPL, LPO, SPARSE, FULLV, true, 1, false, PFV, 1, true>),   \
-                       dim3(blocks), dim3(64), 0, st, a, prune, thr, thr_mask, meta, flags)
-        if (full) {
-            if (pf) AGN_S((DPL % 2 == 0), 1);
-            else AGN_S((DPL % 2 == 0), 0);
-        } else {
-            if (pf) AGN_S(false, 1);
-            else AGN_S(false, 0);
-        }
-#undef AGN_S
-        AGN_HIP(hipGetLastError());
-        hipLaunchKernelGGL((k_prune_tokens<4>), dim3(blocks), dim3(64), 0, st,
-                           a.d_key_off ? (const uint64_t *)a.d_key_off : a.key_off,
-                           (const uint64_t *)a.d_key_len, (const uint32_t *)a.d_rem_off,
-                           (const uint32_t *)a.tsrc, a.tok, a.d_tok, a.n_keys, a.xcd);
-        return hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "k_prune_tokens launch");
     }
 #define AGN_K(FULLV, TAGSV)                                                                    \
     do {                                                                                       \
@@ -1542,7 +1442,6 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
     const char *tc = getenv("AGN_PRUNE_TCOOP");  // A/B knob: 0 | 1
     a.tcoop = (tc && tc[0] == '1') ? 1 : 0;
-    a.tsrc = nullptr;
     a.meta6 = 0;
     return a;
 }
@@ -1680,15 +1579,8 @@ int launch_prune_segmented(const agn_log &log, const uint8_t *prune, const uint6
     a.d_key_off = (uint64_t *)out.key_off;
     a.copy_unselected = 1;
     const bool sparse = log.oc_mask || thr_mask;
-    // set/register: removal tokens in a second pass (k_prune_tokens) unless
-    // AGN_PRUNE_TSPLIT=0
-    const char *ts = getenv("AGN_PRUNE_TSPLIT");
-    const bool tsplit = log.rem_off != nullptr && !(ts && ts[0] == '0') && log.n_entries != 0;
-    if (tsplit) AGN_HIP(pool_malloc(&a.tsrc, (size_t)log.n_entries * sizeof(uint32_t), st));
-    const int rc = sparse ? inplace<true>(a, prune, thr, thr_mask, nullptr, flags, st)
-                          : inplace<false>(a, prune, thr, thr_mask, nullptr, flags, st);
-    if (a.tsrc) (void)hipFreeAsync(a.tsrc, st);
-    return rc;
+    return sparse ? inplace<true>(a, prune, thr, thr_mask, nullptr, flags, st)
+                  : inplace<false>(a, prune, thr, thr_mask, nullptr, flags, st);
 }
 
 // Two-phase prune_ops into a fresh segmented arena (agn_oplog_prune): the

@@ -894,7 +894,11 @@ int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out,
 }
 
 // Sparse batches (D = 8, quad rows) run k_counter_q8e + k_counter_q8m,
-// unless AGN_COUNTER_EARLY=0 (A/B knob: k_counter_key).  AGN_Q8E_KM=0 loads
+// unless AGN_COUNTER_EARLY=0 (A/B knob) or the batch carries AGN_HINT_MIXED:
+// k_counter_key, which scans a mixed key in the same pass (cfg2 with one
+// entry in 8 lacking a DC: 1.24x dense there, 2.56x through the hand-on,
+// whose first pass reads the key's only chunk for nothing;
+// profiles/r04/ab_masked_*).  AGN_Q8E_KM=0 loads
 // the key's DC set under the first chunk instead of with the metadata.
 inline bool early_chunk() {
     const char *v = getenv("AGN_COUNTER_EARLY");
@@ -1052,7 +1056,8 @@ int launch_var(int v, const agn_log &log, const agn_read &req, const agn_result 
         if (v == ROWS_GLDS) return launch_key_g<D, WPB, ROWS_GLDS, false>(log, req, out, st);
     if constexpr (D == 8)
         if (v == ROWS_QUAD || (MSK && v == ROWS_GLDS)) {
-            if (MSK && WPB == 1 && early_chunk()) return launch_q8e(log, req, out, st);
+            if (MSK && WPB == 1 && early_chunk() && !(req.hints & AGN_HINT_MIXED))
+                return launch_q8e(log, req, out, st);
             return launch_key_g<D, WPB, ROWS_QUAD, MSK>(log, req, out, st);
         }
     return launch_key_g<D, WPB, ROWS_VGPR, MSK>(log, req, out, st);

@@ -489,12 +489,15 @@ __global__ __launch_bounds__(64) void k_read6w(agn_ss_cache c, Read6Args a) {
     int64_t sum = 0;
     uint32_t cnt = 0;
     int64_t first_err = -1;
+    // the effect is loaded with the rows (not after the verdict: one round
+    // trip per iteration)
     for (uint64_t b = 0; b < n; b += F::S::OPI) {
+        const uint64_t pos = b + (uint64_t)f.slot;
+        int64_t ev = 0;
+        if (f.sub == 0 && pos < n) ev = a.eff[off + pos];
         bool valid;
         const bool incl = f.step(log, off, n, b, valid);
         const bool lead = incl && f.sub == 0;
-        int64_t ev = 0;
-        if (lead) ev = a.eff[off + b + (uint64_t)f.slot];
         const bool bad = lead && ev == AGN_EFFECT_INVALID;
         cnt += (uint32_t)__builtin_popcountll(ballot(lead));
         if (first_err < 0) {

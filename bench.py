@@ -389,14 +389,18 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
         # R masks that carry every DC are not read, a LastOpCt over every
         # column comes back as AGN_F_CT_FULL instead of a mask word
         r_full = not a.sparse.startswith("subset")
-        dr.hints = _abi.HINT_CT_FLAG | (_abi.HINT_R_FULL if r_full else 0)
+        # many keys whose entries differ (> 1/8): scanned in one pass
+        many_mixed = mixed * 8 > n_keys
+        dr.hints = _abi.HINT_CT_FLAG | (_abi.HINT_R_FULL if r_full else 0) | \
+            (_abi.HINT_MIXED if many_mixed else 0)
         # counter_pn reads a mask per entry only for the keys whose entries
         # differ (agn_log.key_mask); the set/register kernel reads every one
         per_entry = mixed if cfg["crdt_type"] == 1 else n_keys
         presence = {"mode": a.sparse, "key_mask": "agn_log_index_masks",
                     "uniform_keys": n_keys - mixed, "mixed_keys": mixed,
                     "mask_ops": per_entry * cfg["ops_per_key"],
-                    "hints": ["AGN_HINT_CT_FLAG"] + (["AGN_HINT_R_FULL"] if r_full else []),
+                    "hints": ["AGN_HINT_CT_FLAG"] + (["AGN_HINT_R_FULL"] if r_full else []) +
+                             (["AGN_HINT_MIXED"] if many_mixed else []),
                     "r_full": r_full}
     res = eng.alloc_result(n_keys, cfg["n_dcs"], sparse=bool(a.sparse), cap_off=cap)
 
@@ -509,6 +513,12 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
         traffic, traffic_src = pmc_traffic(a.config, n_keys,
                                            f"cfg{a.config}_sparse_{a.sparse}" if a.sparse else None)
+        kname = KERNEL_NAME[a.config]
+        if a.sparse and cfg["crdt_type"] == 1 and cfg["n_dcs"] == 8 and not many_mixed:
+            # the masked D = 8 batch: chunk 0 issued under the key's metadata,
+            # keys whose entries differ handed to a list pass (empty here)
+            kname = "k_counter_q8e (+ k_counter_q8m)"
+
         workload = cfg["name"].format(keys=fmt_keys(n_keys))
         if a.sparse:
             workload += f", presence masks on every clock ({a.sparse})"
@@ -528,7 +538,7 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src, "kernel": KERNEL_NAME[a.config],
+                         "traffic_source": traffic_src, "kernel": kname,
                          "kernel_ms": kern_ms, "algorithmic_bytes": bytes_launch,
                          "algorithmic_bytes_survey": bytes_survey,
                          "frac_survey_bytes": bytes_survey / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

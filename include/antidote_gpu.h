@@ -159,10 +159,15 @@ typedef struct agn_read {
  * caller checked; the masks are then not read).  AGN_HINT_CT_FLAG: the caller
  * reads lastct_mask through AGN_F_CT_FULL (a request whose LastOpCt carries
  * every column gets the flag instead of its mask word; see agn_result).  The
- * read batcher sets both from the requests it packs.  Kernels may ignore a
- * hint (then the mask is loaded / written as without it). */
+ * read batcher sets both from the requests it packs.  AGN_HINT_MIXED: many of
+ * the batch's keys carry entries with different DC sets (agn_log.key_mask 0,
+ * e.g. soon after a DC joined): the counter kernel scans them in the same
+ * pass instead of handing them on to a second one (which re-reads them).
+ * Kernels may ignore a hint (then the mask is loaded / written as without
+ * it); no hint changes a result. */
 #define AGN_HINT_R_FULL 0x1u
 #define AGN_HINT_CT_FLAG 0x2u
+#define AGN_HINT_MIXED 0x4u
 
 /* ---- results ----------------------------------------------------------- */
 typedef struct agn_result {

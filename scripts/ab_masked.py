@@ -38,6 +38,7 @@ VARIANTS = {
     "mixed_old": ("mixed", {"AGN_COUNTER_EARLY": "0"}, 0),
     "mixed": ("mixed", {}, 0),
     "mixed_km1": ("mixed", {"AGN_Q8E_KM": "1"}, 0),
+    "mixed_hint": ("mixed", {}, 0x4),   # AGN_HINT_MIXED: k_counter_key
 }
 KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM")
 

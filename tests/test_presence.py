@@ -87,19 +87,20 @@ def device_result(eng, log, req, index, hints=0):
 
 
 IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "split": "2", "split_km1": "2",
-         "split_ctflag": "2"}
+         "split_ctflag": "2", "split_mixed": "2"}
 
 
 @pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
 @pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "split", "split_km1",
-                                  "split_ctflag"])
+                                  "split_ctflag", "split_mixed"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
 def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
     """quad / quad2 / vgpr: k_counter_key (AGN_COUNTER_EARLY=0); split: the
     default masked D = 8 path -- k_counter_q8e with its hand-ons (keys whose
     entries differ) to the list pass k_counter_q8m; _km1 with the key's DC set
     loaded with the segment metadata (AGN_Q8E_KM=1), _ctflag with AGN_HINT_CT_FLAG
-    (LastOpCt masks over every column as AGN_F_CT_FULL)."""
+    (LastOpCt masks over every column as AGN_F_CT_FULL), _mixed with
+    AGN_HINT_MIXED (k_counter_key: the mixed keys in the same pass)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
     monkeypatch.setenv("AGN_COUNTER_EARLY", "1" if impl.startswith("split") else "0")
@@ -117,7 +118,8 @@ def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
         got = eng.materialize_host(log, req, sparse=True)
     else:
         got = device_result(eng, log, req, index=(path == "device_indexed"),
-                            hints=_abi.HINT_CT_FLAG if impl == "split_ctflag" else 0)
+                            hints={"split_ctflag": _abi.HINT_CT_FLAG,
+                                   "split_mixed": _abi.HINT_MIXED}.get(impl, 0))
     bad = compare(_abi.COUNTER_PN, D, got, want, True, req.n_req)
     assert not bad, bad[:10]
     # absent LastOpCt columns are 0, as the oracle writes them (a corrupted

@@ -131,7 +131,9 @@ def test_vnode_replay_sequential_vs_reference(eng, monkeypatch, read6, d):
                 if has_placeholder(vn, key):
                     quirk.add(key)
         ln, ll, ct = ol.key_meta()
-    assert served > 1000 and log_reads > 0
+    # (at D = 64 a read's clock is rarely below every kept snapshot within
+    # the run: the log fallback is exercised at the narrower widths)
+    assert served > 1000 and (log_reads > 0 or d > 16)
     assert len(quirk) < K // 2
     for k in range(K):
         if k in quirk or k not in vn.ops_cache:

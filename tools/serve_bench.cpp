@@ -28,7 +28,7 @@
 //
 //   serve_bench [type=counter|set|register] [keys=N] [ops=N] [dcs=N] [present=N]
 //               [sparse=0|1] [parts=N] [threads=N] [reads=N] [batch=N] [wait=US]
-//               [wps=N] [hot=N]
+//               [wps=N] [hot=N] [crash=1]
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -40,9 +40,86 @@
 #include <thread>
 #include <vector>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <ucontext.h>
+#include <unistd.h>
+
 #include "antidote_gpu.h"
 
 namespace {
+
+// crash=1: a SIGSEGV / SIGBUS handler (installed after agn_open, so it
+// replaces any a profiler's tool library installed) that names the faulting
+// address, the PC's shared object + symbol (dladdr), a backtrace, and the
+// /proc/self/maps lines around both -- where a crash under a profiler comes
+// from.  Only async-signal-tolerant calls on the raw fd; then the default
+// action (core) is restored and the signal re-raised.
+void put(const char *s) { (void)!write(2, s, std::strlen(s)); }
+void put_hex(const char *label, uint64_t v) {
+    char b[64];
+    std::snprintf(b, sizeof b, "%s0x%llx\n", label, (unsigned long long)v);
+    put(b);
+}
+void maps_near(uint64_t a) {
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd < 0) return;
+    static char buf[1 << 20];
+    ssize_t n = 0, r;
+    while (n < (ssize_t)sizeof buf - 1 && (r = read(fd, buf + n, sizeof buf - 1 - n)) > 0) n += r;
+    close(fd);
+    buf[n] = 0;
+    char *line = buf;
+    while (line && *line) {
+        char *nl = std::strchr(line, '\n');
+        if (nl) *nl = 0;
+        unsigned long long lo = 0, hi = 0;
+        if (std::sscanf(line, "%llx-%llx", &lo, &hi) == 2 && a + (2ull << 20) >= lo && a < hi + (2ull << 20)) {
+            put("  maps: ");
+            put(line);
+            put("\n");
+        }
+        if (nl) *nl = '\n';
+        line = nl ? nl + 1 : nullptr;
+    }
+}
+void on_crash(int sig, siginfo_t *si, void *ctx) {
+    const uint64_t addr = (uint64_t)si->si_addr;
+    const uint64_t pc = (uint64_t)((ucontext_t *)ctx)->uc_mcontext.gregs[REG_RIP];
+    put(sig == SIGSEGV ? "serve_bench: SIGSEGV\n" : "serve_bench: SIGBUS\n");
+    put_hex("  fault address: ", addr);
+    put_hex("  pc: ", pc);
+    put_hex("  thread: ", (uint64_t)gettid());
+    Dl_info di;
+    if (dladdr((void *)pc, &di)) {
+        put("  pc object: ");
+        put(di.dli_fname ? di.dli_fname : "?");
+        put("\n  pc symbol: ");
+        put(di.dli_sname ? di.dli_sname : "?");
+        put("\n");
+        put_hex("  pc - object base: ", pc - (uint64_t)di.dli_fbase);
+    }
+    void *bt[64];
+    const int nb = backtrace(bt, 64);
+    put("  backtrace:\n");
+    backtrace_symbols_fd(bt, nb, 2);
+    put("  mappings near the fault address:\n");
+    maps_near(addr);
+    put("  mappings near the pc:\n");
+    maps_near(pc);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+void install_crash_handler() {
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = on_crash;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigaction(SIGSEGV, &sa, nullptr);
+    sigaction(SIGBUS, &sa, nullptr);
+}
 
 uint64_t splitmix(uint64_t &s) {
     uint64_t z = (s += 0x9E3779B97F4A7C15ull);
@@ -88,7 +165,7 @@ void tag_effect(Partition &pt, uint32_t crdt, uint64_t k, uint64_t &seed, uint32
 
 int main(int argc, char **argv) {
     uint64_t K = 250000, N = 64, D = 8, P = 1, T = 20, M = 5000, batch = 1024, wait = 0, hot = 0;
-    uint64_t sparse = 0, present = 0;
+    uint64_t sparse = 0, present = 0, crash = 0;
     uint32_t crdt = AGN_COUNTER_PN;
     double wps = 0;
     for (int i = 1; i < argc; ++i) {
@@ -112,6 +189,7 @@ int main(int argc, char **argv) {
         else if (k == "hot") hot = std::strtoull(v, nullptr, 10);
         else if (k == "sparse") sparse = std::strtoull(v, nullptr, 10);
         else if (k == "present") present = std::strtoull(v, nullptr, 10);
+        else if (k == "crash") crash = std::strtoull(v, nullptr, 10);
         else if (k == "type") {
             const std::string t = v;
             crdt = t == "set" ? AGN_SET_AW : t == "register" ? AGN_REGISTER_MV : AGN_COUNTER_PN;
@@ -132,6 +210,7 @@ int main(int argc, char **argv) {
     agn_ctx *ctx = nullptr;
     int rc = agn_open(0, &ctx);
     if (rc) die("agn_open", rc);
+    if (crash) install_crash_handler();
     std::vector<Partition> parts(P);
     double t_load = now_s();
     for (uint64_t p = 0; p < P; ++p) {
