@@ -504,7 +504,7 @@ __global__ __launch_bounds__(64) void k_read6w(agn_ss_cache c, Read6Args a) {
             const uint64_t be = ballot(bad);
             if (be) first_err = (int64_t)b + (int64_t)(__builtin_ctzll(be) / LPO);
         }
-        sum += bad ? 0 : ev;
+        sum += (lead && !bad) ? ev : 0;  // ev is loaded for excluded ops too
     }
     const int64_t total = wave_sum_i64(sum);
     const bool ct_ign = f.sct_ign && cnt == 0u;

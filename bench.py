@@ -482,7 +482,7 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
     probe = probe_read_gbs(eng, dl, n_keys * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
 
     gc = gc_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.config) if a.gc else None
-    warm = warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.steps) if a.warm else None
+    warm = warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, a.steps, a.config) if a.warm else None
     ingest = ingest_bench(eng, cfg, sp, torch) if a.ingest else None
     e2e = e2e_bench(eng, dl, dr, res, cfg, n_keys, torch) if a.e2e else None
 
@@ -731,7 +731,7 @@ def e2e_bench(eng, dl, dr, res, cfg, n_keys, torch, chunk=1 << 20, reps=3):
             "note": "keys + R from pinned host, results to pinned host; 3 streams, 2-slot ring"}
 
 
-def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
+def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     """materializer_vnode:read/6 served from the device snapshot cache: one
     priming pass stores each key's snapshot (IsNewSS, >= 5 ops), then every
     timed step is get_from_snapshot_cache (agn_ss_lookup) -> materialize/4
@@ -740,7 +740,7 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
     from antidote_amd import _abi
     D = cfg["n_dcs"]
     if cfg["crdt_type"] != 1:
-        return warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps)
+        return warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id)
     S = _abi.SNAPSHOT_THRESHOLD
     bufs = {"n": eng.empty(4 * n_keys), "clock": eng.empty(8 * n_keys * S * D),
             "last_op": eng.empty(8 * n_keys * S), "value": eng.empty(8 * n_keys * S),
@@ -830,7 +830,7 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps):
             "error_keys": int((flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED)).astype(bool).sum())}
 
 
-def warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps):
+def warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     """read/6 of set_aw / register_mv keys from the device snapshot cache
     (materializer_vnode.erl:384-413,466-509: the cached #materialized_snapshot
     value is the full state): the cache carries a state arena, so a hit's base
@@ -918,8 +918,13 @@ def warm_bench_tags(eng, dl, dr, cfg, n_keys, sp, torch, steps):
     # row, its ignore flag and the base reference, and the base pairs read
     wbytes = (algorithmic_bytes(cfg, n_keys, n_rem, n_live) + n_keys * (8 * D + 1 + 8)
               + 12 * base_pairs)
+    # PMC bytes of the warm k_tags launches (scripts/gpu.sh pmcwarm: the
+    # steps launches before the steps + 1 agn_read_cached ones)
+    wtraffic, wsrc = pmc_traffic(cfg_id, n_keys, f"cfg{cfg_id}_warm") if cfg_id else \
+        (None, "null: config id not given")
     return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
             "materialize_algorithmic_bytes": wbytes,
+            "materialize_traffic": wtraffic, "materialize_traffic_source": wsrc,
             "materialize_frac": wbytes / (t_mat / steps * 1e-3) / 8e12,
             "store_ms": t_store / steps, "ops_per_s": ops / (ms * 1e-3),
             "read_cached_ms": t_rc / steps, "read_cached_ops_per_s": ops / (t_rc / steps * 1e-3),
