@@ -36,7 +36,7 @@ from oracle import py_oracle as po
 pytestmark = pytest.mark.gpu
 
 D = 3
-PTYPE = {_abi.SET_AW: po.SET_AW, _abi.REGISTER_MV: po.REGISTER_MV}
+PTYPE = {_abi.SET_AW: po.SET_AW, _abi.REGISTER_MV: po.REGISTER_MV, _abi.COUNTER_PN: po.COUNTER_PN}
 
 
 def vc(row, mask=None):
@@ -116,15 +116,17 @@ def append_entry(ol, key, oc, entry, txid, mask=None):
               txid=np.array([txid], np.uint64))
 
 
-def log_response(disk, key, R):
+def log_response(disk, key, R, new_value=None):
     """The Erlang side's read of the partition's disk log for a key
     (get_from_snapshot_log -> logging_vnode:get_up_to_time,
     src/logging_vnode.erl:185-190, 522-549, 586-591): its committed ops whose
     transaction snapshot <= R, newest first, ids from 0 at the oldest; base
-    {0, Type:new()}, snapshot time vectorclock:new(), not the newest."""
+    {0, Type:new()} (new_value; [] for set/register), snapshot time
+    vectorclock:new(), not the newest."""
     ops = [p for p in disk if p.key == key and po.vc_le(p.snapshot_time, R)]
     return SnapshotGetResponse([(i, p) for i, p in enumerate(ops)][::-1], len(ops),
-                               MaterializedSnapshot(0, []), {}, False)
+                               MaterializedSnapshot(0, [] if new_value is None else new_value),
+                               {}, False)
 
 
 class NifPartition:
@@ -142,9 +144,10 @@ class NifPartition:
         self.log_reads = self.log_gc = 0
 
     def from_log(self, key, R_dict, gc):
-        resp = log_response(self.disk, key, R_dict)
+        counter = self.typ == _abi.COUNTER_PN
+        resp = log_response(self.disk, key, R_dict, 0 if counter else None)
         if resp.number_of_ops == 0:
-            return ("ok", [])                     # materialize_snapshot :468-471
+            return ("ok", 0 if counter else [])  # materialize_snapshot :468-471
         r = cm.materialize(PTYPE[self.typ], IGNORE, R_dict, resp)
         if r[0] != "ok":
             return r
@@ -155,12 +158,16 @@ class NifPartition:
             for dc, t in ct.items():
                 row[dc] = t
                 m |= 1 << dc
-            if self.typ == _abi.SET_AW:
-                pairs = [(e, t) for e, toks in value for t in toks]
+            if counter:
+                self.bt.store(key, row, clock_mask=np.uint64(m) if self.sparse else None,
+                              last_op=hole, count=count, value=value, gc=True)
             else:
-                pairs = list(value)
-            self.bt.store(key, row, clock_mask=np.uint64(m), last_op=hole, count=count,
-                          tags=[e for e, _ in pairs], toks=[t for _, t in pairs], gc=True)
+                if self.typ == _abi.SET_AW:
+                    pairs = [(e, t) for e, toks in value for t in toks]
+                else:
+                    pairs = list(value)
+                self.bt.store(key, row, clock_mask=np.uint64(m), last_op=hole, count=count,
+                              tags=[e for e, _ in pairs], toks=[t for _, t in pairs], gc=True)
             self.log_gc += 1
         return ("ok", value)
 
