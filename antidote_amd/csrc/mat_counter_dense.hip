@@ -818,6 +818,74 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
                       o_err, mk.o_mask);
 }
 
+// Warm sparse batches (SCT given): k_counter_q8e with two requests per wave,
+// as k_counter_quad2 serves dense warm batches -- both keys' segment
+// metadata in one scalar round trip, both first chunks issued under it, the
+// side loads (R, SCT, the DC sets) under the chunks.  Mixed keys are handed
+// on to k_counter_q8m as in q8e.  (Round 3's two-request masked form carried
+// the per-entry-mask scan inline: 118 VGPRs, slower than one request.)
+template <bool KEYS>
+__global__ __launch_bounds__(64) void k_counter_q8e2(
+    DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
+    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
+    const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
+    const uint64_t *__restrict__ oc, const uint32_t *__restrict__ op_id,
+    const int64_t *__restrict__ eff, const uint64_t *__restrict__ log_txid,
+    const uint64_t *__restrict__ R, const uint64_t *__restrict__ sct,
+    const uint8_t *__restrict__ sct_ignore, const uint64_t *__restrict__ req_txid,
+    const int64_t *__restrict__ base_value, int64_t *__restrict__ o_value,
+    int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
+    uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
+    uint32_t *__restrict__ o_err, uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
+    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
+    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint64_t i0 = uniform_u64((uint64_t)blk * 2u);
+    if (i0 >= a.n_req) return;
+    const bool two = i0 + 1u < a.n_req;
+    const uint64_t i1 = two ? i0 + 1u : i0;
+    Q2Key k0, k1;
+    q2_meta(k0, i0, KEYS ? keys : nullptr, key_off, key_len, key_id0);
+    q2_meta(k1, i1, KEYS ? keys : nullptr, key_off, key_len, key_id0);
+    const bool any = a.n_entries != 0;
+    Q8Chunk c0{}, c1{};
+    if (any) {
+        c0 = q8_load<true, false>(oc, eff, k0.off, 0, a.n_entries);
+        c1 = q8_load<true, false>(oc, eff, k1.off, 0, a.n_entries);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t kmw0 = key_word(mk, k0.key, key_off), kmw1 = key_word(mk, k1.key, key_off);
+    q2_side<true, true>(k0, a, mk, kmw0, key_off, key_type, R, sct, sct_ignore, req_txid);
+    q2_side<true, true>(k1, a, mk, kmw1, key_off, key_type, R, sct, sct_ignore, req_txid);
+    auto mixed = [&](const Q2Key &k, uint64_t kmw) {
+        return !(mk.oc_mask == nullptr || (mk.key_mask && (kmw & 0xFFull)) || k.n == 0);
+    };
+    auto hand_on = [&](uint64_t i) {  // q8e's sub-lists
+        if (lane_id() == 0) {
+            const uint32_t sl = (uint32_t)(i % QL_S);
+            list[(uint64_t)sl * a.ql_cap + atomicAdd(list_n + sl * QL_STRIDE, 1u)] = (uint32_t)i;
+        }
+    };
+    const bool m0 = mixed(k0, kmw0), m1 = two && mixed(k1, kmw1);
+    if (m0) hand_on(i0);
+    if (m1) hand_on(i1);
+    Q2Acc s0, s1;
+    s0.ctA = k0.eA;
+    s0.ctB = k0.eB;
+    s1.ctA = k1.eA;
+    s1.ctB = k1.eB;
+    const bool d0 = any && !k0.corrupt && !m0, d1 = two && any && !k1.corrupt && !m1;
+    if (d0) q2_fold<true>(k0, c0, 0, log_txid, a.n_entries, s0);
+    if (d1) q2_fold<true>(k1, c1, 0, log_txid, a.n_entries, s1);
+    if (d0) q2_rest<true>(k0, oc, eff, log_txid, a.n_entries, s0);
+    if (d1) q2_rest<true>(k1, oc, eff, log_txid, a.n_entries, s1);
+    if (!m0)
+        q2_epilogue<true>(k0, s0, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count,
+                          o_flags, o_err, mk.o_mask);
+    if (two && !m1)
+        q2_epilogue<true>(k1, s1, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count,
+                          o_flags, o_err, mk.o_mask);
+}
+
 // The keys k_counter_q8e handed on (entries with different DC sets): the
 // per-entry-mask quad scan (scan_key_q8_msk), one request per wave, the
 // waves striding over the sub-lists -- the grid does not know their
@@ -938,8 +1006,17 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     const unsigned mb = QL_S * 16u;  // a multiple of QL_S
 #define AGN_Q8M(W, K)                                                                           \
     hipLaunchKernelGGL((k_counter_q8m<W, K>), dim3(mb), dim3(64), 0, st, AGN_ARGS)
+    // warm: two requests per wave unless AGN_Q8E_TWO=0
+    const char *tv = getenv("AGN_Q8E_TWO");
+    const bool two = !(tv && tv[0] == '0');
+    const unsigned nb2 = (unsigned)((req.n_req + 1) / 2);
+#define AGN_Q8E2(K)                                                                             \
+    hipLaunchKernelGGL((k_counter_q8e2<K>), dim3(nb2), dim3(64), 0, st, AGN_ARGS)
     if (rc == AGN_OK) {
-        if (req.sct) {
+        if (req.sct && two) {
+            if (req.keys) { AGN_Q8E2(true); AGN_Q8M(true, true); }
+            else { AGN_Q8E2(false); AGN_Q8M(true, false); }
+        } else if (req.sct) {
             if (req.keys) { AGN_Q8E(true, true); AGN_Q8M(true, true); }
             else { AGN_Q8E(true, false); AGN_Q8M(true, false); }
         } else {
@@ -948,6 +1025,7 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
         }
         if (hipGetLastError() != hipSuccess) rc = fail(AGN_EHIP, "counter q8e: launch");
     }
+#undef AGN_Q8E2
 #undef AGN_Q8M
 #undef AGN_Q8E
 #undef AGN_Q8E_
