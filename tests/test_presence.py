@@ -221,9 +221,10 @@ class DictWorkload:
     DCs 0..n0-1 from the start (n0 = 3: DC 3 joins at step JOIN; n0 = DCAP:
     every column interned, full clocks throughout)."""
 
-    def __init__(self, seed, K, n0=3):
+    def __init__(self, seed, K, n0=3, cap=DCAP):
         self.rng = np.random.default_rng(seed)
-        self.clk = np.zeros(DCAP, np.int64)
+        self.cap = cap
+        self.clk = np.zeros(cap, np.int64)
         self.clk[:n0] = 1000
         self.n_dc = n0
         self.K = K
@@ -238,7 +239,7 @@ class DictWorkload:
     def op(self):
         n = self.n_dc
         c = int(self.rng.integers(0, n))
-        ss = np.zeros(DCAP, np.int64)
+        ss = np.zeros(self.cap, np.int64)
         ss[:n] = np.maximum(self.clk[:n] - self.rng.integers(0, 40, n), 0)
         self.clk[c] += int(self.rng.integers(1, 30))
         oc = ss.copy()
@@ -250,7 +251,7 @@ class DictWorkload:
         n = self.n_dc
         if n == 4 and self.rng.random() < 0.1:
             n = 3   # a reader whose snapshot predates the new DC
-        R = np.zeros(DCAP, np.int64)
+        R = np.zeros(self.cap, np.int64)
         R[:n] = np.maximum(self.clk[:n] - self.rng.integers(0, lag, n), 0)
         return R, self.mask(n)
 
@@ -259,9 +260,12 @@ def dvc(row, n):
     return {d: int(row[d]) for d in range(n)}
 
 
+# width: the partition's columns (nif_part_open's D): 8 (k_read6), 16 / 64
+# (k_read6w, the fused read for wider clocks)
+@pytest.mark.parametrize("width", [8, 16, 64])
 @pytest.mark.parametrize("clocks", ["join", "full"])
 @pytest.mark.parametrize("read6", ["1", "0"])
-def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clocks):
+def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clocks, width):
     """update/2 + read/6 as nif/antidote_gpu_nif.c issues them, on a sparse
     log (presence masks; the NIF's configuration) and on a dense log: every
     read bit-identical between the two (value, NewLastOp, LastOpCt, Count,
@@ -272,11 +276,11 @@ def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clo
     start (the steady deployment: the dense routes serve every read)."""
     monkeypatch.setenv("AGN_READ6", read6)
     K, steps = 24, 3500
-    w = DictWorkload(23, K, n0=3 if clocks == "join" else DCAP)
+    w = DictWorkload(23 + width, K, n0=3 if clocks == "join" else width, cap=width)
     vn = po.MaterializerVnode()
     quirk, served, n_cmp = set(), 0, 0
-    with OpLog(eng, _abi.COUNTER_PN, DCAP, K, sparse=True) as ls, \
-            OpLog(eng, _abi.COUNTER_PN, DCAP, K, sparse=False) as ld, \
+    with OpLog(eng, _abi.COUNTER_PN, width, K, sparse=True) as ls, \
+            OpLog(eng, _abi.COUNTER_PN, width, K, sparse=False) as ld, \
             Batcher(ls, max_batch=8, cached=True) as bs, \
             Batcher(ld, max_batch=8, cached=True) as bd:
         for s in range(steps):
@@ -295,7 +299,7 @@ def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clo
                     if ol.gc_due(key)[0]:
                         bt.read(key, R=ss.astype(np.uint64),
                                 R_mask=np.array([w.mask()]) if sparse else None, gc=True)
-                    ol.append(np.array([key], np.uint64), oc.reshape(1, DCAP).astype(np.uint64),
+                    ol.append(np.array([key], np.uint64), oc.reshape(1, width).astype(np.uint64),
                               oc_mask=np.array([[w.mask()]]) if sparse else None,
                               eff=np.array([eff], np.int64), txid=np.array([s + 1], np.uint64))
                 if vn.ops_cache.get(key) and any(vn.ops_cache[key][po.FIRST_OP - 1 + i] == 0
