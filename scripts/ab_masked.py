@@ -39,7 +39,6 @@ VARIANTS = {
     "mixed": ("mixed", {}, 0),
     "mixed_km1": ("mixed", {"AGN_Q8E_KM": "1"}, 0),
     "mixed_hint": ("mixed", {}, 0x4),   # AGN_HINT_MIXED: k_counter_key
-    "masked_one": ("masked", {"AGN_Q8E_TWO": "0"}, 0x2),  # warm: one request per wave
     "masked_two": ("masked", {"AGN_Q8E_TWO": "1"}, 0x2),  # warm: k_counter_q8e2
 }
 KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM", "AGN_Q8E_TWO")

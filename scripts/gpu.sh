@@ -56,22 +56,22 @@ expand() {
       for c in ${PMC_CONFIGS-1 2 3 4 5}; do
         case $c in 1) k=k_counter_key; n=10000;; 2) k=k_counter_key; n=10000000;;
                    3) k=k_tags; n=1000000;; 4) k=k_tags; n=1000000;; 5) k=k_gst_cols; n=4096;; esac
-        echo "fetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
-        echo "write$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "fetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
+        echo "write$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "pmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_fetch$c/run_counter_collection.csv gpurun_out/prof_write$c/run_counter_collection.csv $k $n $c gpurun_out/pmc/cfg$c.json"
       done
       # the one-pass GC kernel (segmented agn_prune_ops) on the cfg2 / cfg3 logs
       for c in ${PMC_GC_CONFIGS-2 3}; do
         case $c in 2) n=10000000;; 3) n=1000000;; esac
-        echo "gcfetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_gcfetch$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
-        echo "gcwrite$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_gcwrite$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "gcfetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_gcfetch$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
+        echo "gcwrite$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_gcwrite$c -o run -- python3 bench.py --config $c --gc --steps 1 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "gcpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_gcfetch$c/run_counter_collection.csv gpurun_out/prof_gcwrite$c/run_counter_collection.csv k_prune_inplace $n gc gpurun_out/pmc/gc_cfg$c.json"
       done;;
     pmcsparse)
       # cfg2 with presence masks (bench.py --sparse MODE): the masked counter kernel
       for m in ${PMC_SPARSE-full mixed}; do
-        echo "sfetch$m|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_sfetch$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
-        echo "swrite$m|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_swrite$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "sfetch$m|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_sfetch$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
+        echo "swrite$m|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_swrite$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         case $m in mixed) sk=k_counter_key;; *) sk=k_counter_q8e;; esac
         echo "spmcj$m|60|python3 scripts/pmc_traffic.py gpurun_out/prof_sfetch$m/run_counter_collection.csv gpurun_out/prof_swrite$m/run_counter_collection.csv $sk 10000000 2 gpurun_out/pmc/cfg2_sparse_$m.json"
       done;;
@@ -79,8 +79,8 @@ expand() {
       # warm cfg3 / cfg4 (bench.py --warm: k_tags from the cached states): the
       # 3 warm steps' launches, before the 4 agn_read_cached ones
       for c in ${PMC_WARM-3 4}; do
-        echo "wfetch$c|240|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_wfetch$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
-        echo "wwrite$c|240|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_wwrite$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0"
+        echo "wfetch$c|240|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_wfetch$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
+        echo "wwrite$c|240|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_wwrite$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "wpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_wfetch$c/run_counter_collection.csv gpurun_out/prof_wwrite$c/run_counter_collection.csv k_tags 1000000 $c gpurun_out/pmc/cfg${c}_warm.json tail:3:4"
       done;;
     pmctail)

@@ -87,12 +87,12 @@ def device_result(eng, log, req, index, hints=0):
 
 
 IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "split": "2", "split_km1": "2",
-         "split_ctflag": "2", "split_mixed": "2", "split_one": "2"}
+         "split_ctflag": "2", "split_mixed": "2", "split_two": "2"}
 
 
 @pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
 @pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "split", "split_km1",
-                                  "split_ctflag", "split_mixed", "split_one"])
+                                  "split_ctflag", "split_mixed", "split_two"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
 def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
     """quad / quad2 / vgpr: k_counter_key (AGN_COUNTER_EARLY=0); split: the
@@ -100,14 +100,14 @@ def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
     entries differ) to the list pass k_counter_q8m; _km1 with the key's DC set
     loaded with the segment metadata (AGN_Q8E_KM=1), _ctflag with AGN_HINT_CT_FLAG
     (LastOpCt masks over every column as AGN_F_CT_FULL), _mixed with
-    AGN_HINT_MIXED (k_counter_key: the mixed keys in the same pass); the warm
-    requests (SCT given) run two per wave (k_counter_q8e2), _one: one per
-    wave (AGN_Q8E_TWO=0)."""
+    AGN_HINT_MIXED (k_counter_key: the mixed keys in the same pass), _two with
+    the warm requests (SCT given) two per wave (k_counter_q8e2,
+    AGN_Q8E_TWO=1)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
     monkeypatch.setenv("AGN_COUNTER_EARLY", "1" if impl.startswith("split") else "0")
     monkeypatch.setenv("AGN_Q8E_KM", "1" if impl == "split_km1" else "0")
-    monkeypatch.setenv("AGN_Q8E_TWO", "0" if impl == "split_one" else "1")
+    monkeypatch.setenv("AGN_Q8E_TWO", "1" if impl == "split_two" else "0")
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
     else:
