@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OK = 0
 EINVAL, EHIP, ENOMEM, ECAPACITY, ENOTSUP, ERCCL, ENODEV = -1, -2, -3, -4, -5, -6, -7
@@ -129,6 +129,7 @@ class AgnGenCfg(C.Structure):
 PROTOTYPES = {
     "agn_abi_version": (C.c_int, []),
     "agn_last_error": (C.c_char_p, []),
+    "agn_env_reload": (C.c_int, []),
     "agn_strerror": (C.c_char_p, [C.c_int]),
     "agn_open": (C.c_int, [C.c_int, C.POINTER(P)]),
     "agn_close": (C.c_int, [P]),

@@ -60,3 +60,20 @@ def check(rc: int, what: str = ""):
         msg = lib.agn_last_error().decode(errors="replace")
         raise EngineError(rc, f"{what}: {msg}" if what else msg)
     return rc
+
+
+def env_changed():
+    """Tell the library that an AGN_* environment knob changed in this process
+    (it caches them: agn_env_reload).  A no-op before the library is loaded."""
+    if _lib is not None:
+        _lib.agn_env_reload()
+
+
+def set_knob(name, value):
+    """Set (value given) or unset (None) an AGN_* knob for this process and
+    pass the change on to the library."""
+    if value is None:
+        os.environ.pop(name, None)
+    else:
+        os.environ[name] = value
+    env_changed()

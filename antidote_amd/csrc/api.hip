@@ -37,6 +37,19 @@ struct agn_ctx {
     // host-staged materialize: stagers (stream + buffers) reused across calls
     std::mutex st_mu;
     std::vector<agn::Stager *> st_all, st_free;
+    // agn_log_index_masks' mixed-key count per key_mask buffer it built (the
+    // last kMaskIdx): agn_materialize adds AGN_HINT_MIXED to a batch over such
+    // a log when enough of its keys are mixed -- a hint changes no result, so
+    // a stale entry (a buffer rewritten by the caller) only costs speed
+    struct MaskIdx {
+        const uint64_t *key_mask;
+        uint64_t n_keys, mixed;
+    };
+    static constexpr int kMaskIdx = 16;
+    std::mutex mi_mu;
+    MaskIdx mi[kMaskIdx] = {};
+    unsigned mi_next = 0;
+    std::atomic<bool> mi_any{false};
 };
 
 namespace agn {
@@ -64,6 +77,22 @@ int use_device(agn_ctx *ctx) {
     return AGN_OK;
 }
 
+// ---- cached environment knobs (common.hpp EnvKnob) -------------------------
+std::atomic<uint32_t> g_env_gen{1};
+static std::mutex g_env_mu;
+
+void EnvKnob::refresh(uint32_t g) {
+    std::lock_guard<std::mutex> lk(g_env_mu);
+    if (gen_.load(std::memory_order_relaxed) == g) return;
+    const char *v = getenv(name_);
+    set_ = v != nullptr;
+    if (v) {
+        strncpy(val_, v, sizeof val_ - 1);
+        val_[sizeof val_ - 1] = 0;
+    }
+    gen_.store(g, std::memory_order_release);
+}
+
 // ---- the library's memory pools (one per device) ---------------------------
 namespace {
 constexpr int kMaxDevices = 64;
@@ -72,7 +101,7 @@ hipMemPool_t g_pool[kMaxDevices] = {};
 int g_pool_users[kMaxDevices] = {};
 
 uint64_t pool_keep_bytes() {
-    const char *v = getenv("AGN_POOL_KEEP");
+    const char *v = AGN_KNOB("AGN_POOL_KEEP");
     if (!v || !*v) return UINT64_MAX;
     return strtoull(v, nullptr, 10);
 }
@@ -101,9 +130,9 @@ hipError_t pool_of(int dev, hipMemPool_t *out) {
 hipError_t pool_malloc(void **p, size_t bytes, hipStream_t st) {
     // test hook: AGN_TEST_POOL_FAIL=n makes the n-th allocation from now fail
     // (tests/test_oplog.py drives the all-or-nothing paths with it)
-    // (unset -- every production call -- costs one getenv and no lock)
+    // (unset -- every production call -- costs one cached-knob load and no lock)
     static std::atomic<bool> was_armed{false};
-    const char *v = getenv("AGN_TEST_POOL_FAIL");
+    const char *v = AGN_KNOB("AGN_TEST_POOL_FAIL");
     if (v || was_armed.load(std::memory_order_relaxed)) {
         static std::mutex mu;
         static std::string armed;
@@ -129,6 +158,17 @@ hipError_t pool_malloc(void **p, size_t bytes, hipStream_t st) {
 }
 
 static bool is_tag_type(uint32_t t) { return t == AGN_SET_AW || t == AGN_REGISTER_MV; }
+
+// A log whose key_mask agn_log_index_masks built (same buffer, same key
+// count) with many mixed keys (many_mixed).
+static bool mixed_log(agn_ctx *ctx, const agn_log *log) {
+    if (!ctx->mi_any.load(std::memory_order_acquire)) return false;
+    std::lock_guard<std::mutex> g(ctx->mi_mu);
+    for (const auto &m : ctx->mi)
+        if (m.key_mask == log->key_mask && m.n_keys == log->n_keys)
+            return many_mixed(m.mixed, m.n_keys);
+    return false;
+}
 
 static int validate(const agn_log *log, const agn_read *req, const agn_result *out) {
     if (!log || !req || !out) return fail(AGN_EINVAL, "null descriptor");
@@ -165,6 +205,11 @@ extern "C" {
 int agn_abi_version(void) { return AGN_ABI_VERSION; }
 
 const char *agn_last_error(void) { return g_err; }
+
+int agn_env_reload(void) {
+    g_env_gen.fetch_add(1, std::memory_order_acq_rel);
+    return AGN_OK;
+}
 
 const char *agn_strerror(int code) {
     switch (code) {
@@ -300,7 +345,15 @@ int agn_materialize(agn_ctx *ctx, const agn_log *log, const agn_read *req, agn_r
     if (rc) return rc;
     if (req->n_req == 0) return AGN_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (log->crdt_type == AGN_COUNTER_PN) return launch_counter(*log, *req, *out, s);
+    if (log->crdt_type == AGN_COUNTER_PN) {
+        if (log->oc_mask && log->key_mask && !(req->hints & AGN_HINT_MIXED) &&
+            mixed_log(ctx, log)) {
+            agn_read r = *req;
+            r.hints |= AGN_HINT_MIXED;
+            return launch_counter(*log, r, *out, s);
+        }
+        return launch_counter(*log, *req, *out, s);
+    }
     return launch_tags(*log, *req, *out, s);
 }
 
@@ -341,7 +394,17 @@ int agn_log_index_masks(agn_ctx *ctx, const agn_log *log, uint64_t *out, void *s
         return fail(AGN_EINVAL, "index_masks: n_dcs=%u not in [1,64]", log->n_dcs);
     int rc = use_device(ctx);
     if (rc) return rc;
-    return launch_index_masks(*log, out, (hipStream_t)stream);
+    uint64_t mixed = 0;
+    rc = launch_index_masks(*log, out, log->oc_mask ? &mixed : nullptr, (hipStream_t)stream);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(ctx->mi_mu);
+    int slot = -1;
+    for (int i = 0; i < agn_ctx::kMaskIdx && slot < 0; ++i)
+        if (ctx->mi[i].key_mask == out) slot = i;
+    if (slot < 0) slot = (int)(ctx->mi_next++ % agn_ctx::kMaskIdx);
+    ctx->mi[slot] = {out, log->n_keys, mixed};
+    ctx->mi_any.store(true, std::memory_order_release);
+    return AGN_OK;
 }
 
 int agn_state_capacity(const agn_log *log, const agn_read *req, uint64_t *cap_off) {
@@ -708,7 +771,7 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
 // the fused kernel's single launch wins below.  AGN_READ_CACHED_SPLIT=<n>
 // moves the switch (0: never).
 static uint64_t read_cached_split() {
-    const char *v = getenv("AGN_READ_CACHED_SPLIT");
+    const char *v = AGN_KNOB("AGN_READ_CACHED_SPLIT");
     if (v && v[0]) {
         const uint64_t n = strtoull(v, nullptr, 10);
         return n ? n : ~0ull;

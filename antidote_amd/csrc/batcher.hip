@@ -734,6 +734,10 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
         req.txid = (const uint64_t *)(d + o_txid);
         req.req_type = B->crdt;
         req.base_value = (const int64_t *)(d + o_base);
+        // many of the batch's keys with entries of different DC sets (e.g.
+        // soon after a DC joined): the counter kernel scans them in one pass
+        if (sparse && many_mixed(oplog_mixed_keys(B->log, n, keys.data()), n))
+            req.hints |= AGN_HINT_MIXED;
         agn_result res;
         std::memset(&res, 0, sizeof res);
         res.value = (int64_t *)(d + o_val);
@@ -884,6 +888,8 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
             for (uint32_t x = 0; m && x < W && rfull; ++x) rfull = (m[x] & full[x]) == full[x];
         }
         req.hints = AGN_HINT_CT_FLAG | (rfull ? AGN_HINT_R_FULL : 0u);
+        if (!tags && many_mixed(oplog_mixed_keys(B->log, n, keys.data()), n))
+            req.hints |= AGN_HINT_MIXED;
     }
     if (tags) {
         req.base_off = (const uint64_t *)(d + o_boff);
@@ -1017,7 +1023,10 @@ int run_store(agn_batcher *B, const StoreReq &s) {
         }
         agn_log view;
         oplog_view(B->log, &view);
-        rc = launch_ss_store_req(B->ss, view.key_off, view.key_len, 1,
+        // no key_off: the store's op count is the log response's (> 0, the
+        // caller's check, :469-475), not the device list's, which a GC may
+        // have emptied
+        rc = launch_ss_store_req(B->ss, nullptr, nullptr, 1,
                                  (const uint64_t *)(B->dbuf + d_keys), (const uint8_t *)(x + o_first),
                                  (const uint8_t *)(x + o_st), (const uint8_t *)(x + o_gc), res,
                                  (uint8_t *)(B->dbuf + d_pr), B->thr, B->thrm, B->stream);
@@ -1183,7 +1192,7 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     if (crdt != AGN_COUNTER_PN) {
         c.state_cap = std::max<uint64_t>(16 * K1, 1u << 16);
         // test knob: a small first arena, so re-packs and growth happen early
-        const char *ai = getenv("AGN_SS_ARENA_INIT");
+        const char *ai = AGN_KNOB("AGN_SS_ARENA_INIT");
         if (ai && std::strtoull(ai, nullptr, 10) > 0) c.state_cap = std::strtoull(ai, nullptr, 10);
         if (e == hipSuccess) e = hipMalloc((void **)&c.state_tag, c.state_cap * 4);
         if (e == hipSuccess) e = hipMalloc((void **)&c.state_tok, c.state_cap * 8);
@@ -1210,9 +1219,9 @@ int agn_batcher_create_cached(agn_oplog *log, uint32_t slots, uint32_t max_batch
     // the worker only looks at `cached` under the queue lock, after a read arrives
     std::lock_guard<std::mutex> g((*out)->mu);
     (*out)->cached = true;
-    const char *r6 = getenv("AGN_READ6");
+    const char *r6 = AGN_KNOB("AGN_READ6");
     (*out)->read6 = !(r6 && r6[0] == '0');
-    const char *tf = getenv("AGN_TAGS_FUSED");
+    const char *tf = AGN_KNOB("AGN_TAGS_FUSED");
     (*out)->tags_fused = !(tf && tf[0] == '0');
     (*out)->ss = c;
     (*out)->thr = thr;

@@ -71,8 +71,12 @@ __global__ __launch_bounds__(256) void k_ss_store(agn_ss_cache c, const uint64_t
     // a state arena stores the result's state pairs (set_aw / register_mv)
     const bool st = c.state_tag != nullptr && res.out_off != nullptr;
     const uint64_t so = st ? res.out_off[i] : 0ull;
+    // nops: the key's device op count (number_of_ops of the read's ops list,
+    // :468-471); without key_off the caller's snapshot came from a log
+    // response whose number_of_ops it checked (agn_batcher_store): not 0
+    const uint64_t nops = key_off ? key_n(key_off, key_len, k) : 1ull;
     const bool pr = ss_store_one<G>(
-        g, c, k, key_n(key_off, key_len, k), status[i], is_first[i],
+        g, c, k, nops, status[i], is_first[i],
         should_gc != nullptr && should_gc[i] != 0, res.lastct + i * D,
         res.lastct_mask ? res.lastct_mask + i * W : nullptr, res.hole[i],
         (handle && !st) ? handle[i] : st ? 0 : res.value[i], res.count[i], res.flags[i], thr, thrm,

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
 #include <shared_mutex>
 
 #include "../../include/antidote_gpu.h"
@@ -12,6 +13,35 @@
 #define AGN_WAVE 64
 
 namespace agn {
+
+// Environment knobs (A/B switches and test hooks, AGN_*): each is read once
+// and cached, so a launch costs one atomic load instead of a getenv walk over
+// the environment (serving batches launch every few microseconds).
+// agn_env_reload() bumps g_env_gen and every knob re-reads its variable at
+// its next use -- the tests and A/B scripts change knobs between launches.
+extern std::atomic<uint32_t> g_env_gen;
+class EnvKnob {
+  public:
+    explicit EnvKnob(const char *name) : name_(name) {}
+    const char *get() {  // the variable's value, nullptr when unset
+        const uint32_t g = g_env_gen.load(std::memory_order_acquire);
+        if (gen_.load(std::memory_order_acquire) != g) refresh(g);
+        return set_ ? val_ : nullptr;
+    }
+
+  private:
+    void refresh(uint32_t g);  // api.hip
+    const char *name_;
+    std::atomic<uint32_t> gen_{0};
+    bool set_ = false;
+    char val_[48] = {};
+};
+// getenv(NAME) through a per-call-site cached knob
+#define AGN_KNOB(NAME)                     \
+    ([]() -> const char * {                \
+        static ::agn::EnvKnob knob_(NAME); \
+        return knob_.get();                \
+    }())
 
 // Thread-local last-error message (agn_last_error).
 void set_error(const char *fmt, ...);
@@ -113,9 +143,17 @@ __device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
     return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
 }
 
+// AGN_HINT_MIXED routing threshold: a masked counter batch with more than
+// 1/16 of its keys mixed (entries with different DC sets) is scanned in one
+// pass (k_counter_key MSK, 1.11x dense on uniform keys, 1.24x on mixed ones)
+// instead of k_counter_q8e + the hand-on (1.04x, and ~2.5x for a mixed
+// 64-op key, whose only chunk q8e reads before handing it on): break-even
+// near a twentieth of the keys.
+inline bool many_mixed(uint64_t mixed, uint64_t n) { return mixed * 16 > n; }
+
 // A/B knob AGN_XCD_REMAP=0|1 (default on).
 inline bool xcd_remap() {
-    const char *v = getenv("AGN_XCD_REMAP");
+    const char *v = AGN_KNOB("AGN_XCD_REMAP");
     return !(v && v[0] == '0');
 }
 
@@ -156,13 +194,14 @@ void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, u
 int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *keys,
                      uint32_t *lens, std::shared_lock<std::shared_mutex> &hold);
 void oplog_view(const agn_oplog *L, agn_log *v);
+uint64_t oplog_mixed_keys(agn_oplog *L, uint64_t n, const uint64_t *keys);
 agn_ctx *oplog_ctx(const agn_oplog *L);
 
 // Launchers (defined in the .hip files).
 int launch_counter(const agn_log &log, const agn_read &req, const agn_result &out,
                    hipStream_t s);
 int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st);
-int launch_index_masks(const agn_log &log, uint64_t *out, hipStream_t st);
+int launch_index_masks(const agn_log &log, uint64_t *out, uint64_t *mixed, hipStream_t st);
 int launch_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,
                          hipStream_t s);
 int tune_counter_dense(const agn_log &log, const agn_read &req, const agn_result &out,

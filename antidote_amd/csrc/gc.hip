@@ -1253,14 +1253,14 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
                   const uint64_t *thr_mask, uint32_t *meta, uint32_t *flags, hipStream_t st) {
     // waves per block: 1 (default; the grid is the key list, as the counter
     // kernel) or 4 (AGN_PRUNE_WPB=4, A/B knob)
-    const char *ev = getenv("AGN_PRUNE_WPB");
+    const char *ev = AGN_KNOB("AGN_PRUNE_WPB");
     const bool w4 = ev && ev[0] == '4';
     const unsigned blocks = grid_for(a.n_keys, w4 ? 4 : 1, 0x7fffffffu);
     const bool full = !a.mask && (DPL % 2 == 0) && a.D == (uint32_t)(DPL * LPO);
     const bool tags = a.rem_off != nullptr;
     // the register budget of MINW waves per SIMD instead of the compiler's
     // choice: AGN_PRUNE_MINW=6|8 (A/B knob; the tail kernel: 8, counter only)
-    const char *mw = getenv("AGN_PRUNE_MINW");
+    const char *mw = AGN_KNOB("AGN_PRUNE_MINW");
     const bool mw6 = mw && mw[0] == '6', mw8 = mw && mw[0] == '8';
     if (a.d_key_off && a.meta6) {  // the engine-owned log: toward the end of the live range
         // waves per block: 1 (default) or 4 (AGN_PRUNE_WPB=4, A/B knob).  The
@@ -1268,7 +1268,7 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         // (prefix drop, 2M x 64: 2.43 vs 2.53 ms for the GC call, 4 waves
         // per block 2.93; profiles/r03/ab_prune_tail.log); AGN_PRUNE_TAIL_MINW=1
         // gives the compiler's allocation (7 waves)
-        const char *tmw = getenv("AGN_PRUNE_TAIL_MINW");
+        const char *tmw = AGN_KNOB("AGN_PRUNE_TAIL_MINW");
         const bool w8 = !(tmw && tmw[0] == '1');
         // counter_pn with dense 8-DC rows: KPW keys per wave, every key's
         // metadata and newest chunk in flight before the first is walked --
@@ -1276,7 +1276,7 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
         // 2.43 for one key per wave at 8 waves per SIMD and 2.35 for 4 keys;
         // profiles/r03/ab_prune_tail_kpw.log); AGN_PRUNE_TAIL_KPW=1|2|4
         if constexpr (DPL == 8 && LPO == 1 && !SPARSE) {
-            const char *kv = getenv("AGN_PRUNE_TAIL_KPW");
+            const char *kv = AGN_KNOB("AGN_PRUNE_TAIL_KPW");
             const int kpw = kv ? atoi(kv) : 2;
             if (full && !tags && !w4 && (kpw == 2 || kpw == 4)) {
                 if (kpw == 2)
@@ -1337,7 +1337,7 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     // (cfg3: 13.79 vs 13.26; profiles/r03/*_abp{2,3}.log); AGN_PRUNE_CT=0|1
     // (A/B knob) overrides
     if constexpr (DPL == 8 && !SPARSE) {
-        const char *cv = getenv("AGN_PRUNE_CT");
+        const char *cv = AGN_KNOB("AGN_PRUNE_CT");
         const bool ct = (cv && (cv[0] == '0' || cv[0] == '1')) ? cv[0] == '1' : !tags;
         if (full && ct && !w4) {
             if (tags)
@@ -1356,7 +1356,7 @@ int inplace_shape(const InplaceArgs &a, const uint8_t *prune, const uint64_t *th
     // ms on two boxes), AGN_PRUNE_PF=0|1|2|3 (A/B knob; 3: with the next
     // iteration's fields predicted (EF); 2: held to 5 waves per
     // SIMD, slower: 14.5)
-    const char *pv = getenv("AGN_PRUNE_PF");
+    const char *pv = AGN_KNOB("AGN_PRUNE_PF");
     const int pf = w4 || mw6 || mw8 ? 0
                    : (pv && pv[0] >= '0' && pv[0] <= '3') ? pv[0] - '0'
                    : (tags ? 1 : 0);
@@ -1438,9 +1438,9 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.key_list = nullptr;
     a.list_flags = nullptr;
     a.xcd = xcd_remap() ? 1 : 0;
-    const char *lf = getenv("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
+    const char *lf = AGN_KNOB("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
-    const char *tc = getenv("AGN_PRUNE_TCOOP");  // A/B knob: 0 | 1
+    const char *tc = AGN_KNOB("AGN_PRUNE_TCOOP");  // A/B knob: 0 | 1
     a.tcoop = (tc && tc[0] == '1') ? 1 : 0;
     a.meta6 = 0;
     return a;
@@ -1449,7 +1449,7 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
 // The engine-owned log's prune: toward the end of the live range (k_prune_tail)
 // unless AGN_PRUNE_TAIL=0 (A/B knob: the start-anchored k_prune_inplace).
 void engine_log_mode(InplaceArgs &a, const agn_log &view) {
-    const char *v = getenv("AGN_PRUNE_TAIL");
+    const char *v = AGN_KNOB("AGN_PRUNE_TAIL");
     a.meta6 = 1;
     a.d_key_off = (v && v[0] == '0') ? nullptr : const_cast<uint64_t *>(view.key_off);
 }

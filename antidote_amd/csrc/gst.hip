@@ -256,14 +256,14 @@ int launch_gst_min(uint32_t D, uint64_t P, uint64_t E, const uint64_t *clocks,
         // column-resident kernel: ~target blocks over all epochs, >= 32 block
         // steps each.  A/B knobs: AGN_GST_BLOCKS (target, default 1024),
         // AGN_GST_UNROLL = 4 | 8 (rows in flight per thread)
-        const char *eb = getenv("AGN_GST_BLOCKS");
-        const char *eu = getenv("AGN_GST_UNROLL");
+        const char *eb = AGN_KNOB("AGN_GST_BLOCKS");
+        const char *eu = AGN_KNOB("AGN_GST_UNROLL");
         const uint64_t target = eb ? strtoull(eb, nullptr, 10) : 1024;
         const int unroll = (eu && eu[0] == '8') ? 8 : 4;
         // non-temporal row loads (default; AGN_GST_NT=0 for plain loads): the
         // clocks are streamed once, 0.366 -> 0.311 ms on cfg5 (scripts/ab_gst.py,
         // profiles/r02/ab_gst.log)
-        const char *en = getenv("AGN_GST_NT");
+        const char *en = AGN_KNOB("AGN_GST_NT");
         const bool nt = !(en && en[0] == '0');
         const uint64_t RG = (2u * GST_THREADS) / D;
         uint64_t bands = ((target ? target : 1024) + E - 1) / E;

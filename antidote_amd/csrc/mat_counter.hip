@@ -106,7 +106,7 @@ int launch_counter(const agn_log &log, const agn_read &req, const agn_result &ou
     if (req.n_req == 0) return AGN_OK;
     // AGN_COUNTER_IMPL=general forces the general kernel (A/B and tests)
     const bool force_general = [] {
-        const char *v = getenv("AGN_COUNTER_IMPL");
+        const char *v = AGN_KNOB("AGN_COUNTER_IMPL");
         return v && v[0] == 'g';
     }();
     if (!force_general) {

@@ -30,6 +30,7 @@
 // the LDS-DMA path also reads the chunk's 4-byte op ids (+4 per op).
 #include <atomic>
 #include <cstdlib>
+#include <vector>
 
 #include "counter_scan.hpp"
 
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
 
 // agn_log.key_id0, unless AGN_COUNTER_ID0=0 (A/B knob: always load the op id)
 inline const uint32_t *id0_index(const agn_log &log) {
-    const char *v = getenv("AGN_COUNTER_ID0");
+    const char *v = AGN_KNOB("AGN_COUNTER_ID0");
     return (v && v[0] == '0') ? nullptr : log.key_id0;
 }
 
@@ -966,10 +967,13 @@ int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out,
 // k_counter_key, which scans a mixed key in the same pass (cfg2 with one
 // entry in 8 lacking a DC: 1.24x dense there, 2.56x through the hand-on,
 // whose first pass reads the key's only chunk for nothing;
-// profiles/r04/ab_masked_*).  AGN_Q8E_KM=0 loads
-// the key's DC set under the first chunk instead of with the metadata.
+// profiles/r04/ab_masked_*).  The hint comes from the caller, from the read
+// batcher (the op log's host copy of the key DC sets) or from agn_materialize
+// itself for a key_mask that agn_log_index_masks built (many_mixed).  By
+// default q8e loads the key's DC set under the first chunk; AGN_Q8E_KM=1
+// loads it with the segment metadata instead.
 inline bool early_chunk() {
-    const char *v = getenv("AGN_COUNTER_EARLY");
+    const char *v = AGN_KNOB("AGN_COUNTER_EARLY");
     return !(v && v[0] == '0');
 }
 
@@ -981,7 +985,7 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     // the key's DC set loaded under the first chunk (default; cold masked
     // cfg2 1.047x dense vs 1.107x with the metadata, profiles/r04/), or with
     // the segment metadata (AGN_Q8E_KM=1)
-    const char *kv = getenv("AGN_Q8E_KM");
+    const char *kv = AGN_KNOB("AGN_Q8E_KM");
     const bool km0 = !(kv && kv[0] == '1');
     // QL_S counters (QL_STRIDE apart), then QL_S sub-lists of ql_cap indices
     a.ql_cap = (uint32_t)((req.n_req + QL_S - 1) / QL_S);
@@ -1008,7 +1012,7 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     hipLaunchKernelGGL((k_counter_q8m<W, K>), dim3(mb), dim3(64), 0, st, AGN_ARGS)
     // warm: two requests per wave with AGN_Q8E_TWO=1 (k_counter_q8e2; not
     // yet measured against one request per wave, so not the default)
-    const char *tv = getenv("AGN_Q8E_TWO");
+    const char *tv = AGN_KNOB("AGN_Q8E_TWO");
     const bool two = tv && tv[0] == '1';
     const unsigned nb2 = (unsigned)((req.n_req + 1) / 2);
 #define AGN_Q8E2(K)                                                                             \
@@ -1039,7 +1043,7 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
 // Two chunks per step for D <= 4 (scan_key PAIR), unless AGN_COUNTER_PAIR=0
 // (A/B knob).
 inline uint32_t pair_chunks() {
-    const char *v = getenv("AGN_COUNTER_PAIR");
+    const char *v = AGN_KNOB("AGN_COUNTER_PAIR");
     return (v && v[0] == '0') ? 0u : 1u;
 }
 
@@ -1069,9 +1073,9 @@ inline int cur_dev() {
 }
 
 inline int forced_variant() {
-    const char *v = getenv("AGN_COUNTER_VARIANT");
+    const char *v = AGN_KNOB("AGN_COUNTER_VARIANT");
     if (v && v[0] >= '0' && v[0] <= '3') return v[0] - '0';
-    v = getenv("AGN_COUNTER_GLDS");
+    v = AGN_KNOB("AGN_COUNTER_GLDS");
     if (v && (v[0] == '0' || v[0] == '1')) return v[0] - '0';
     return -1;
 }
@@ -1090,7 +1094,7 @@ int counter_variant() {
 
 template <int D, int WPB, int VAR, bool KEYS, bool MSK>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    const char *qv = getenv("AGN_COUNTER_QUAD_NT");
+    const char *qv = AGN_KNOB("AGN_COUNTER_QUAD_NT");
     DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, pair_chunks(),
                 (qv && qv[0] >= '0' && qv[0] <= '3') ? (uint32_t)(qv[0] - '0') : 1u};
     const MaskArgs mk = mask_args(log, req, out);
@@ -1171,28 +1175,42 @@ int launch_dense(const agn_log &log, const agn_read &req, const agn_result &out,
 
 // agn_log_index_masks: one wave per key; out[k] = the mask word every entry
 // of the segment carries (low D bits), 0 when they differ or the key is empty.
+// The block's mixed keys (non-empty, entries differ) are added to one of
+// IM_CNT counters (IM_STRIDE words apart: one counter per 128-byte line).
+constexpr uint32_t IM_CNT = 256, IM_STRIDE = 16;
 __global__ __launch_bounds__(256) void k_index_masks(const uint64_t *__restrict__ key_off,
                                                     const uint64_t *__restrict__ key_len,
                                                     const uint64_t *__restrict__ oc_mask,
                                                     uint64_t full, uint64_t n_keys,
-                                                    uint64_t *__restrict__ out) {
+                                                    uint64_t *__restrict__ out,
+                                                    unsigned long long *__restrict__ mixed) {
+    __shared__ uint32_t blk_mixed;
+    if (threadIdx.x == 0) blk_mixed = 0;
+    __syncthreads();
     const uint64_t k = uniform_u64((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6));
-    if (k >= n_keys) return;
     const int lane = lane_id();
-    const uint64_t off = key_off[k];
-    const uint64_t n = key_len ? key_len[k] : key_off[k + 1] - off;
-    if (n == 0 || oc_mask == nullptr) {
-        if (lane == 0) out[k] = n ? full : 0ull;
-        return;
+    if (k < n_keys) {
+        const uint64_t off = key_off[k];
+        const uint64_t n = key_len ? key_len[k] : key_off[k + 1] - off;
+        if (n == 0 || oc_mask == nullptr) {
+            if (lane == 0) out[k] = n ? full : 0ull;
+        } else {
+            const uint64_t m0 = uniform_u64(oc_mask[off]) & full;
+            bool ok = true;
+            for (uint64_t b = 0; ok && b < n; b += AGN_WAVE) {
+                const uint64_t p = b + (uint64_t)lane;
+                const bool bad = p < n && (oc_mask[off + p] & full) != m0;
+                ok = ballot(bad) == 0;
+            }
+            if (lane == 0) {
+                out[k] = ok ? m0 : 0ull;
+                if (!ok) atomicAdd(&blk_mixed, 1u);
+            }
+        }
     }
-    const uint64_t m0 = uniform_u64(oc_mask[off]) & full;
-    bool ok = true;
-    for (uint64_t b = 0; ok && b < n; b += AGN_WAVE) {
-        const uint64_t p = b + (uint64_t)lane;
-        const bool bad = p < n && (oc_mask[off + p] & full) != m0;
-        ok = ballot(bad) == 0;
-    }
-    if (lane == 0) out[k] = ok ? m0 : 0ull;
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_mixed && mixed)
+        atomicAdd(&mixed[(blockIdx.x % IM_CNT) * IM_STRIDE], (unsigned long long)blk_mixed);
 }
 
 // agn_log_index_ids: one wave per key, lanes over the segment's positions.
@@ -1221,15 +1239,36 @@ __global__ __launch_bounds__(256) void k_index_ids(const uint64_t *__restrict__ 
 
 }  // namespace
 
-int launch_index_masks(const agn_log &log, uint64_t *out, hipStream_t st) {
+int launch_index_masks(const agn_log &log, uint64_t *out, uint64_t *mixed, hipStream_t st) {
     const uint64_t nb = (log.n_keys + 3) / 4;
+    if (mixed) *mixed = 0;
     if (nb == 0) return AGN_OK;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "index_masks: too many keys");
     if (log.n_dcs > 64) return fail(AGN_ENOTSUP, "index_masks: n_dcs %u > 64", log.n_dcs);
+    unsigned long long *cnt = nullptr;
+    const size_t cb = (size_t)IM_CNT * IM_STRIDE * sizeof(unsigned long long);
+    if (mixed) {
+        AGN_HIP(pool_malloc(&cnt, cb, st));
+        if (hipMemsetAsync(cnt, 0, cb, st) != hipSuccess) {
+            (void)hipFreeAsync(cnt, st);
+            return fail(AGN_EHIP, "index_masks: counter reset");
+        }
+    }
     hipLaunchKernelGGL(k_index_masks, dim3((unsigned)nb), dim3(256), 0, st, log.key_off,
-                       log.key_len, log.oc_mask, low_bits(log.n_dcs), log.n_keys, out);
-    AGN_HIP(hipGetLastError());
-    return AGN_OK;
+                       log.key_len, log.oc_mask, low_bits(log.n_dcs), log.n_keys, out, cnt);
+    int rc = hipGetLastError() == hipSuccess ? AGN_OK : fail(AGN_EHIP, "index_masks: launch");
+    if (cnt) {
+        // the count is read back here: the call blocks until the index is built
+        std::vector<unsigned long long> h((size_t)IM_CNT * IM_STRIDE);
+        if (rc == AGN_OK &&
+            (hipMemcpyAsync(h.data(), cnt, cb, hipMemcpyDeviceToHost, st) != hipSuccess ||
+             hipStreamSynchronize(st) != hipSuccess))
+            rc = fail(AGN_EHIP, "index_masks: mixed-key count");
+        if (rc == AGN_OK)
+            for (uint32_t i = 0; i < IM_CNT; ++i) *mixed += h[(size_t)i * IM_STRIDE];
+        (void)hipFreeAsync(cnt, st);
+    }
+    return rc;
 }
 
 int launch_index_ids(const agn_log &log, uint32_t *out, hipStream_t st) {
@@ -1315,7 +1354,7 @@ int tune_counter_dense(const agn_log &log, const agn_read &req, const agn_result
     if (log.crdt_type != AGN_COUNTER_PN || log.oc_mask || req.R_mask || req.sct_mask ||
         out.lastct_mask || req.n_req == 0)
         return AGN_ENOTSUP;
-    const char *impl = getenv("AGN_COUNTER_IMPL");
+    const char *impl = AGN_KNOB("AGN_COUNTER_IMPL");
     if (impl && impl[0] == 'g') return AGN_ENOTSUP;  // general kernel forced
     switch (log.n_dcs) {
         case 2: return tune_dense<2>(log, req, out, st, rounds, choice, ms);

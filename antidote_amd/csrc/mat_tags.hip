@@ -749,7 +749,7 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
     // one wave per key: the grid is the batch (the wave dispatcher then
     // overlaps keys; AGN_TAGS_GRID=<blocks> caps it for A/B); a list pass
     // grid-strides over a resident grid
-    const char *ge = getenv("AGN_TAGS_GRID");
+    const char *ge = AGN_KNOB("AGN_TAGS_GRID");
     const unsigned cap = in ? 8192u : ge ? (unsigned)atoi(ge) : 0x7fffffffu;
     const unsigned blocks = grid_for(req.n_req, FAST_WPB, cap);
     TagLists fast{in, in_n, ovf, ovf_n, mix, mix_n};
@@ -828,7 +828,7 @@ int launch_masked(const agn_log &log, const agn_read &req, const agn_result &out
 // Contiguous row loads for dense clocks with 4 DCs per lane (k_tags CT);
 // AGN_TAGS_CT=0 (A/B knob) keeps the LPO-lanes-by-4-DCs loads.
 inline bool tags_ct() {
-    const char *v = getenv("AGN_TAGS_CT");
+    const char *v = AGN_KNOB("AGN_TAGS_CT");
     return !(v && v[0] == '0');
 }
 
@@ -858,7 +858,7 @@ int launch_full(const agn_log &log, const agn_read &req, const agn_result &out, 
 // waves) lost 12 % / 9 % to the extra sub-iterations
 // (profiles/r01/ab_tags_dpl.log).  AGN_TAGS_DPL8=1 (A/B knob) keeps 8.
 inline bool tags_dpl8() {
-    const char *v = getenv("AGN_TAGS_DPL8");
+    const char *v = AGN_KNOB("AGN_TAGS_DPL8");
     return v && v[0] == '1';
 }
 
@@ -885,7 +885,7 @@ int dispatch(const agn_log &log, const agn_read &req, const agn_result &out, hip
 template <bool SET>
 int dispatch_masked(const agn_log &log, const agn_read &req, const agn_result &out,
                     hipStream_t st) {
-    const char *v = getenv("AGN_TAGS_MSK");
+    const char *v = AGN_KNOB("AGN_TAGS_MSK");
     if (v && v[0] == '0') return AGN_ENOTSUP;
     const bool warm = req.sct != nullptr;
 #define AGN_M(DPL, LPO, CTV, SD, SL)                                                         \
@@ -1007,13 +1007,13 @@ bool tags_serve_supported(const agn_log &log, bool sparse) {
     const uint32_t D = log.n_dcs;
     if (D == 16 || D == 32 || D == 64) {  // the CT shapes, dense or MSK
         if (!tags_ct()) return false;
-        const char *v = getenv("AGN_TAGS_MSK");
+        const char *v = AGN_KNOB("AGN_TAGS_MSK");
         return !sparse || !(v && v[0] == '0');
     }
     if (D == 0 || D > 8) return false;
     if (D % 2) return true;
     if (sparse) {
-        const char *v = getenv("AGN_TAGS_MSK");
+        const char *v = AGN_KNOB("AGN_TAGS_MSK");
         return !(v && v[0] == '0');
     }
     return D != 4 || tags_ct();

@@ -1046,6 +1046,20 @@ int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *k
 }
 void oplog_view(const agn_oplog *L, agn_log *v) { fill_view(L, v); }
 
+// How many of keys[0..n) hold entries with different DC sets (umask 0, not
+// empty): the read batcher's AGN_HINT_MIXED decision, from the host's copy
+// of agn_log.key_mask -- no device read.
+uint64_t oplog_mixed_keys(agn_oplog *L, uint64_t n, const uint64_t *keys) {
+    if (!L->sparse || L->umask.empty()) return 0;
+    std::lock_guard<std::mutex> g(L->wmu);
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t k = keys[i];
+        m += k < L->K && L->umask[k] == 0 && L->len[k] != 0;
+    }
+    return m;
+}
+
 int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uint64_t *d_keys,
                      const uint8_t *d_flags, const uint64_t *thr, const uint64_t *thr_mask,
                      hipStream_t st) {

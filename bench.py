@@ -89,9 +89,11 @@ def parse():
                          "memory, results back to pinned host memory; PCIe-inclusive)")
     ap.add_argument("--configs", default="auto",
                     help="BASELINE configs measured after the headline and reported in the same "
-                         "line's 'configs' object: comma list of 1, 2:full, 2:mixed, 3, 4, 5; "
-                         "'auto' = every config (N = 1) or the multi-GPU ones 4, 5 (N > 1) when "
-                         "the headline is the default cfg2 run; 'none' = headline only")
+                         "line's 'configs' object: comma list of 1, 2:full, 2:mixed, 3, 4, 5, "
+                         "N:warm (read/6 from the device snapshot cache: lookup -> warm "
+                         "materialize -> store), N:gc (the one-pass prune_ops GC); "
+                         "'auto' = " + AUTO_CONFIGS + " (N = 1) or the multi-GPU ones 4, 5 "
+                         "(N > 1) when the headline is the default cfg2 run; 'none' = headline only")
     ap.add_argument("--cpu-target-s", type=float, default=10.0,
                     help="seconds of CPU work per thread count in the CPU baseline")
     return ap.parse_args()
@@ -103,6 +105,11 @@ def fmt_keys(n):
             return f"{n / div:g}{suf}"
     return str(n)
 
+
+# the default run's sub-configs (N = 1): every BASELINE config, the masked
+# cfg2 batch the Erlang NIF's partitions run, the warm read/6 of the three
+# materialize configs and the one-pass GC of cfg3
+AUTO_CONFIGS = "1,2:full,3,4,5,2:warm,3:warm,4:warm,3:gc"
 
 KERNEL_SOURCES = {   # the sources the dominant kernel of each config is built from
     1: ("mat_counter_dense.hip", "counter_scan.hpp", "filter.hpp", "common.hpp"),
@@ -215,7 +222,7 @@ def presence_masks(mode, D, n_ops, n_keys, rng=None, torch=None):
     return ocm.reshape(n_ops, 1), np.full((n_keys, 1), full, np.uint64)
 
 
-def cpu_baseline(cfg, n_keys, threads, target_s=10.0, sparse=""):
+def cpu_baseline(cfg, n_keys, threads, target_s=10.0, sparse="", warm=0):
     """The C oracle (oracle/liboracle.so, a restatement of the Erlang path) on a
     bounded host-generated sample of the same workload.  Each chunk of the
     sample is materialized `reps` times so that the timed CPU work is about
@@ -235,7 +242,7 @@ def cpu_baseline(cfg, n_keys, threads, target_s=10.0, sparse=""):
         k = min(chunk, n_keys - done)
         g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=cfg["n_dcs"], n_keys=k,
                            ops_per_key=cfg["ops_per_key"], n_elems=cfg["n_elems"],
-                           seed=cfg["seed"], key_base=done, key_stride=1, warm=0)
+                           seed=cfg["seed"], key_base=done, key_stride=1, warm=warm)
         hl, hr = gen_host(g)
         cap = (np.arange(k + 1, dtype=np.uint64) * np.uint64(cfg["ops_per_key"])
                if cfg["crdt_type"] != 1 else None)
@@ -263,6 +270,89 @@ def cpu_baseline(cfg, n_keys, threads, target_s=10.0, sparse=""):
         free_gen_host(hl, hr)
         done += k
     return {nt: work[nt] / secs[nt] for nt in tcounts}, {nt: secs[nt] for nt in tcounts}, reps
+
+
+def cpu_baseline_gc(cfg, n_keys, target_s=2.0):
+    """The C oracle's prune_ops (oracle_prune_ops: check_filter over every
+    key, src/materializer_vnode.erl:566-604) on a bounded host-generated
+    sample of the same log, each key's read clock R as its threshold, as
+    gc_bench runs the device kernel; 1 thread.  Returns (entries/s, seconds,
+    passes)."""
+    from antidote_amd import _abi
+    from antidote_amd.engine import free_gen_host, gen_host
+    lib = _abi.bind(C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so")), _abi.ORACLE_PROTOTYPES)
+    D, N = cfg["n_dcs"], cfg["ops_per_key"]
+    g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=D, n_keys=n_keys, ops_per_key=N,
+                       n_elems=cfg["n_elems"], seed=cfg["seed"], key_base=0, key_stride=1, warm=0)
+    hl, hr = gen_host(g)
+    E = int(hl.n_entries)
+    tags = cfg["crdt_type"] != 1
+    n_rem = int(np.ctypeslib.as_array(C.cast(hl.rem_off, C.POINTER(C.c_uint32)),
+                                      (E + 1,))[-1]) if tags else 0
+    arrs = {"key_off": np.zeros(n_keys + 1, np.uint64), "oc": np.zeros(E * D, np.uint64),
+            "op_id": np.zeros(E, np.uint32), "txid": np.zeros(E, np.uint64)}
+    if tags:
+        arrs.update(tag=np.zeros(E, np.uint32), add_tok=np.zeros(E, np.uint64),
+                    rem_off=np.zeros(E + 1, np.uint32), rem_tok=np.zeros(max(n_rem, 1), np.uint64))
+    else:
+        arrs["eff"] = np.zeros(E, np.int64)
+    out = _abi.AgnLog()
+    out.crdt_type, out.n_dcs, out.n_keys = cfg["crdt_type"], D, n_keys
+    for name, arr in arrs.items():
+        setattr(out, name, arr.ctypes.data)
+    secs, passes = 0.0, 0
+    while secs < target_s or passes == 0:
+        t0 = time.perf_counter()
+        rc = lib.oracle_prune_ops(C.byref(hl), None, hr.R, None, C.byref(out), None)
+        secs += time.perf_counter() - t0
+        assert rc == 0
+        passes += 1
+    free_gen_host(hl, hr)
+    return E * passes / secs, secs, passes
+
+
+def warm_line(line, w, cfg, n_keys, world, a):
+    """A warm sub-line: read/6 served from the device snapshot cache.  value =
+    ops/s of agn_read_cached (lookup -> warm materialize -> store, one C-ABI
+    call per step); the roofline is the warm materialize kernel's."""
+    ops = n_keys * cfg["ops_per_key"] * world
+    ms = w["read_cached_ms"]
+    kms = w["materialize_ms"]
+    alg = w["materialize_algorithmic_bytes"]
+    ach = alg / (kms * 1e-3) / 1e9
+    line.update(value=ops / (ms * 1e-3), ms_per_step=ms, vc_compares_per_s=2 * ops / (ms * 1e-3))
+    line["config"]["workload"] += (", warm read/6 from the device snapshot cache (agn_read_cached: "
+                                   "lookup -> materialize from the cached base -> store)")
+    line["roofline"] = {
+        "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": ach / HBM_PEAK_GBS, "traffic": w.get("materialize_traffic"),
+        "traffic_source": w.get("materialize_traffic_source"),
+        "kernel": ("k_counter_quad2 (warm materialize, two requests per wave)"
+                   if cfg["crdt_type"] == 1 else "k_tags (warm, from the cached states)"),
+        "kernel_ms": kms, "algorithmic_bytes": alg, "kernel_src_sha16": kernel_src_sha16(a.config)}
+    line["warm"] = w
+    return line
+
+
+def gc_line(line, gc, cfg, n_keys, world, a):
+    """A GC sub-line: prune_ops over every key (the one-pass segmented kernel);
+    value = op-log entries filtered per second."""
+    seg = gc["segmented"]
+    E = gc["entries"] * world
+    ach = seg["algorithmic_bytes"] / (seg["ms"] * 1e-3) / 1e9
+    line.update(value=E / (seg["ms"] * 1e-3), ms_per_step=seg["ms"], vc_compares_per_s=None,
+                unit="ops/s", value_note="op-log entries GC-filtered per second")
+    line["config"]["workload"] += (", GC: prune_ops / check_filter of every key against its read "
+                                   "clock (snapshot_insert_gc, src/materializer_vnode.erl:513-604)")
+    line["roofline"] = {
+        "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": ach / HBM_PEAK_GBS, "traffic": seg.get("traffic"),
+        "traffic_source": seg.get("traffic_source"),
+        "kernel": "k_prune_inplace (segmented one pass)", "kernel_ms": seg["ms"],
+        "algorithmic_bytes": seg["algorithmic_bytes"], "kernel_src_sha16": kernel_src_sha16("gc"),
+        "frac_of_copy_probe": seg.get("frac_of_copy_probe")}
+    line["gc"] = gc
+    return line
 
 
 def pmc_traffic(config, n_units, name=None):
@@ -313,10 +403,13 @@ def main():
     # freed), its own warmup + barrier-bracketed timed launches, PMC traffic and
     # a short CPU baseline -- reported in the same JSON line, never in `value`
     configs = {}
-    for name, cid, sparse in sub_configs(a, world):
+    for name, cid, sparse, mode in sub_configs(a, world):
         sa = argparse.Namespace(**vars(a))
         sa.config, sa.sparse, sa.keys, sa.configs = cid, sparse, 0, "none"
         sa.gc = sa.warm = sa.ingest = sa.e2e = sa.gst = sa.post_gc = False
+        # a warm / gc sub-line reports that path as its own line (line_mode)
+        sa.line_mode = mode
+        sa.warm, sa.gc = mode == "warm", mode == "gc"
         sa.steps = max(a.steps, 200) if cid == 1 else a.steps
         sa.cpu_target_s = min(a.cpu_target_s, 2.0)
         sa.cpu_keys = 0 if a.cpu_keys == 0 else -2    # -2: the sub-config sample size
@@ -334,20 +427,23 @@ def main():
 
 
 def sub_configs(a, world):
-    """(name, config, sparse) of the configs measured after the headline."""
+    """(name, config, sparse, mode) of the configs measured after the headline:
+    "N:full|mixed|subsetK" = presence masks, "N:warm" / "N:gc" = that path."""
     spec = a.configs
     if spec == "auto":
         extra = a.gc or a.warm or a.ingest or a.e2e or a.post_gc or a.gst or a.keys
         if a.config != 2 or a.sparse or extra:
             return []
-        spec = "1,2:full,3,4,5" if world == 1 else "4,5"
+        spec = AUTO_CONFIGS if world == 1 else "4,5"
     if spec == "none":
         return []
     out = []
     for item in spec.split(","):
-        cid, _, sparse = item.strip().partition(":")
-        name = f"cfg{cid}" + (f"_masked_{sparse}" if sparse else "")
-        out.append((name, int(cid), sparse))
+        cid, _, opt = item.strip().partition(":")
+        if opt in ("warm", "gc"):
+            out.append((f"cfg{cid}_{opt}", int(cid), "", opt))
+        else:
+            out.append((f"cfg{cid}" + (f"_masked_{opt}" if opt else ""), int(cid), opt, ""))
     return out
 
 
@@ -500,10 +596,20 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
         # ~cpu_target_s seconds per thread count
         n_cpu = a.cpu_keys if a.cpu_keys >= 0 else \
             (64_000_000 if a.cpu_keys == -1 else 8_000_000) // cfg["ops_per_key"]
-        if world == 1 and n_cpu > 0:
+        mode = getattr(a, "line_mode", "")
+        if world == 1 and n_cpu > 0 and mode == "gc":
+            n_gc = min(n_keys, max(1, 2_000_000 // cfg["ops_per_key"]))
+            rate, secs, passes = cpu_baseline_gc(cfg, n_gc, target_s=a.cpu_target_s)
+            cpu = {"value": rate, "unit": "ops/s", "cores": 1, "kind": "port",
+                   "sample": f"{n_gc} keys x {cfg['ops_per_key']} ops of the same log "
+                             f"(host-generated), oracle_prune_ops (oracle/oracle.c -O3), "
+                             f"1 thread, {passes} pass(es) = {secs:.1f} s",
+                   "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
+        elif world == 1 and n_cpu > 0:
             thr = a.cpu_threads or min(16, os.cpu_count() or 1)
             rates, secs, reps = cpu_baseline(cfg, min(n_cpu, n_keys), thr,
-                                             target_s=a.cpu_target_s, sparse=a.sparse)
+                                             target_s=a.cpu_target_s, sparse=a.sparse,
+                                             warm=1 if mode == "warm" else 0)
             cpu = {"value": rates[1], "unit": "ops/s", "cores": 1, "kind": "port",
                    "sample": f"{min(n_cpu, n_keys)} keys x {cfg['ops_per_key']} ops of the same "
                              f"workload (host-generated, same SplitMix64 streams), "
@@ -511,6 +617,9 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
                              f"{secs[1]:.1f} s of CPU time",
                    "value_mt": rates.get(thr), "mt_threads": thr if thr > 1 else None,
                    "erlang": "not reproducible offline (no Erlang runtime; SURVEY.md §8(c))"}
+            if mode == "warm":
+                cpu["sample"] += (" -- the warm materialize/4 (SCT = a cached base covering a "
+                                  "random prefix); the cache lookup / store are not in it")
         traffic, traffic_src = pmc_traffic(a.config, n_keys,
                                            f"cfg{a.config}_sparse_{a.sparse}" if a.sparse else None)
         kname = KERNEL_NAME[a.config]
@@ -553,6 +662,13 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
         }
         if presence:
             line["presence"] = presence
+        mode = getattr(a, "line_mode", "")
+        if mode == "warm" and warm:
+            line = warm_line(line, warm, cfg, n_keys, world, a)
+            warm = None
+        elif mode == "gc" and gc:
+            line = gc_line(line, gc, cfg, n_keys, world, a)
+            gc = None
         if gst:
             line["gst"] = gst
         if post_gc:
@@ -790,12 +906,10 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     # kernel forced at this size (AGN_READ_CACHED_SPLIT=0)
     dkeys = eng.upload(np.arange(n_keys, dtype=np.uint64))
     t_rc = {}
+    from antidote_amd._lib import set_knob
     old_split = os.environ.get("AGN_READ_CACHED_SPLIT")
     for form, split in (("default", old_split), ("fused", "0")):
-        if split is None:
-            os.environ.pop("AGN_READ_CACHED_SPLIT", None)
-        else:
-            os.environ["AGN_READ_CACHED_SPLIT"] = split
+        set_knob("AGN_READ_CACHED_SPLIT", split)
         t_rc[form] = 0.0
         for i in range(steps + 1):
             ev[0].record()
@@ -805,10 +919,7 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
             torch.cuda.synchronize()
             if i:
                 t_rc[form] += ev[0].elapsed_time(ev[1])
-    if old_split is None:
-        os.environ.pop("AGN_READ_CACHED_SPLIT", None)
-    else:
-        os.environ["AGN_READ_CACHED_SPLIT"] = old_split
+    set_knob("AGN_READ_CACHED_SPLIT", old_split)
     t_fused = t_rc["fused"]
     hits_f = eng.download(bufs["status"], np.uint8, (n_keys,))
     for b in list(bufs.values()) + list(res.bufs.values()) + [dkeys]:
@@ -817,8 +928,13 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     # the warm materialize's bytes: the cold kernel's plus the SCT row, its
     # ignore flag and the base value per request
     wbytes = algorithmic_bytes(cfg, n_keys) + n_keys * (8 * D + 1 + 8)
+    # PMC bytes of the warm k_counter_quad2 launches (scripts/gpu.sh pmcwarm:
+    # the steps launches after the 2 priming ones, before the read_cached ones)
+    wtraffic, wsrc = pmc_traffic(cfg_id, n_keys, f"cfg{cfg_id}_warm") if cfg_id else \
+        (None, "null: config id not given")
     return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
             "materialize_algorithmic_bytes": wbytes,
+            "materialize_traffic": wtraffic, "materialize_traffic_source": wsrc,
             "materialize_frac": wbytes / (t_mat / steps * 1e-3) / 8e12,
             "store_ms": t_store / steps, "ops_per_s": ops / (ms * 1e-3),
             "read_cached_ms": t_rc["default"] / steps,

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define AGN_ABI_VERSION 5
+#define AGN_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 #define AGN_OK 0
@@ -193,6 +193,10 @@ typedef struct agn_ctx agn_ctx;
 int agn_abi_version(void);
 const char *agn_last_error(void);
 const char *agn_strerror(int code);
+/* The library reads its AGN_* environment knobs (A/B switches, test hooks)
+ * once and caches them; after changing one in a running process, call this
+ * so the next launch sees it.  Not part of the reference's API. */
+int agn_env_reload(void);
 
 /* Open a context on HIP device `device` (riak_core vnode start analogue:
  * src/materializer_vnode.erl:120-131). */
@@ -258,7 +262,12 @@ int agn_log_index_ids(agn_ctx *ctx, const agn_log *log, uint32_t *out, void *str
  * out[k] = the presence word all of key k's entries share (low D bits), or 0
  * when they differ or the key is empty.  The caller owns out ([n_keys] u64,
  * device) and sets log.key_mask = out; rebuild it when entries change.  A
- * log without oc_mask gets every key's full word (all D DCs present). */
+ * log without oc_mask gets every key's full word (all D DCs present).
+ * ABI v6: the call also counts the log's mixed keys (non-empty, entries with
+ * different DC sets) and blocks until the index is built; the context keeps
+ * the count with `out`, and agn_materialize over a log whose key_mask is
+ * `out` (same n_keys) routes a counter batch by it as if AGN_HINT_MIXED
+ * were passed when more than 1/16 of the log's keys are mixed. */
 int agn_log_index_masks(agn_ctx *ctx, const agn_log *log, uint64_t *out, void *stream);
 
 /* Upper bound of live pairs per request for set/register types:

@@ -12,30 +12,36 @@
  *   open(Device) -> {ok, Ctx} | {error, Reason}
  *
  *   Engine-owned partition (the materializer_vnode ETS ops cache in HBM,
- *   one per vnode; the resource's destructor frees it):
+ *   one per vnode, holding keys of every CRDT type like ops_cache-<P>; one
+ *   device op log per type, created with the type's first op; the resource's
+ *   destructor frees them).  Type = a type atom (antidote_crdt_counter_pn,
+ *   antidote_crdt_set_aw, antidote_crdt_register_mv) or its id 1..3:
  *   part_open(Ctx, Type, NDcs, NKeys, Cached) -> {ok, Part}
- *   part_update(Part, Key, OcPairs, TxId, Effect) -> {ok, OpId, GcDue}
+ *       Type: the type whose log is created up front
+ *   part_update(Part, Key, Type, OcPairs, TxId, Effect) -> {ok, OpId, GcDue}
  *       update/2 -> op_insert_gc/3 (agn_oplog_append): OcPairs =
  *       [{Dc, Time}] of the op's OpSSCommit, TxId a term or ignore, Effect the
  *       #clocksi_payload.op_param (counter_pn integer, set_aw
  *       [{Elem, AddToks, RemToks}], register_mv {V, Tok, Ovr} | {reset, Ovr})
- *   part_read(Part, Key, RPairs, TxId, Gc) -> {ok, Value, NewLastOp, LastOpCt,
- *       IsNewSS, Count} | {error, no_snapshot} | {error, Reason}
+ *   part_read(Part, Key, Type, RPairs, TxId, Gc) -> {ok, Value, NewLastOp,
+ *       LastOpCt, IsNewSS, Count} | {error, no_snapshot} | {error, Reason}
  *       cached partition: the whole read/6 (device snapshot cache + GC);
- *       Gc = true is op_insert_gc's GC read
- *   part_materialize(Part, Key, RPairs, SctPairs | ignore, TxId, Base) ->
+ *       Gc = true is op_insert_gc's GC read.  Raises corrupted_ops_cache when
+ *       the key holds ops of another type (src/clocksi_materializer.erl:191)
+ *   part_materialize(Part, Key, Type, RPairs, SctPairs | ignore, TxId, Base) ->
  *       same result: materialize/4 of the resident ops from a caller base
  *       (the reference's own ETS snapshot cache stays in Erlang)
- *   part_gc_due(Part, Key) -> boolean()
- *       op_insert_gc's GC trigger for the key's next op (:635), checked
- *       before the insert as the reference does
+ *   part_gc_due(Part, Key, Type) -> boolean()
+ *       op_insert_gc's GC trigger for the key's next op of Type (:635),
+ *       checked before the insert as the reference does
  *   part_gc(Part, Key, ThresholdPairs) -> ok
- *       snapshot_insert_gc's prune_ops + resize for one key (agn_oplog_prune)
- *   part_store(Part, Key, CommitTimePairs, NewLastOp, Count, Value, Gc) -> ok
+ *       snapshot_insert_gc's prune_ops + resize for one key (agn_oplog_prune),
+ *       over its ops of every type
+ *   part_store(Part, Key, Type, CommitTimePairs, NewLastOp, Count, Value, Gc) -> ok
  *       materialize_snapshot's store of a snapshot served from the log
  *       (agn_batcher_store; Gc = true: op_insert_gc's GC read)
  *   part_stats(Part) -> {Entries, Slots, Tokens}
- *   part_key_meta(Part, Key) -> {Length, ListLen, OpId}
+ *   part_key_meta(Part, Key, Type) -> {Length, ListLen, OpId}
  *   Keys, DC ids, TxIds, elements / values and tokens are interned exactly
  *   (agn_interner over enif_term_to_binary), never hashed.
  *   materialize(Ctx, Type, NDcs, Log, Read, CapOff) ->
@@ -85,26 +91,40 @@ static void ctx_dtor(ErlNifEnv *env, void *obj) {
 }
 
 /* ---- partition resource ------------------------------------------------ */
+/* One CRDT type's share of a partition: the device op log of the partition's
+ * ops of that type, its read batcher and part_gc's scratch.  The reference's
+ * ops_cache-<P> holds keys of any type; a key's ops normally share one type
+ * (its bucket's), and a read of another type raises corrupted_ops_cache. */
 typedef struct {
-    ctx_res *ctx;           /* kept alive while the partition lives */
     agn_oplog *log;
     agn_batcher *bt;
-    agn_interner *keys, *dcs, *txids, *tags, *toks;
-    uint32_t type, D, W;
-    uint64_t K;
-    int cached;
     /* part_gc scratch (device): prune flags [K], threshold row [K][D] (+ mask) */
-    pthread_mutex_t gc_mu;
     uint8_t *d_prune;
     uint64_t *d_thr, *d_thrm;
+    int ready;              /* published (release) once every field is set */
+} part_sub;
+
+#define NTYPES 4 /* indexed by AGN_COUNTER_PN .. AGN_REGISTER_MV */
+
+typedef struct {
+    ctx_res *ctx;           /* kept alive while the partition lives */
+    part_sub sub[NTYPES];
+    pthread_mutex_t sub_mu; /* creation of a type's log */
+    agn_interner *keys, *dcs, *txids, *tags, *toks;
+    uint32_t type, D, W;    /* type: the one part_open created */
+    uint64_t K;
+    int cached;
+    pthread_mutex_t gc_mu;
     /* the original effect term (external format) of every op whose effect the
-     * engine could not encode (an invalid entry), by (key, op id): a read that
-     * includes it returns {error, {unexpected_operation, Effect, Type}} with
-     * that term, as materializer:update_snapshot/3 (src/materializer.erl:51-58) */
+     * engine could not encode (an invalid entry), by (key, type, op id): a read
+     * that includes it returns {error, {unexpected_operation, Effect, Type}}
+     * with that term, as materializer:update_snapshot/3 (src/materializer.erl:
+     * 51-58).  Recorded before the append makes the op visible; a key's
+     * records are dropped once a GC leaves it no ops. */
     pthread_mutex_t inv_mu;
     struct inv_op {
         uint64_t key;
-        uint32_t id;
+        uint32_t type, id;
         ErlNifBinary eff;
     } *inv;
     size_t n_inv, cap_inv;
@@ -120,7 +140,8 @@ static const char *type_name(uint32_t type) {
 }
 
 /* keep the effect term of an invalid op (one writer: the vnode) */
-static int inv_put(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t id, ERL_NIF_TERM eff) {
+static int inv_put(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t type, uint32_t id,
+                   ERL_NIF_TERM eff) {
     ErlNifBinary b;
     if (!enif_term_to_binary(env, eff, &b)) return AGN_ENOMEM;
     pthread_mutex_lock(&p->inv_mu);
@@ -136,6 +157,7 @@ static int inv_put(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t id, ERL_N
         p->cap_inv = c;
     }
     p->inv[p->n_inv].key = key;
+    p->inv[p->n_inv].type = type;
     p->inv[p->n_inv].id = id;
     p->inv[p->n_inv].eff = b;
     p->n_inv++;
@@ -143,12 +165,13 @@ static int inv_put(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t id, ERL_N
     return AGN_OK;
 }
 
-/* the effect term of op `id` of `key`, or 'undefined' */
-static ERL_NIF_TERM inv_get(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t id) {
+/* the effect term of op `id` of `key` (type `type`), or 'undefined' */
+static ERL_NIF_TERM inv_get(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t type,
+                            uint32_t id) {
     ERL_NIF_TERM out = enif_make_atom(env, "undefined");
     pthread_mutex_lock(&p->inv_mu);
     for (size_t i = p->n_inv; i-- > 0;)
-        if (p->inv[i].key == key && p->inv[i].id == id) {
+        if (p->inv[i].key == key && p->inv[i].type == type && p->inv[i].id == id) {
             if (!enif_binary_to_term(env, p->inv[i].eff.data, p->inv[i].eff.size, &out, 0))
                 out = enif_make_atom(env, "undefined");
             break;
@@ -157,15 +180,34 @@ static ERL_NIF_TERM inv_get(ErlNifEnv *env, part_res *p, uint64_t key, uint32_t 
     return out;
 }
 
+/* drop the records of `key`'s ops of `type` with id >= `from` (from = 0: all
+ * of them -- a GC left the key no ops of the type) */
+static void inv_drop(part_res *p, uint64_t key, uint32_t type, uint32_t from) {
+    pthread_mutex_lock(&p->inv_mu);
+    size_t j = 0;
+    for (size_t i = 0; i < p->n_inv; ++i) {
+        if (p->inv[i].key == key && p->inv[i].type == type && p->inv[i].id >= from) {
+            enif_release_binary(&p->inv[i].eff);
+            continue;
+        }
+        p->inv[j++] = p->inv[i];
+    }
+    p->n_inv = j;
+    pthread_mutex_unlock(&p->inv_mu);
+}
+
 static void part_dtor(ErlNifEnv *env, void *obj) {
     (void)env;
     part_res *p = (part_res *)obj;
-    if (p->bt) agn_batcher_destroy(p->bt);
-    if (p->log) agn_oplog_destroy(p->log);
-    if (p->ctx) {
-        agn_dev_free(p->ctx->ctx, p->d_prune);
-        agn_dev_free(p->ctx->ctx, p->d_thr);
-        agn_dev_free(p->ctx->ctx, p->d_thrm);
+    for (int t = 0; t < NTYPES; ++t) {
+        part_sub *s = &p->sub[t];
+        if (s->bt) agn_batcher_destroy(s->bt);
+        if (s->log) agn_oplog_destroy(s->log);
+        if (p->ctx) {
+            agn_dev_free(p->ctx->ctx, s->d_prune);
+            agn_dev_free(p->ctx->ctx, s->d_thr);
+            agn_dev_free(p->ctx->ctx, s->d_thrm);
+        }
     }
     agn_interner_destroy(p->keys);
     agn_interner_destroy(p->dcs);
@@ -173,6 +215,7 @@ static void part_dtor(ErlNifEnv *env, void *obj) {
     agn_interner_destroy(p->tags);
     agn_interner_destroy(p->toks);
     pthread_mutex_destroy(&p->gc_mu);
+    pthread_mutex_destroy(&p->sub_mu);
     for (size_t i = 0; i < p->n_inv; ++i) enif_release_binary(&p->inv[i].eff);
     enif_free(p->inv);
     pthread_mutex_destroy(&p->inv_mu);
@@ -376,7 +419,70 @@ static ERL_NIF_TERM nif_select_base(ErlNifEnv *env, int argc, const ERL_NIF_TERM
 
 /* ---- partition functions -------------------------------------------------- */
 static int get_part(ErlNifEnv *env, ERL_NIF_TERM t, part_res **out) {
-    return enif_get_resource(env, t, PART_RES, (void **)out) && (*out)->log != NULL;
+    return enif_get_resource(env, t, PART_RES, (void **)out) && (*out)->keys != NULL;
+}
+
+/* a CRDT type: its atom or its id */
+static int type_of(ErlNifEnv *env, ERL_NIF_TERM t, uint32_t *type) {
+    unsigned v;
+    if (enif_get_uint(env, t, &v)) {
+        *type = v;
+        return v >= AGN_COUNTER_PN && v <= AGN_REGISTER_MV;
+    }
+    for (uint32_t x = AGN_COUNTER_PN; x <= AGN_REGISTER_MV; ++x)
+        if (enif_is_identical(t, atom(env, type_name(x)))) {
+            *type = x;
+            return 1;
+        }
+    return 0;
+}
+
+/* the partition's log of `type`, NULL while it holds no op of that type */
+static part_sub *sub_get(part_res *p, uint32_t type) {
+    part_sub *s = &p->sub[type];
+    return __atomic_load_n(&s->ready, __ATOMIC_ACQUIRE) ? s : NULL;
+}
+
+/* the log of `type`, created with the type's first op (op log, read batcher,
+ * part_gc scratch); the writer creates, readers see it once published */
+static int sub_make(part_res *p, uint32_t type, part_sub **out) {
+    part_sub *s = sub_get(p, type);
+    if (s) {
+        *out = s;
+        return AGN_OK;
+    }
+    pthread_mutex_lock(&p->sub_mu);
+    s = &p->sub[type];
+    int rc = AGN_OK;
+    if (!s->ready) {
+        agn_ctx *c = p->ctx->ctx;
+        rc = agn_oplog_create(c, type, p->D, p->K, 1, 0, &s->log);
+        if (!rc) rc = p->cached ? agn_batcher_create_cached(s->log, 0, 1024, 50, &s->bt)
+                                : agn_batcher_create(s->log, 1024, 50, &s->bt);
+        if (!rc) rc = agn_dev_alloc(c, p->K, (void **)&s->d_prune);
+        if (!rc) rc = agn_dev_alloc(c, p->K * p->D * 8, (void **)&s->d_thr);
+        if (!rc) rc = agn_dev_alloc(c, p->K * p->W * 8, (void **)&s->d_thrm);
+        if (!rc) __atomic_store_n(&s->ready, 1, __ATOMIC_RELEASE);
+        /* on failure the fields stay for the destructor; a later op retries */
+    }
+    pthread_mutex_unlock(&p->sub_mu);
+    *out = rc ? NULL : s;
+    return rc;
+}
+
+/* does `key` hold ops of a type other than `type` (materialize_intern's
+ * type check over the key's ops, src/clocksi_materializer.erl:190-191)? */
+static int other_type_ops(part_res *p, uint64_t key, uint32_t type, int *out) {
+    *out = 0;
+    for (uint32_t t = AGN_COUNTER_PN; t <= AGN_REGISTER_MV && !*out; ++t) {
+        part_sub *s = t == type ? NULL : sub_get(p, t);
+        uint32_t len = 0;
+        if (!s) continue;
+        int rc = agn_oplog_key_meta(s->log, 1, &key, &len, NULL, NULL);
+        if (rc) return rc;
+        *out = len != 0;
+    }
+    return AGN_OK;
 }
 
 /* exact id of a term: its external format through an interner */
@@ -448,35 +554,33 @@ static int txid_of(ErlNifEnv *env, part_res *p, ERL_NIF_TERM t, uint64_t *id) {
 
 static ERL_NIF_TERM nif_part_open(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     ctx_res *c;
-    unsigned type, D;
+    uint32_t type;
+    unsigned D;
     ErlNifUInt64 K;
     if (argc != 5 || !enif_get_resource(env, argv[0], CTX_RES, (void **)&c) || !c->ctx ||
-        !enif_get_uint(env, argv[1], &type) || !enif_get_uint(env, argv[2], &D) || D == 0 ||
+        !type_of(env, argv[1], &type) || !enif_get_uint(env, argv[2], &D) || D == 0 ||
         D > 256 || !enif_get_uint64(env, argv[3], &K) || K == 0)
         return enif_make_badarg(env);
     const int cached = enif_is_identical(argv[4], atom(env, "true"));
     part_res *p = enif_alloc_resource(PART_RES, sizeof *p);
     memset(p, 0, sizeof *p);
     pthread_mutex_init(&p->gc_mu, NULL);
+    pthread_mutex_init(&p->sub_mu, NULL);
     pthread_mutex_init(&p->inv_mu, NULL);
     p->type = type;
     p->D = D;
     p->W = (D + 63) / 64;
     p->K = K;
     p->cached = cached;
-    int rc = agn_oplog_create(c->ctx, type, D, K, 1, 0, &p->log);
-    if (!rc) rc = cached ? agn_batcher_create_cached(p->log, 0, 1024, 50, &p->bt)
-                         : agn_batcher_create(p->log, 1024, 50, &p->bt);
-    if (!rc) rc = agn_interner_create(1, K, &p->keys);
+    p->ctx = c;
+    enif_keep_resource(c);
+    part_sub *s;
+    int rc = agn_interner_create(1, K, &p->keys);
     if (!rc) rc = agn_interner_create(1, D, &p->dcs);
     if (!rc) rc = agn_interner_create(1, UINT64_MAX / 2, &p->txids);
     if (!rc) rc = agn_interner_create(0, 0xFFFFFFFEull, &p->tags);
     if (!rc) rc = agn_interner_create(1, UINT64_MAX / 2, &p->toks);
-    if (!rc) rc = agn_dev_alloc(c->ctx, K, (void **)&p->d_prune);
-    if (!rc) rc = agn_dev_alloc(c->ctx, K * D * 8, (void **)&p->d_thr);
-    if (!rc) rc = agn_dev_alloc(c->ctx, K * p->W * 8, (void **)&p->d_thrm);
-    p->ctx = c;
-    enif_keep_resource(c);
+    if (!rc) rc = sub_make(p, type, &s);
     if (rc) {
         ERL_NIF_TERM e = error_tuple(env, rc);
         enif_release_resource(p);  /* the destructor frees what was created */
@@ -523,12 +627,13 @@ static int push_entry(ErlNifEnv *env, part_res *p, entries *E, uint64_t tag, uin
     return 0;
 }
 
-static int effect_entries(ErlNifEnv *env, part_res *p, ERL_NIF_TERM eff, entries *E) {
+static int effect_entries(ErlNifEnv *env, part_res *p, uint32_t type, ERL_NIF_TERM eff,
+                          entries *E) {
     E->n = E->nrem = 0;
     E->rem_off[0] = 0;
     int ar;
     const ERL_NIF_TERM *tp;
-    if (p->type == AGN_REGISTER_MV) {
+    if (type == AGN_REGISTER_MV) {
         uint64_t tag = 0, tok = 0;
         if (!enif_get_tuple(env, eff, &ar, &tp)) return -1;
         if (ar == 2 && enif_is_identical(tp[0], atom(env, "reset")))
@@ -565,12 +670,17 @@ static int effect_entries(ErlNifEnv *env, part_res *p, ERL_NIF_TERM eff, entries
 
 static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
-    if (argc != 5 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    uint32_t type;
+    if (argc != 6 || !get_part(env, argv[0], &p) || !type_of(env, argv[2], &type))
+        return enif_make_badarg(env);
     uint64_t k, tx, row[256], mask[4];
     int rc = key_index(env, p, argv[1], &k);
-    if (!rc) rc = clock_row(env, p, argv[2], row, mask);
-    if (!rc) rc = txid_of(env, p, argv[3], &tx);
+    if (!rc) rc = clock_row(env, p, argv[3], row, mask);
+    if (!rc) rc = txid_of(env, p, argv[4], &tx);
     if (rc == AGN_EINVAL) return enif_make_badarg(env);
+    if (rc) return error_tuple(env, rc);
+    part_sub *sb;
+    rc = sub_make(p, type, &sb);
     if (rc) return error_tuple(env, rc);
     const uint32_t D = p->D, W = p->W;
     uint64_t keys[MAXE], txids[MAXE];
@@ -586,13 +696,13 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     }
     uint32_t n = 1;
     int invalid = 0;
-    if (p->type == AGN_COUNTER_PN) {
+    if (type == AGN_COUNTER_PN) {
         ErlNifSInt64 v;
-        invalid = !enif_get_int64(env, argv[4], &v) || v == AGN_EFFECT_INVALID;
+        invalid = !enif_get_int64(env, argv[5], &v) || v == AGN_EFFECT_INVALID;
         eff[0] = invalid ? AGN_EFFECT_INVALID : (int64_t)v;
         E->n = 0;
     } else {
-        const int ne = effect_entries(env, p, argv[4], E);
+        const int ne = effect_entries(env, p, type, argv[5], E);
         if (ne < 0) {  /* not representable: one invalid entry (update/2 raises at read) */
             E->n = 1;
             E->nrem = 0;
@@ -618,16 +728,24 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
         memcpy(oc + (size_t)i * D, row, D * 8);
         memcpy(ocm + (size_t)i * W, mask, W * 8);
     }
-    rc = agn_oplog_append(p->log, n, keys, same, oc, ocm, txids,
-                          p->type == AGN_COUNTER_PN ? eff : NULL,
-                          p->type == AGN_COUNTER_PN ? NULL : E->tag,
-                          p->type == AGN_COUNTER_PN ? NULL : E->add,
-                          p->type == AGN_COUNTER_PN ? NULL : E->rem_off,
-                          p->type == AGN_COUNTER_PN ? NULL : E->rem, ids, due);
+    /* an invalid op's effect term is recorded under the id the append gives
+     * it (the key's op counter + 1; one writer) before a read can see it */
+    uint32_t next = 0;
+    if (invalid) {
+        rc = agn_oplog_key_meta(sb->log, 1, &k, NULL, NULL, &next);
+        if (!rc) rc = inv_put(env, p, k, type, next + 1, argv[5]);
+    }
+    if (!rc)
+        rc = agn_oplog_append(sb->log, n, keys, same, oc, ocm, txids,
+                              type == AGN_COUNTER_PN ? eff : NULL,
+                              type == AGN_COUNTER_PN ? NULL : E->tag,
+                              type == AGN_COUNTER_PN ? NULL : E->add,
+                              type == AGN_COUNTER_PN ? NULL : E->rem_off,
+                              type == AGN_COUNTER_PN ? NULL : E->rem, ids, due);
+    if (rc && invalid) inv_drop(p, k, type, next + 1);
     enif_free(E);
     enif_free(oc);
     enif_free(ocm);
-    if (!rc && invalid) rc = inv_put(env, p, k, ids[0], argv[4]);
     if (rc) return error_tuple(env, rc);
     return enif_make_tuple3(env, atom(env, "ok"), enif_make_uint(env, ids[0]),
                             atom(env, due[0] ? "true" : "false"));
@@ -635,10 +753,10 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
 
 /* the state pairs of a set/register result -> orddict [{Elem, [Tok]}] /
  * sorted [{Value, Token}] (decoded through the interners) */
-static ERL_NIF_TERM state_term(ErlNifEnv *env, part_res *p, uint32_t n, const uint32_t *tag,
-                               const uint64_t *tok) {
+static ERL_NIF_TERM state_term(ErlNifEnv *env, part_res *p, uint32_t type, uint32_t n,
+                               const uint32_t *tag, const uint64_t *tok) {
     ERL_NIF_TERM l = enif_make_list(env, 0);
-    if (p->type == AGN_REGISTER_MV) {
+    if (type == AGN_REGISTER_MV) {
         for (uint32_t i = n; i-- > 0;)
             l = enif_make_list_cell(env, enif_make_tuple2(env, id_term(env, p->tags, tag[i]),
                                                          id_term(env, p->toks, tok[i])), l);
@@ -657,7 +775,7 @@ static ERL_NIF_TERM state_term(ErlNifEnv *env, part_res *p, uint32_t n, const ui
     return l;
 }
 
-static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, uint64_t key,
+static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, uint32_t type, uint64_t key,
                                 const agn_key_result *o, const uint64_t *ct, const uint64_t *ctm) {
     /* erlang:error(corrupted_ops_cache) (src/clocksi_materializer.erl:190-191) */
     if (o->flags & AGN_F_ERR_CORRUPTED)
@@ -667,10 +785,11 @@ static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, uint64_t key,
     if (o->flags & AGN_F_ERR_UNEXPECTED)
         return enif_make_tuple2(env, atom(env, "error"),
                                 enif_make_tuple3(env, atom(env, "unexpected_operation"),
-                                                 inv_get(env, p, key, o->err_pos),
-                                                 atom(env, type_name(p->type))));
-    ERL_NIF_TERM v = p->type == AGN_COUNTER_PN ? enif_make_int64(env, o->value)
-                                               : state_term(env, p, o->out_n, o->out_tag, o->out_tok);
+                                                 inv_get(env, p, key, type, o->err_pos),
+                                                 atom(env, type_name(type))));
+    ERL_NIF_TERM v = type == AGN_COUNTER_PN
+                         ? enif_make_int64(env, o->value)
+                         : state_term(env, p, type, o->out_n, o->out_tag, o->out_tok);
     ERL_NIF_TERM lct = (o->flags & AGN_F_CT_IGNORE) ? atom(env, "ignore") : clock_pairs(env, p, ct, ctm);
     ERL_NIF_TERM res[6] = {atom(env, "ok"), v, enif_make_int64(env, o->hole), lct,
                            atom(env, (o->flags & AGN_F_NEWSS) ? "true" : "false"),
@@ -681,8 +800,8 @@ static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, uint64_t key,
 /* a set_aw orddict [{Elem, [Tok]}] / register_mv [{V, Tok}] -> interned
  * (tag, token) pairs in the result layout (enif_alloc'ed; NULL when empty);
  * AGN_EINVAL for a malformed term */
-static int state_pairs(ErlNifEnv *env, part_res *p, ERL_NIF_TERM st, uint32_t *n_out,
-                       uint32_t **tags_out, uint64_t **toks_out) {
+static int state_pairs(ErlNifEnv *env, part_res *p, uint32_t type, ERL_NIF_TERM st,
+                       uint32_t *n_out, uint32_t **tags_out, uint64_t **toks_out) {
     unsigned nl = 0;
     *n_out = 0;
     *tags_out = NULL;
@@ -695,7 +814,7 @@ static int state_pairs(ErlNifEnv *env, part_res *p, ERL_NIF_TERM st, uint32_t *n
         const ERL_NIF_TERM *tp;
         unsigned m = 1;
         if (!enif_get_tuple(env, h, &ar, &tp) || ar != 2) return AGN_EINVAL;
-        if (p->type == AGN_SET_AW && !enif_get_list_length(env, tp[1], &m)) return AGN_EINVAL;
+        if (type == AGN_SET_AW && !enif_get_list_length(env, tp[1], &m)) return AGN_EINVAL;
         cap += m;
     }
     uint32_t *tg = enif_alloc(4 * (cap + 1));
@@ -712,7 +831,7 @@ static int state_pairs(ErlNifEnv *env, part_res *p, ERL_NIF_TERM st, uint32_t *n
         uint64_t id_tag, id_tok;
         enif_get_tuple(env, h, &ar, &tp);
         int rc = term_id(env, p->tags, tp[0], &id_tag);
-        if (p->type == AGN_REGISTER_MV) {
+        if (type == AGN_REGISTER_MV) {
             if (!rc) rc = term_id(env, p->toks, tp[1], &id_tok);
             if (!rc) {
                 tg[n] = (uint32_t)id_tag;
@@ -740,10 +859,10 @@ static int state_pairs(ErlNifEnv *env, part_res *p, ERL_NIF_TERM st, uint32_t *n
     return AGN_OK;
 }
 
-/* one read through the partition's batcher */
+/* one read of `type` through the partition's batcher of that type */
 static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM key,
-                                     ERL_NIF_TERM rpairs, ERL_NIF_TERM sct, ERL_NIF_TERM txid,
-                                     ERL_NIF_TERM base, int gc) {
+                                     uint32_t type, ERL_NIF_TERM rpairs, ERL_NIF_TERM sct,
+                                     ERL_NIF_TERM txid, ERL_NIF_TERM base, int gc) {
     uint64_t k, tx, R[256], Rm[4], S[256], Sm[4], ct[256], ctm[4];
     int rc = key_index(env, p, key, &k);
     if (!rc) rc = clock_row(env, p, rpairs, R, Rm);
@@ -752,6 +871,29 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     if (!rc && has_sct) rc = clock_row(env, p, sct, S, Sm);
     if (rc == AGN_EINVAL) return enif_make_badarg(env);
     if (rc) return error_tuple(env, rc);
+    /* erlang:error(corrupted_ops_cache) (src/clocksi_materializer.erl:190-191):
+     * the key holds ops of another type than the read's */
+    int other = 0;
+    rc = other_type_ops(p, k, type, &other);
+    if (rc) return error_tuple(env, rc);
+    if (other) return enif_raise_exception(env, atom(env, "corrupted_ops_cache"));
+    part_sub *sb = sub_get(p, type);
+    if (!sb) {
+        /* no op of this type was ever written: materialize/4 of an empty ops
+         * list -- the base value, NewLastOp = get_first_id([]) = 0, LastOpCt
+         * = SCT (ignore for read/6), nothing new, nothing cached */
+        ERL_NIF_TERM v;
+        ErlNifSInt64 b = 0;
+        if (type == AGN_COUNTER_PN)
+            v = (!enif_is_identical(base, atom(env, "undefined")) && enif_get_int64(env, base, &b))
+                    ? enif_make_int64(env, b) : enif_make_int64(env, 0);
+        else
+            v = (!p->cached && enif_is_list(env, base)) ? base : enif_make_list(env, 0);
+        ERL_NIF_TERM res[6] = {atom(env, "ok"), v, enif_make_int64(env, 0),
+                               has_sct ? sct : atom(env, "ignore"), atom(env, "false"),
+                               enif_make_uint(env, 0)};
+        return enif_make_tuple_from_array(env, res, 6);
+    }
     agn_key_read rd;
     agn_key_result o;
     memset(&rd, 0, sizeof rd);
@@ -768,7 +910,7 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     uint32_t len = 0, nb = 0;
     uint32_t *btag = NULL, *otag = NULL;
     uint64_t *btok = NULL, *otok = NULL;
-    if (p->type == AGN_COUNTER_PN) {
+    if (type == AGN_COUNTER_PN) {
         ErlNifSInt64 v = 0;
         if (!enif_is_identical(base, atom(env, "undefined")) && !enif_get_int64(env, base, &v))
             return enif_make_badarg(env);
@@ -776,19 +918,19 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     } else if (!p->cached) {
         /* base state pairs: set_aw orddict [{Elem, [Tok]}], register_mv [{V, Tok}]
          * (a cached partition's base state is the device snapshot cache's) */
-        const int src = state_pairs(env, p, base, &nb, &btag, &btok);
+        const int src = state_pairs(env, p, type, base, &nb, &btag, &btok);
         if (src == AGN_EINVAL) return enif_make_badarg(env);
         if (src) goto oom;
         rd.n_base = nb;
         rd.base_tag = btag;
         rd.base_tok = btok;
     }
-    if (p->type != AGN_COUNTER_PN) {
+    if (type != AGN_COUNTER_PN) {
         /* room for the state: the key's entries + the base (a cached base:
          * the largest state the partition's cache holds for the key) */
         uint32_t bound = 0;
-        if (agn_oplog_key_meta(p->log, 1, &k, &len, NULL, NULL)) goto oom;
-        if (p->cached && agn_batcher_state_bound(p->bt, k, &bound)) goto oom;
+        if (agn_oplog_key_meta(sb->log, 1, &k, &len, NULL, NULL)) goto oom;
+        if (p->cached && agn_batcher_state_bound(sb->bt, k, &bound)) goto oom;
         o.out_cap = len + nb + bound + (p->cached ? 16u : 0u);
         otag = enif_alloc(4 * (o.out_cap + 1));
         otok = enif_alloc(8 * (o.out_cap + 1));
@@ -796,8 +938,8 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
         o.out_tag = otag;
         o.out_tok = otok;
     }
-    rc = agn_batcher_read(p->bt, &rd, &o);
-    if (rc == AGN_ECAPACITY && p->type != AGN_COUNTER_PN && o.out_n > o.out_cap) {
+    rc = agn_batcher_read(sb->bt, &rd, &o);
+    if (rc == AGN_ECAPACITY && type != AGN_COUNTER_PN && o.out_n > o.out_cap) {
         /* the state outgrew the buffer (updates landed after key_meta): read
          * again with room for it (a read/6 is repeatable: the second one is
          * served from what the first stored).  The first pass already ran a GC
@@ -812,13 +954,15 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
         if (!otag || !otok) goto oom;
         o.out_tag = otag;
         o.out_tok = otok;
-        rc = agn_batcher_read(p->bt, &rd, &o);
+        rc = agn_batcher_read(sb->bt, &rd, &o);
     }
     ERL_NIF_TERM r;
     if (rc) r = error_tuple(env, rc);
     else if (p->cached && o.status == AGN_SS_LOG)
         r = enif_make_tuple2(env, atom(env, "error"), atom(env, "no_snapshot"));
-    else r = read_result(env, p, k, &o, ct, ctm);
+    else r = read_result(env, p, type, k, &o, ct, ctm);
+    if (!rc && gc && agn_oplog_key_meta(sb->log, 1, &k, &len, NULL, NULL) == AGN_OK && len == 0)
+        inv_drop(p, k, type, 0);  /* the GC read pruned every op of the key */
     enif_free(btag);
     enif_free(btok);
     enif_free(otag);
@@ -834,55 +978,66 @@ oom:
 
 static ERL_NIF_TERM nif_part_read(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
-    if (argc != 5 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    uint32_t type;
+    if (argc != 6 || !get_part(env, argv[0], &p) || !type_of(env, argv[2], &type))
+        return enif_make_badarg(env);
     /* read/6 through the device snapshot cache: a partition opened with
      * Cached = false keeps the reference's ETS cache (use part_materialize) */
     if (!p->cached)
         return enif_make_tuple2(env, atom(env, "error"), atom(env, "not_cached"));
-    return part_read_common(env, p, argv[1], argv[2], atom(env, "ignore"), argv[3],
-                            atom(env, "undefined"), enif_is_identical(argv[4], atom(env, "true")));
+    return part_read_common(env, p, argv[1], type, argv[3], atom(env, "ignore"), argv[4],
+                            atom(env, "undefined"), enif_is_identical(argv[5], atom(env, "true")));
 }
 
 static ERL_NIF_TERM nif_part_materialize(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
-    if (argc != 6 || !get_part(env, argv[0], &p) || p->cached) return enif_make_badarg(env);
-    return part_read_common(env, p, argv[1], argv[2], argv[3], argv[4], argv[5], 0);
+    uint32_t type;
+    if (argc != 7 || !get_part(env, argv[0], &p) || p->cached || !type_of(env, argv[2], &type))
+        return enif_make_badarg(env);
+    return part_read_common(env, p, argv[1], type, argv[3], argv[4], argv[5], argv[6], 0);
 }
 
-/* part_store(Part, Key, CommitTimePairs, NewLastOp, Count, Value, Gc) -> ok:
- * materialize_snapshot's store (:466-509) of a snapshot the vnode
+/* part_store(Part, Key, Type, CommitTimePairs, NewLastOp, Count, Value, Gc) ->
+ * ok: materialize_snapshot's store (:466-509) of a snapshot the vnode
  * materialized from the log (get_from_snapshot_log, :416-419), on the
  * partition's device cache (agn_batcher_store); Gc = true for op_insert_gc's
  * GC read (a log response is never the newest, so only it stores) */
 static ERL_NIF_TERM nif_part_store(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
-    if (argc != 7 || !get_part(env, argv[0], &p) || !p->cached) return enif_make_badarg(env);
+    uint32_t type;
+    if (argc != 8 || !get_part(env, argv[0], &p) || !p->cached || !type_of(env, argv[2], &type))
+        return enif_make_badarg(env);
     uint64_t k, row[256], mask[4];
     ErlNifSInt64 last_op = 0, value = 0;
     unsigned count = 0;
     int rc = key_index(env, p, argv[1], &k);
-    if (!rc) rc = clock_row(env, p, argv[2], row, mask);
-    if (rc == AGN_EINVAL || !enif_get_int64(env, argv[3], &last_op) ||
-        !enif_get_uint(env, argv[4], &count))
+    if (!rc) rc = clock_row(env, p, argv[3], row, mask);
+    if (rc == AGN_EINVAL || !enif_get_int64(env, argv[4], &last_op) ||
+        !enif_get_uint(env, argv[5], &count))
         return enif_make_badarg(env);
     if (rc) return error_tuple(env, rc);
     uint32_t n = 0, *tags = NULL;
     uint64_t *toks = NULL;
-    if (p->type == AGN_COUNTER_PN) {
-        if (!enif_get_int64(env, argv[5], &value)) return enif_make_badarg(env);
+    if (type == AGN_COUNTER_PN) {
+        if (!enif_get_int64(env, argv[6], &value)) return enif_make_badarg(env);
     } else {
-        rc = state_pairs(env, p, argv[5], &n, &tags, &toks);
+        rc = state_pairs(env, p, type, argv[6], &n, &tags, &toks);
         if (rc == AGN_EINVAL) return enif_make_badarg(env);
         if (rc) return error_tuple(env, rc);
     }
-    const int gc = enif_is_identical(argv[6], atom(env, "true"));
-    rc = agn_batcher_store(p->bt, k, row, mask, last_op, count, value, n, tags, toks,
-                           gc ? AGN_READ_GC : 0u);
+    const int gc = enif_is_identical(argv[7], atom(env, "true"));
+    part_sub *sb;
+    rc = sub_make(p, type, &sb);
+    if (!rc)
+        rc = agn_batcher_store(sb->bt, k, row, mask, last_op, count, value, n, tags, toks,
+                               gc ? AGN_READ_GC : 0u);
     enif_free(tags);
     enif_free(toks);
     return rc ? error_tuple(env, rc) : atom(env, "ok");
 }
 
+/* part_gc(Part, Key, ThresholdPairs): snapshot_insert_gc's prune_ops over the
+ * key's ops of every type (prune_ops filters the whole ETS tuple, :566-604) */
 static ERL_NIF_TERM nif_part_gc(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
     if (argc != 3 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
@@ -894,44 +1049,68 @@ static ERL_NIF_TERM nif_part_gc(ErlNifEnv *env, int argc, const ERL_NIF_TERM arg
     agn_ctx *c = p->ctx->ctx;
     const uint8_t one = 1;
     pthread_mutex_lock(&p->gc_mu);
-    rc = agn_memset_d(c, p->d_prune, 0, p->K, NULL);
-    if (!rc) rc = agn_memcpy_h2d(c, p->d_prune + k, &one, 1, NULL);
-    if (!rc) rc = agn_memcpy_h2d(c, p->d_thr + k * p->D, row, p->D * 8, NULL);
-    if (!rc) rc = agn_memcpy_h2d(c, p->d_thrm + k * p->W, mask, p->W * 8, NULL);
-    if (!rc) rc = agn_stream_sync(c, NULL);
-    if (!rc) rc = agn_oplog_prune(p->log, p->d_prune, p->d_thr, p->d_thrm, NULL, NULL);
+    for (uint32_t t = AGN_COUNTER_PN; t <= AGN_REGISTER_MV && !rc; ++t) {
+        part_sub *s = sub_get(p, t);
+        uint32_t len = 0;
+        if (!s) continue;
+        rc = agn_oplog_key_meta(s->log, 1, &k, &len, NULL, NULL);
+        if (rc || len == 0) continue;
+        rc = agn_memset_d(c, s->d_prune, 0, p->K, NULL);
+        if (!rc) rc = agn_memcpy_h2d(c, s->d_prune + k, &one, 1, NULL);
+        if (!rc) rc = agn_memcpy_h2d(c, s->d_thr + k * p->D, row, p->D * 8, NULL);
+        if (!rc) rc = agn_memcpy_h2d(c, s->d_thrm + k * p->W, mask, p->W * 8, NULL);
+        if (!rc) rc = agn_stream_sync(c, NULL);
+        if (!rc) rc = agn_oplog_prune(s->log, s->d_prune, s->d_thr, s->d_thrm, NULL, NULL);
+        if (!rc) rc = agn_oplog_key_meta(s->log, 1, &k, &len, NULL, NULL);
+        if (!rc && len == 0) inv_drop(p, k, t, 0);
+    }
     pthread_mutex_unlock(&p->gc_mu);
     return rc ? error_tuple(env, rc) : atom(env, "ok");
 }
 
 static ERL_NIF_TERM nif_part_gc_due(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
+    uint32_t type;
     uint64_t k;
     uint8_t due = 0;
-    if (argc != 2 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    if (argc != 3 || !get_part(env, argv[0], &p) || !type_of(env, argv[2], &type))
+        return enif_make_badarg(env);
     int rc = key_index(env, p, argv[1], &k);
-    if (!rc) rc = agn_oplog_gc_due(p->log, 1, &k, &due);
+    part_sub *s = sub_get(p, type);
+    /* no log of the type yet: the key's first op (id 1, Length 0) is not due */
+    if (!rc && s) rc = agn_oplog_gc_due(s->log, 1, &k, &due);
     if (rc) return error_tuple(env, rc);
     return atom(env, due ? "true" : "false");
 }
 
 static ERL_NIF_TERM nif_part_stats(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
-    uint64_t e, s, t;
+    uint64_t E = 0, S = 0, T = 0;
     if (argc != 1 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
-    int rc = agn_oplog_stats(p->log, &e, &s, &t);
-    if (rc) return error_tuple(env, rc);
-    return enif_make_tuple3(env, enif_make_uint64(env, e), enif_make_uint64(env, s),
-                            enif_make_uint64(env, t));
+    for (uint32_t t = AGN_COUNTER_PN; t <= AGN_REGISTER_MV; ++t) {
+        part_sub *s = sub_get(p, t);
+        uint64_t e, sl, tk;
+        if (!s) continue;
+        int rc = agn_oplog_stats(s->log, &e, &sl, &tk);
+        if (rc) return error_tuple(env, rc);
+        E += e;
+        S += sl;
+        T += tk;
+    }
+    return enif_make_tuple3(env, enif_make_uint64(env, E), enif_make_uint64(env, S),
+                            enif_make_uint64(env, T));
 }
 
 static ERL_NIF_TERM nif_part_key_meta(ErlNifEnv *env, int argc, const ERL_NIF_TERM argv[]) {
     part_res *p;
+    uint32_t type;
     uint64_t k;
     uint32_t len = 0, ll = 0, ct = 0;
-    if (argc != 2 || !get_part(env, argv[0], &p)) return enif_make_badarg(env);
+    if (argc != 3 || !get_part(env, argv[0], &p) || !type_of(env, argv[2], &type))
+        return enif_make_badarg(env);
     int rc = key_index(env, p, argv[1], &k);
-    if (!rc) rc = agn_oplog_key_meta(p->log, 1, &k, &len, &ll, &ct);
+    part_sub *s = sub_get(p, type);
+    if (!rc && s) rc = agn_oplog_key_meta(s->log, 1, &k, &len, &ll, &ct);
     if (rc) return error_tuple(env, rc);
     return enif_make_tuple3(env, enif_make_uint(env, len), enif_make_uint(env, ll),
                             enif_make_uint(env, ct));
@@ -940,14 +1119,14 @@ static ERL_NIF_TERM nif_part_key_meta(ErlNifEnv *env, int argc, const ERL_NIF_TE
 static ErlNifFunc funcs[] = {
     {"open", 1, nif_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_open", 5, nif_part_open, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"part_update", 5, nif_part_update, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"part_read", 5, nif_part_read, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"part_materialize", 6, nif_part_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_update", 6, nif_part_update, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_read", 6, nif_part_read, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_materialize", 7, nif_part_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_gc", 3, nif_part_gc, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"part_store", 7, nif_part_store, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"part_gc_due", 2, nif_part_gc_due, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_store", 8, nif_part_store, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_gc_due", 3, nif_part_gc_due, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"part_stats", 1, nif_part_stats, ERL_NIF_DIRTY_JOB_IO_BOUND},
-    {"part_key_meta", 2, nif_part_key_meta, ERL_NIF_DIRTY_JOB_IO_BOUND},
+    {"part_key_meta", 3, nif_part_key_meta, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"materialize", 6, nif_materialize, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"gst_min", 5, nif_gst_min, ERL_NIF_DIRTY_JOB_IO_BOUND},
     {"select_base", 7, nif_select_base, ERL_NIF_DIRTY_JOB_IO_BOUND},

@@ -15,10 +15,10 @@
 -export([materialize/4, get_min_time/1]).
 %% clocksi_materializer:new/1, materialize_eager/3; materializer:update_snapshot/3
 -export([new/1, materialize_eager/3, update_snapshot/3]).
-%% engine-owned partition (one per materializer_vnode)
--export([part_open/5, part_update/5, part_read/5, part_materialize/6, part_gc/3,
-         part_gc_due/2, part_stats/1, part_key_meta/2, part_store/7]).
--export([new_partition/3, update/3, read/4, read/5, read_from/6, gc/3]).
+%% engine-owned partition (one per materializer_vnode, keys of every type)
+-export([part_open/5, part_update/6, part_read/6, part_materialize/7, part_gc/3,
+         part_gc_due/3, part_stats/1, part_key_meta/3, part_store/8]).
+-export([new_partition/3, update/3, read/5, read_cached/5, read_from/7, gc/3]).
 
 -on_load(init/0).
 
@@ -46,14 +46,14 @@ materialize(_Ctx, _Type, _NDcs, _Log, _Read, _CapOff) -> erlang:nif_error(not_lo
 gst_min(_Ctx, _NDcs, _NParts, _Clocks, _Defined) -> erlang:nif_error(not_loaded).
 select_base(_Ctx, _NDcs, _CacheOff, _Clocks, _ClockMask, _R, _RMask) -> erlang:nif_error(not_loaded).
 part_open(_Ctx, _Type, _NDcs, _NKeys, _Cached) -> erlang:nif_error(not_loaded).
-part_update(_Part, _Key, _OcPairs, _TxId, _Effect) -> erlang:nif_error(not_loaded).
-part_read(_Part, _Key, _RPairs, _TxId, _Gc) -> erlang:nif_error(not_loaded).
-part_materialize(_Part, _Key, _RPairs, _Sct, _TxId, _Base) -> erlang:nif_error(not_loaded).
+part_update(_Part, _Key, _Type, _OcPairs, _TxId, _Effect) -> erlang:nif_error(not_loaded).
+part_read(_Part, _Key, _Type, _RPairs, _TxId, _Gc) -> erlang:nif_error(not_loaded).
+part_materialize(_Part, _Key, _Type, _RPairs, _Sct, _TxId, _Base) -> erlang:nif_error(not_loaded).
 part_gc(_Part, _Key, _ThresholdPairs) -> erlang:nif_error(not_loaded).
-part_store(_Part, _Key, _CommitTimePairs, _NewLastOp, _Count, _Value, _Gc) -> erlang:nif_error(not_loaded).
-part_gc_due(_Part, _Key) -> erlang:nif_error(not_loaded).
+part_store(_Part, _Key, _Type, _CommitTimePairs, _NewLastOp, _Count, _Value, _Gc) -> erlang:nif_error(not_loaded).
+part_gc_due(_Part, _Key, _Type) -> erlang:nif_error(not_loaded).
 part_stats(_Part) -> erlang:nif_error(not_loaded).
-part_key_meta(_Part, _Key) -> erlang:nif_error(not_loaded).
+part_key_meta(_Part, _Key, _Type) -> erlang:nif_error(not_loaded).
 
 ctx() ->
     case persistent_term:get({?MODULE, ctx}, undefined) of
@@ -336,11 +336,15 @@ get_min_time(Dict) ->
                                T =/= ?U64_MAX]).
 
 %% ---------------------------------------------------------------------------
-%% The engine-owned partition: materializer_vnode's ops cache in HBM.
+%% The engine-owned partition: materializer_vnode's ops cache in HBM.  Like
+%% ops_cache-<P> it holds keys of every CRDT type (one device op log per
+%% type, created with the type's first op); a read of a key that holds ops of
+%% another type raises corrupted_ops_cache, as materialize_intern does
+%% (src/clocksi_materializer.erl:190-191).
 %% Cached = true: the snapshot cache lives on the device too (every type: the
-%% set_aw / register_mv snapshot states stay on the device), read/4 is the
+%% set_aw / register_mv snapshot states stay on the device), read/5 is the
 %% whole read/6; Cached = false: the reference's own ETS
-%% snapshot cache stays, and read_from/6 is materialize/4 over the resident ops.
+%% snapshot cache stays, and read_from/7 is materialize/4 over the resident ops.
 new_partition(Type, NKeys, Cached) ->
     {ok, Ps} = application:get_env(antidote, gpu_dcs),   % DC slots per clock (<= 256)
     part_open(ctx(), type_id(Type), Ps, NKeys, Cached).
@@ -350,17 +354,18 @@ new_partition(Type, NKeys, Cached) ->
 %% snapshot time (:640) runs first, then the op is inserted.  Its OpSSCommit is
 %% the snapshot_time with the commit DC set to the commit time
 %% (src/clocksi_materializer.erl:224).  Returns {ok, OpId, GcRan}.  (With the
-%% reference's ETS snapshot cache, the vnode checks part_gc_due/2 itself, runs
+%% reference's ETS snapshot cache, the vnode checks part_gc_due/3 itself, runs
 %% its own internal_read(..., true) -- whose snapshot_insert_gc calls gc/3 --
-%% and then part_update/5.)
+%% and then part_update/6.)
 update(Part, Key, #clocksi_payload{type = Type, snapshot_time = SS, commit_time = {Dc, Ct},
                                    txid = TxId, op_param = Effect}) ->
-    GcRan = case part_gc_due(Part, Key) of
+    TypeId = type_id(Type),
+    GcRan = case part_gc_due(Part, Key, TypeId) of
                 true ->
-                    case part_read(Part, Key, dict:to_list(SS), ignore, true) of
+                    case part_read(Part, Key, TypeId, dict:to_list(SS), ignore, true) of
                         {error, not_cached} ->
                             %% an uncached partition's GC read is the vnode's own
-                            %% (its ETS snapshot cache): use part_update/5 there
+                            %% (its ETS snapshot cache): use part_update/6 there
                             erlang:error({update_needs_cached_partition, Key});
                         {error, no_snapshot} ->
                             %% no cached snapshot <= the op's snapshot time: the GC
@@ -374,23 +379,23 @@ update(Part, Key, #clocksi_payload{type = Type, snapshot_time = SS, commit_time 
                     end;
                 false -> false
             end,
-    case part_update(Part, Key, dict:to_list(dict:store(Dc, Ct, SS)), TxId, Effect) of
+    case part_update(Part, Key, TypeId, dict:to_list(dict:store(Dc, Ct, SS)), TxId, Effect) of
         {ok, OpId, _} -> {ok, OpId, GcRan};
         Error -> Error
     end.
 
-%% read/6 on a cached partition: {ok, Value} | {error, no_snapshot} (the
-%% caller reads the log: get_from_snapshot_log, :416-419; read/5 below does
-%% it) | {error, Reason}.
-read(Part, Key, MinSnapshotTime, TxId) ->
-    case part_read(Part, Key, dict:to_list(MinSnapshotTime), TxId, false) of
+%% read/6 on a cached partition without the log fallback: {ok, Value} |
+%% {error, no_snapshot} (the caller reads the log: get_from_snapshot_log,
+%% :416-419; read/5 below does it) | {error, Reason}.
+read_cached(Part, Key, Type, MinSnapshotTime, TxId) ->
+    case part_read(Part, Key, type_id(Type), dict:to_list(MinSnapshotTime), TxId, false) of
         {ok, Value, _NewLastOp, _LastOpCt, _IsNewSS, _Count} -> {ok, Value};
         Other -> Other
     end.
 
 %% read/6 with the log fallback (internal_read/7, :371-376, ShouldGc = false).
 read(Part, Key, Type, MinSnapshotTime, TxId) ->
-    case read(Part, Key, MinSnapshotTime, TxId) of
+    case read_cached(Part, Key, Type, MinSnapshotTime, TxId) of
         {error, no_snapshot} -> read_from_log(Part, Key, Type, MinSnapshotTime, TxId, false);
         Other -> Other
     end.
@@ -399,8 +404,11 @@ read(Part, Key, Type, MinSnapshotTime, TxId) ->
 %% cached partition: the key's ops from the partition's log
 %% (logging_vnode:get_up_to_time), materialize/4 over them on the device
 %% (per-call path), and -- for a GC read -- the result stored with its GC on
-%% the device cache (part_store/7).  A log response is never the newest
+%% the device cache (part_store/8).  A log response is never the newest
 %% snapshot (src/logging_vnode.erl:538-540), so a plain read stores nothing.
+%% The reference's store cannot fail; a device store that does (the arena
+%% re-pack out of memory, a clock wider than the partition) leaves the
+%% snapshot uncached, which only costs a later read the log again.
 read_from_log(Part, Key, Type, SnapshotTime, TxId, ShouldGc) ->
     LogId = log_utilities:get_logid_from_key(Key),
     Partition = log_utilities:get_key_partition(Key),
@@ -415,8 +423,13 @@ read_from_log(Part, Key, Type, SnapshotTime, TxId, ShouldGc) ->
                 {ok, Value, NewLastOp, CommitTime, _WasUpdated, Count} ->
                     case ShouldGc of
                         true ->
-                            ok = part_store(Part, Key, dict:to_list(CommitTime), NewLastOp,
-                                            Count, Value, true);
+                            case part_store(Part, Key, type_id(Type), dict:to_list(CommitTime),
+                                            NewLastOp, Count, Value, true) of
+                                ok -> ok;
+                                {error, Why} ->
+                                    logger:warning("gpu partition: snapshot of ~p not cached: ~p",
+                                                   [Key, Why])
+                            end;
                         false -> ok
                     end,
                     {ok, Value}
@@ -426,9 +439,10 @@ read_from_log(Part, Key, Type, SnapshotTime, TxId, ShouldGc) ->
 %% materialize/4 over the partition's resident ops from a base snapshot the
 %% caller's ETS snapshot cache selected: same result as
 %% clocksi_materializer:materialize/4 ({ok, V, NewLastOp, LastOpCt, IsNewSS, Count}).
-read_from(Part, Key, MinSnapshotTime, SCT, TxId, BaseValue) ->
+read_from(Part, Key, Type, MinSnapshotTime, SCT, TxId, BaseValue) ->
     Sct = case SCT of ignore -> ignore; _ -> dict:to_list(SCT) end,
-    case part_materialize(Part, Key, dict:to_list(MinSnapshotTime), Sct, TxId, BaseValue) of
+    case part_materialize(Part, Key, type_id(Type), dict:to_list(MinSnapshotTime), Sct, TxId,
+                          BaseValue) of
         {ok, V, H, Ct, NewSS, C} ->
             {ok, V, H, case Ct of ignore -> ignore; _ -> dict:from_list(Ct) end, NewSS, C};
         Other -> Other

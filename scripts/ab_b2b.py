@@ -7,6 +7,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 from bench import CONFIGS, probe_read_gbs  # noqa: E402
@@ -23,6 +24,7 @@ byts = K * 64 * 72 + K * 168
 for rnd in range(3):
     for glds in ("0", "1"):
         os.environ["AGN_COUNTER_GLDS"] = glds
+        env_changed()
         for _ in range(2):
             eng.materialize(dl, dr, res, stream=sp)
         torch.cuda.synchronize()

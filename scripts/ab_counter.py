@@ -7,6 +7,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 
@@ -26,8 +27,10 @@ for rnd in range(12):
                      ("AGN_COUNTER_IMPL", impl)):
             if x is None:
                 os.environ.pop(k, None)
+                env_changed()
             else:
                 os.environ[k] = x
+                env_changed()
         b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b.record()
         eng.materialize(dl, dr, res[v], stream=sp)
@@ -40,7 +43,9 @@ from bench import probe_read_gbs  # noqa: E402
 pr = probe_read_gbs(eng, dl, keys * 64 * 8 * 8, sp, torch)
 print(f"probe read ceiling: {pr:.0f} GB/s")
 os.environ.pop("AGN_COUNTER_IMPL", None)
+env_changed()
 os.environ.pop("AGN_COUNTER_VARIANT", None)
+env_changed()
 ref = eng.fetch_result(res["general"])
 same = {}
 for v in res:

@@ -12,6 +12,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 from bench import CONFIGS, algorithmic_bytes, probe_read_gbs  # noqa: E402
@@ -55,8 +56,10 @@ for c in a.cfg or [2]:
         for k in KNOBS:
             if k in env:
                 os.environ[k] = env[k]
+                env_changed()
             else:
                 os.environ.pop(k, None)
+                env_changed()
 
     for rnd in range(a.rounds):
         order = names[rnd % len(names):] + names[:rnd % len(names)]
@@ -77,6 +80,7 @@ for c in a.cfg or [2]:
         outs[x] = eng.fetch_result(res)
     for k in KNOBS:
         os.environ.pop(k, None)
+        env_changed()
     first = next(iter(VARS))
     fields = FIELDS if cfg["crdt_type"] == 1 else FIELDS[1:] + ("out_n", "out_tag", "out_tok")
     n_live = 0 if cfg["crdt_type"] == 1 else int(outs[first].out_n.astype(np.int64).sum())

@@ -6,6 +6,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 
@@ -19,12 +20,15 @@ GRIDS = ["196608", "625000", "1250000", "2500000"]
 res = eng.alloc_result(keys, 8, sparse=False)
 sp = torch.cuda.current_stream().cuda_stream
 os.environ["AGN_COUNTER_VARIANT"] = var
+env_changed()
 times = {g: [] for g in GRIDS}
 for rnd in range(8):
     for g in GRIDS:
         os.environ["AGN_GROUP_BLOCKS"] = g
+        env_changed()
         if g == "0":
             os.environ.pop("AGN_GROUP_BLOCKS")
+            env_changed()
         b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b.record()
         eng.materialize(dl, dr, res, stream=sp)

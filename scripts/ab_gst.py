@@ -12,6 +12,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from antidote_amd._lib import env_changed  # noqa: E402
 
 
 def main():
@@ -35,7 +36,9 @@ def main():
     for r in range(rounds):
         for name, b, u, nt in (variants if r % 2 == 0 else variants[::-1]):
             os.environ["AGN_GST_BLOCKS"], os.environ["AGN_GST_UNROLL"] = b, u
+            env_changed()
             os.environ["AGN_GST_NT"] = nt
+            env_changed()
             eng.gst_min(D, P, E, clocks.data_ptr(), None, out.data_ptr(), sp)
             torch.cuda.synchronize()
             if ref is None:

@@ -8,6 +8,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 from bench import probe_read_gbs  # noqa: E402
@@ -29,7 +30,9 @@ for rnd in range(14):
     for v in order:
         for k in ("AGN_COUNTER_ID0", "AGN_COUNTER_GLDS", "AGN_COUNTER_KPW"):
             os.environ.pop(k, None)
+            env_changed()
         os.environ.update(VARS[v])
+        env_changed()
         b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b.record()
         eng.materialize(dl, dr, res, stream=sp)

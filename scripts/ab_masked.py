@@ -25,6 +25,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from antidote_amd._lib import env_changed  # noqa: E402
 
 HINTS = 0x1 | 0x2  # AGN_HINT_R_FULL | AGN_HINT_CT_FLAG
 # name: (inputs, env, hints)
@@ -40,8 +41,14 @@ VARIANTS = {
     "mixed_km1": ("mixed", {"AGN_Q8E_KM": "1"}, 0),
     "mixed_hint": ("mixed", {}, 0x4),   # AGN_HINT_MIXED: k_counter_key
     "masked_two": ("masked", {"AGN_Q8E_TWO": "1"}, 0x2),  # warm: k_counter_q8e2
+    # round 5: the dense kernel one request per wave (k_counter_key quad rows;
+    # warm dense batches default to two per wave, k_counter_quad2), and the
+    # masked batch through k_counter_quad2's MSK form
+    "dense_q1": ("dense", {"AGN_COUNTER_VARIANT": "2"}, 0),
+    "masked_quad2": ("masked", {"AGN_COUNTER_VARIANT": "3"}, HINTS),
+    "masked_old_hints": ("masked", {"AGN_COUNTER_EARLY": "0"}, HINTS),
 }
-KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM", "AGN_Q8E_TWO")
+KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM", "AGN_Q8E_TWO", "AGN_COUNTER_VARIANT")
 
 
 def main():
@@ -87,8 +94,10 @@ def main():
         for k in KNOBS:
             if k in env:
                 os.environ[k] = env[k]
+                env_changed()
             else:
                 os.environ.pop(k, None)
+                env_changed()
     ms = {n: [] for n in names}
     ref, same = {}, {}
     for r in range(rounds + 1):

@@ -11,6 +11,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 from bench import CONFIGS, algorithmic_bytes, probe_read_gbs  # noqa: E402
@@ -71,7 +72,9 @@ for rnd in range(14):
         lib, env = VARS[v]
         for k in ENVS:
             os.environ.pop(k, None)
+            env_changed()
         os.environ.update(env)
+        env_changed()
         b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b.record()
         run(lib)
@@ -83,6 +86,7 @@ for rnd in range(14):
             outs[v] = eng.fetch_result(res)
 for k in ENVS:
     os.environ.pop(k, None)
+    env_changed()
 pr = probe_read_gbs(eng, dl, K * cfg["ops_per_key"] * cfg["n_dcs"] * 8, sp, torch)
 n_rem = n_live = 0
 if cfg["crdt_type"] != 1:

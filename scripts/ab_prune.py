@@ -19,6 +19,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from antidote_amd._lib import env_changed  # noqa: E402
 
 
 def main():
@@ -64,12 +65,14 @@ def main():
                 ("mw6", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "6"}),
                 ("mw8", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "8"})]
     os.environ["AGN_PRUNE_WPB"] = "1"
+    env_changed()
     best = {v[0]: [] for v in variants}
     sums = {}
     chk = ["key_len", "oc", "op_id"] + (["eff"] if cfg["crdt_type"] == 1 else ["tag", "add_tok", "rem_tok"])
     for r in range(rounds):
         for name, env in (variants if r % 2 == 0 else variants[::-1]):
             os.environ.update({"AGN_PRUNE_TCOOP": "0", **env})
+            env_changed()
             eng.prune_ops(din, None, dr.R, None, out)
             torch.cuda.synchronize()
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -18,6 +18,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine, OpLog  # noqa: E402
 
@@ -52,6 +53,7 @@ def main():
     for r in range(rounds + 1):
         for name, env in (variants if r % 2 == 0 else variants[::-1]):
             os.environ.update({"AGN_PRUNE_TAIL_KPW": "1", **env})
+            env_changed()
             with OpLog(eng, _abi.COUNTER_PN, D, K, init_slots=N + 8) as ol:
                 ol.append(keys, oc, txid=txid, eff=eff)
                 ol.flush()

@@ -13,6 +13,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 from bench import CONFIGS, algorithmic_bytes  # noqa: E402
@@ -49,7 +50,9 @@ def main():
             for name, env in (variants if rnd % 2 == 0 else variants[::-1]):
                 for k in knobs:
                     os.environ.pop(k, None)
+                    env_changed()
                 os.environ.update(env)
+                env_changed()
                 b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 b.record()
                 eng.materialize(dl, dr, res, stream=sp)
@@ -73,6 +76,7 @@ def main():
             bb.free()
     for k in knobs:
         os.environ.pop(k, None)
+        env_changed()
     print(json.dumps(report), flush=True)
 
 

@@ -8,6 +8,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from antidote_amd._lib import env_changed  # noqa: E402
 from antidote_amd import _abi  # noqa: E402
 from antidote_amd.engine import Engine  # noqa: E402
 from bench import CONFIGS, algorithmic_bytes, probe_read_gbs  # noqa: E402
@@ -36,6 +37,7 @@ for c in cfgs:
     for rnd in range(14):
         for x in VAR:
             os.environ["AGN_XCD_REMAP"] = x
+            env_changed()
             b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             b.record()
             eng.materialize(dl, dr, res[x], stream=sp)
@@ -59,3 +61,4 @@ for c in cfgs:
         for bb in r.bufs.values():
             bb.free()
 os.environ.pop("AGN_XCD_REMAP", None)
+env_changed()

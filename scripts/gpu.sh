@@ -76,12 +76,14 @@ expand() {
         echo "spmcj$m|60|python3 scripts/pmc_traffic.py gpurun_out/prof_sfetch$m/run_counter_collection.csv gpurun_out/prof_swrite$m/run_counter_collection.csv $sk 10000000 2 gpurun_out/pmc/cfg2_sparse_$m.json"
       done;;
     pmcwarm)
-      # warm cfg3 / cfg4 (bench.py --warm: k_tags from the cached states): the
-      # 3 warm steps' launches, before the 4 agn_read_cached ones
-      for c in ${PMC_WARM-3 4}; do
+      # warm cfg2 / cfg3 / cfg4 (bench.py --warm: k_counter_quad2 from the
+      # cached base, k_tags from the cached states): the 3 warm steps'
+      # launches, before the 4 agn_read_cached ones
+      for c in ${PMC_WARM-2 3 4}; do
+        case $c in 2) k=k_counter_quad2; n=10000000;; *) k=k_tags; n=1000000;; esac
         echo "wfetch$c|240|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_wfetch$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "wwrite$c|240|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_wwrite$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
-        echo "wpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_wfetch$c/run_counter_collection.csv gpurun_out/prof_wwrite$c/run_counter_collection.csv k_tags 1000000 $c gpurun_out/pmc/cfg${c}_warm.json tail:3:4"
+        echo "wpmcj$c|60|python3 scripts/pmc_traffic.py gpurun_out/prof_wfetch$c/run_counter_collection.csv gpurun_out/prof_wwrite$c/run_counter_collection.csv $k $n $c gpurun_out/pmc/cfg${c}_warm.json tail:3:4"
       done;;
     pmctail)
       # the engine-owned log's in-place GC (k_prune_tail) on the prefix-drop bench

@@ -35,3 +35,30 @@ def eng():
     e = Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture
+def monkeypatch(monkeypatch):
+    """pytest's monkeypatch, with every environment change passed on to the
+    library's cached AGN_* knobs (agn_env_reload)."""
+    from antidote_amd import _lib
+    setenv, delenv = monkeypatch.setenv, monkeypatch.delenv
+
+    def _setenv(*a, **k):
+        setenv(*a, **k)
+        _lib.env_changed()
+
+    def _delenv(*a, **k):
+        delenv(*a, **k)
+        _lib.env_changed()
+    monkeypatch.setenv, monkeypatch.delenv = _setenv, _delenv
+    yield monkeypatch
+
+
+@pytest.fixture(autouse=True)
+def _knobs_current():
+    """The previous test's monkeypatch undo has restored the environment:
+    the library re-reads its knobs before this test runs."""
+    from antidote_amd import _lib
+    _lib.env_changed()
+    yield

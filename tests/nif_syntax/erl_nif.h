@@ -52,6 +52,7 @@ int enif_get_tuple(ErlNifEnv *env, ERL_NIF_TERM term, int *arity, const ERL_NIF_
 int enif_get_list_cell(ErlNifEnv *env, ERL_NIF_TERM term, ERL_NIF_TERM *head, ERL_NIF_TERM *tail);
 int enif_get_list_length(ErlNifEnv *env, ERL_NIF_TERM term, unsigned *len);
 int enif_is_empty_list(ErlNifEnv *env, ERL_NIF_TERM term);
+int enif_is_list(ErlNifEnv *env, ERL_NIF_TERM term);
 int enif_is_identical(ERL_NIF_TERM lhs, ERL_NIF_TERM rhs);
 int enif_inspect_binary(ErlNifEnv *env, ERL_NIF_TERM bin_term, ErlNifBinary *bin);
 int enif_term_to_binary(ErlNifEnv *env, ERL_NIF_TERM term, ErlNifBinary *bin);

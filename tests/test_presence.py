@@ -293,7 +293,7 @@ def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clo
                 pay = po.Payload(key, po.COUNTER_PN, eff, dvc(ss, n), (c, ct), s + 1)
                 try:
                     vn.update(key, pay)
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(key)
                 for ol, bt, sparse in ((ls, bs, True), (ld, bd, False)):
                     if ol.gc_due(key)[0]:
@@ -322,7 +322,7 @@ def test_nif_sequence_sparse_vs_dense_and_reference(eng, monkeypatch, read6, clo
                 except NotImplementedError:
                     assert gs["status"] == _abi.SS_LOG, (s, key)
                     continue
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(key)
                     continue
                 assert gs["status"] in (_abi.SS_HIT, _abi.SS_NEW), (s, key, gs["status"])
@@ -355,12 +355,28 @@ FULL_MASKED = [
     ("cfg2", dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0,
                   seed=20250113), "mixed"),
     ("cfg2-warm", dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0,
+                       seed=20250113, warm=1), "full"),
+    ("cfg2-warm", dict(crdt_type=1, n_dcs=8, n_keys=10_000_000, ops_per_key=64, n_elems=0,
                        seed=20250113, warm=1), "mixed"),
     ("cfg3", dict(crdt_type=2, n_dcs=16, n_keys=1_000_000, ops_per_key=256, n_elems=32,
                   seed=20250114), "full"),
     ("cfg3", dict(crdt_type=2, n_dcs=16, n_keys=1_000_000, ops_per_key=256, n_elems=32,
                   seed=20250114), "mixed"),
 ]
+
+# The forms a masked counter batch is launched in (name: hints, key_mask):
+# "copy" = a key_mask buffer the context did not index (no routing by the
+# log's mixed-key count), "indexed" = agn_log_index_masks' own buffer.
+#   plain : k_counter_q8e, mixed keys handed on to k_counter_q8m
+#   auto  : as the library routes it by itself (AGN_HINT_MIXED when more than
+#           1/16 of the keys are mixed)
+#   bench : AGN_HINT_CT_FLAG | AGN_HINT_R_FULL, as bench.py and the read
+#           batcher pass them (LastOpCt masks over every column come back as
+#           AGN_F_CT_FULL)
+#   mixed : AGN_HINT_MIXED (k_counter_key, mixed keys in the same pass)
+HINT_FORMS = {"plain": (0, "copy"), "auto": (0, "indexed"),
+              "bench": (_abi.HINT_CT_FLAG | _abi.HINT_R_FULL, "copy"),
+              "mixed": (_abi.HINT_MIXED, "copy")}
 
 
 @pytest.mark.parametrize("name,spec,mode", FULL_MASKED,
@@ -369,7 +385,9 @@ def test_full_size_masked_sampled(eng, oracle_lib, name, spec, mode):
     """BASELINE shapes with presence masks on every op clock and read (the
     NIF's partition logs, bench.py --sparse): key DC sets indexed on the
     device, every key materialized, a sample bit-exact against the oracle
-    (host-generated keys with the same masks)."""
+    (host-generated keys with the same masks).  Counter batches run in every
+    HINT_FORMS form, bench.py's hinted one included; a request flagged
+    AGN_F_CT_FULL must be one whose oracle LastOpCt mask is every column."""
     import torch
     from antidote_amd.engine import free_gen_host, gen_host
     cfg = _abi.AgnGenCfg(**{"key_base": 0, "key_stride": 1, "warm": 0, **spec})
@@ -384,50 +402,63 @@ def test_full_size_masked_sampled(eng, oracle_lib, name, spec, mode):
     dl.oc_mask, dr.R_mask = ocm.data_ptr(), rm.data_ptr()
     cap = np.arange(K + 1, dtype=np.uint64) * np.uint64(N) if cfg.crdt_type != 1 else None
     res = eng.alloc_result(K, D, sparse=True, cap_off=cap)
-    kb = None
+    kb = kcopy = None
+    rng = np.random.default_rng(cfg.seed + 7)
+    sample = np.sort(rng.choice(K, 48, replace=False))
+    sample[0], sample[-1] = 0, K - 1
+    want = {}
+    for k in sample:   # the oracle on host-generated copies of the sampled keys
+        c1 = _abi.AgnGenCfg(crdt_type=cfg.crdt_type, n_dcs=D, n_keys=1, ops_per_key=N,
+                            n_elems=cfg.n_elems, seed=cfg.seed, key_base=int(k),
+                            key_stride=1, warm=cfg.warm)
+        hl, hr = gen_host(c1)
+        hm = entry_masks(np.arange(int(k) * N, (int(k) + 1) * N, dtype=np.int64), D, mode,
+                         np).astype(np.uint64).reshape(N, 1)
+        hrm = np.full((1, 1), (1 << D) - 1, np.uint64)
+        hl.oc_mask, hr.R_mask = hm.ctypes.data, hrm.ctypes.data
+        capo = np.array([0, N], np.uint64) if cfg.crdt_type != 1 else None
+        w = alloc_result(1, D, sparse=True, cap_off=capo)
+        assert oracle_lib.oracle_materialize(C.byref(hl), C.byref(hr),
+                                             C.byref(result_struct(w)), 1) == 0
+        hl.oc_mask = hr.R_mask = None
+        free_gen_host(hl, hr)
+        want[int(k)] = w
+    forms = HINT_FORMS if cfg.crdt_type == 1 else {"plain": (0, "indexed")}
     try:
         kb = eng.index_masks(dl)
+        kcopy = eng.upload(eng.download(kb, np.uint64, (K,)))
         torch.cuda.synchronize()
-        eng.materialize(dl, dr, res)
-        eng.sync()
-        flags = eng.download(res.bufs["flags"], np.uint32, (K,))
-        assert not (flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED |
-                             _abi.F_ERR_CAPACITY)).any()
-        rng = np.random.default_rng(cfg.seed + 7)
-        sample = np.sort(rng.choice(K, 48, replace=False))
-        sample[0], sample[-1] = 0, K - 1
-        full = eng.fetch_result(res)
-        for k in sample:
-            c1 = _abi.AgnGenCfg(crdt_type=cfg.crdt_type, n_dcs=D, n_keys=1, ops_per_key=N,
-                                n_elems=cfg.n_elems, seed=cfg.seed, key_base=int(k),
-                                key_stride=1, warm=cfg.warm)
-            hl, hr = gen_host(c1)
-            hm = entry_masks(np.arange(int(k) * N, (int(k) + 1) * N, dtype=np.int64), D, mode,
-                             np).astype(np.uint64).reshape(N, 1)
-            hrm = np.full((1, 1), (1 << D) - 1, np.uint64)
-            hl.oc_mask, hr.R_mask = hm.ctypes.data, hrm.ctypes.data
-            capo = np.array([0, N], np.uint64) if cfg.crdt_type != 1 else None
-            w = alloc_result(1, D, sparse=True, cap_off=capo)
-            assert oracle_lib.oracle_materialize(C.byref(hl), C.byref(hr),
-                                                 C.byref(result_struct(w)), 1) == 0
-            hl.oc_mask = hr.R_mask = None
-            free_gen_host(hl, hr)
-            assert int(full.flags[k]) == int(w.flags[0]), k
-            assert int(full.hole[k]) == int(w.hole[0]), k
-            assert int(full.count[k]) == int(w.count[0]), k
-            assert np.array_equal(full.lastct[k], w.lastct[0]), k
-            assert np.array_equal(full.lastct_mask[k], w.lastct_mask[0]), k
-            if cfg.crdt_type == 1:
-                assert int(full.value[k]) == int(w.value[0]), k
-            else:
-                n, o = int(full.out_n[k]), int(full.out_off[k])
-                assert n == int(w.out_n[0]), k
-                assert np.array_equal(full.out_tag[o:o + n], w.out_tag[:n]), k
-                assert np.array_equal(full.out_tok[o:o + n], w.out_tok[:n]), k
+        for form, (hints, km) in forms.items():
+            dl.key_mask = (kb if km == "indexed" else kcopy).ptr
+            dr.hints = hints
+            eng.materialize(dl, dr, res)
+            eng.sync()
+            raw_flags = eng.download(res.bufs["flags"], np.uint32, (K,))
+            assert not (raw_flags & (_abi.F_ERR_UNEXPECTED | _abi.F_ERR_CORRUPTED |
+                                     _abi.F_ERR_CAPACITY)).any(), form
+            if not hints & _abi.HINT_CT_FLAG:
+                assert not (raw_flags & _abi.F_CT_FULL).any(), form
+            full = eng.fetch_result(res)   # AGN_F_CT_FULL expanded to its mask word
+            for k in sample:
+                w = want[int(k)]
+                if raw_flags[k] & _abi.F_CT_FULL:
+                    assert int(w.lastct_mask[0, 0]) == (1 << D) - 1, (form, k)
+                assert int(full.flags[k]) == int(w.flags[0]), (form, k)
+                assert int(full.hole[k]) == int(w.hole[0]), (form, k)
+                assert int(full.count[k]) == int(w.count[0]), (form, k)
+                assert np.array_equal(full.lastct[k], w.lastct[0]), (form, k)
+                assert np.array_equal(full.lastct_mask[k], w.lastct_mask[0]), (form, k)
+                if cfg.crdt_type == 1:
+                    assert int(full.value[k]) == int(w.value[0]), (form, k)
+                else:
+                    n, o = int(full.out_n[k]), int(full.out_off[k])
+                    assert n == int(w.out_n[0]), (form, k)
+                    assert np.array_equal(full.out_tag[o:o + n], w.out_tag[:n]), (form, k)
+                    assert np.array_equal(full.out_tok[o:o + n], w.out_tok[:n]), (form, k)
     finally:
         dl.oc_mask = dr.R_mask = dl.key_mask = None
         eng.free_gen(dl, dr)
-        for b in list(res.bufs.values()) + ([kb] if kb else []):
+        for b in list(res.bufs.values()) + [x for x in (kb, kcopy) if x]:
             b.free()
         del ocm, rm
         torch.cuda.empty_cache()

@@ -240,7 +240,7 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
                 pay = po.Payload(key, PTYPE[typ], eff, vc(ss, int(mask)), (c, ct), s + 1)
                 try:
                     vn.update(key, pay)
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(key)
                 part.update(key, pay, oc, entry, s + 1, mask, ss)
                 if placeholder(vn, key):
@@ -252,7 +252,7 @@ def test_batcher_states_vs_reference(eng, typ, d, logk, read6, monkeypatch):
                     continue
                 try:
                     want = vn.read(key, PTYPE[typ], vc(R), po.IGNORE)
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(key)
                     continue
                 assert want == got, (s, key, g["status"], want, got)
@@ -307,7 +307,7 @@ def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
                     pay = po.Payload(key, PTYPE[typ], eff, vc(ss, int(mask)), (c, ct), s + 1)
                     try:
                         vn.update(key, pay)
-                    except (po.BadMatch, TypeError, ValueError):
+                    except po.BadMatch:
                         quirk.add(key)
                     for p in (pa, pb):
                         p.update(key, pay, oc, entry, s + 1, mask, ss)
@@ -325,7 +325,7 @@ def test_batcher_fused_vs_sequence_mixed_dcs(eng, typ, d, monkeypatch):
                         continue
                     try:
                         want = vn.read(key, PTYPE[typ], vc(R, rm), po.IGNORE)
-                    except (po.BadMatch, TypeError, ValueError):
+                    except po.BadMatch:
                         quirk.add(key)
                         continue
                     assert want == ra, (s, key, ga["status"], want, ra)
@@ -400,7 +400,7 @@ def test_read_cached_states_vs_reference(eng, typ):
                 s += 1
                 try:
                     vn.update(key, po.Payload(key, PTYPE[typ], eff, vc(ss), (c_, ct), s))
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(key)
                 append_entry(ol, key, oc, entry, s)
                 if placeholder(vn, key):
@@ -426,7 +426,7 @@ def test_read_cached_states_vs_reference(eng, typ):
                 except NotImplementedError:
                     assert status[k] == _abi.SS_LOG, (rnd, k)
                     continue
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(k)
                     continue
                 assert status[k] in (_abi.SS_HIT, _abi.SS_NEW), (rnd, k, status[k])
@@ -529,7 +529,7 @@ def test_state_arena_repacks_vs_reference(eng, typ, monkeypatch):
                 pay = po.Payload(key, PTYPE[typ], eff, vc(ss), (c, ct), s + 1)
                 try:
                     vn.update(key, pay)
-                except (po.BadMatch, TypeError, ValueError):
+                except po.BadMatch:
                     quirk.add(key)
                 part.update(key, pay, oc, entry, s + 1, np.uint64((1 << d) - 1), ss)
                 if placeholder(vn, key):
