@@ -123,6 +123,22 @@ __host__ __device__ inline uint64_t key_n(const uint64_t *key_off, const uint64_
     return key_len ? key_len[k] : key_off[k + 1] - key_off[k];
 }
 
+// A load of memory the running kernel never writes, through the constant
+// address space: at a wave-uniform address it is a scalar (s_load) load even
+// where the kernel stores through other pointers that might alias it (a
+// grid-stride loop), which otherwise keeps it a vector load.  Never use it
+// on an array the same launch writes.
+template <class T>
+__device__ __forceinline__ T ldc(const T *p) {
+    return *(const __attribute__((address_space(4))) T *)p;
+}
+// A byte of a read-only byte array (key_type, sct_ignore) by ldc of its
+// aligned dword (byte arrays are allocated in whole dwords or more).
+__device__ __forceinline__ uint32_t ldc_byte(const uint8_t *p, uint64_t idx) {
+    const uint32_t w = ldc(reinterpret_cast<const uint32_t *>(p) + (idx >> 2));
+    return (__builtin_amdgcn_readfirstlane(w) >> ((uint32_t)(idx & 3u) * 8u)) & 0xffu;
+}
+
 // Scalar (wave-uniform) value: lets hipcc keep it in an SGPR.
 __device__ inline uint64_t uniform_u64(uint64_t v) {
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);

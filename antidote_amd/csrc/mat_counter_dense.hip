@@ -491,34 +491,78 @@ __device__ __forceinline__ void q2_meta(Q2Key &k, uint64_t i, const uint64_t *__
 }
 
 // The rest of a request's prologue: key_type, SCT and its ignore byte, TxId,
-// R, the presence words of a sparse batch.
+// R, the presence words of a sparse batch -- as raw scalar loads (q2_load:
+// every address depends only on the request and the key's segment), then the
+// values derived from them (q2_apply).  Scalar loads return out of order, so
+// the first use of any of them waits for all (lgkmcnt(0)): k_counter_q8e
+// issues the whole group under chunk 0's rows and puts a scheduling barrier
+// before the first use -- left alone, the scheduler interleaved uses with the
+// loads and the warm masked prologue became three dependent scalar round
+// trips after the rows (warm masked cfg2 1.23x the dense warm kernel).
+struct Q2Raw {
+    uint64_t kmw, txv, rmw, smw;
+    uint64_t r[8], sv[8];
+    uint32_t ktw, sibw;  // the dwords holding key_type[key] / sct_ignore[i]
+};
+
 template <bool ANY_WARM, bool MSK>
-__device__ __forceinline__ void q2_side(Q2Key &k, const DenseArgs &a, const MaskArgs &mk,
-                                        uint64_t kmw, const uint64_t *__restrict__ key_off,
-                                        const uint8_t *__restrict__ key_type,
-                                        const uint64_t *__restrict__ R,
-                                        const uint64_t *__restrict__ sct,
-                                        const uint8_t *__restrict__ sct_ignore,
-                                        const uint64_t *__restrict__ req_txid) {
+__device__ __forceinline__ Q2Raw q2_load(const Q2Key &k, const DenseArgs &a, const MaskArgs &mk,
+                                         bool with_km, const uint64_t *__restrict__ key_off,
+                                         const uint8_t *__restrict__ key_type,
+                                         const uint64_t *__restrict__ R,
+                                         const uint64_t *__restrict__ sct,
+                                         const uint8_t *__restrict__ sct_ignore,
+                                         const uint64_t *__restrict__ req_txid) {
     constexpr int D = 8;
     const uint64_t i = k.i;
-    const uint32_t kty =
-        byte_of(key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off), k.key);
-    k.corrupt = k.n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu);
-    const uint32_t sib =
-        ANY_WARM ? byte_of(sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R), i) : 0u;
-    k.sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
-    const uint64_t txv = uniform_u64((req_txid ? req_txid : R)[i]);
-    k.txr = req_txid ? txv : 0ull;
-    uint64_t rmw = 0, smw = 0;
+    Q2Raw x;
+    const uint8_t *ktp = key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off);
+    x.ktw = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(ktp)[k.key >> 2]);
+    const uint8_t *sip = sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R);
+    x.sibw = ANY_WARM ? __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(sip)[i >> 2])
+                      : 0u;
+    x.txv = uniform_u64((req_txid ? req_txid : R)[i]);
+    x.kmw = (MSK && with_km) ? key_word(mk, k.key, key_off) : 0ull;
+    x.rmw = x.smw = 0ull;
     if constexpr (MSK) {
         // AGN_HINT_R_FULL: every R mask carries all D DCs (not read)
         const bool rfull = (a.hints & AGN_HINT_R_FULL) != 0u;
-        rmw = uniform_u64(*((mk.R_mask && !rfull) ? mk.R_mask + i : R));
-        if (rfull) rmw = ~0ull;
-        smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
+        x.rmw = uniform_u64(*((mk.R_mask && !rfull) ? mk.R_mask + i : R));
+        x.smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
     }
-    const Presence<D> pr = presence<D, MSK>(mk, kmw, rmw, smw, k.n);
+    const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        x.r[j] = uniform_u64(R[i * D + j]);
+        x.sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
+    }
+    return x;
+}
+
+// Pins the raw side values behind the scheduling barrier: the IR passes hoist
+// a use (kmw & 0xFF) next to its load, where its wait would precede the other
+// loads' issue; a use of an asm output cannot move above the asm.
+__device__ __forceinline__ void q2_pin(Q2Raw &x) {
+    asm volatile("" : "+s"(x.kmw), "+s"(x.txv), "+s"(x.rmw), "+s"(x.smw), "+s"(x.ktw), "+s"(x.sibw));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+s"(x.r[j]), "+s"(x.sv[j]));
+}
+
+template <bool ANY_WARM, bool MSK>
+__device__ __forceinline__ void q2_apply(Q2Key &k, const DenseArgs &a, const MaskArgs &mk,
+                                         const Q2Raw &x, uint64_t kmw,
+                                         const uint8_t *__restrict__ key_type,
+                                         const uint64_t *__restrict__ sct,
+                                         const uint8_t *__restrict__ sct_ignore,
+                                         const uint64_t *__restrict__ req_txid) {
+    constexpr int D = 8;
+    const uint32_t kty = (x.ktw >> ((uint32_t)(k.key & 3u) * 8u)) & 0xffu;
+    k.corrupt = k.n != 0 && key_type != nullptr && kty != (a.req_type & 0xffu);
+    const uint32_t sib = ANY_WARM ? (x.sibw >> ((uint32_t)(k.i & 3u) * 8u)) & 0xffu : 0u;
+    k.sct_ign = !ANY_WARM || sct == nullptr || (sct_ignore && sib != 0u);
+    k.txr = req_txid ? x.txv : 0ull;
+    const uint64_t rmw = (a.hints & AGN_HINT_R_FULL) ? ~0ull : x.rmw;
+    const Presence<D> pr = presence<D, MSK>(mk, kmw, rmw, x.smw, k.n);
     k.U = pr.U;
     k.Rm = pr.Rm;
     k.Sm = pr.Sm;
@@ -528,15 +572,12 @@ __device__ __forceinline__ void q2_side(Q2Key &k, const DenseArgs &a, const Mask
     k.uni = known;
     k.noR = MSK && known && !pr.uni;
     uint64_t r[D], sv[D], ev[D];
-    const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
         const bool inU = ((pr.U >> j) & 1ull) != 0ull;
-        r[j] = uniform_u64(R[i * D + j]);
-        sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
-        ev[j] = (k.sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : sv[j];  // dict read of SCT
-        sv[j] = (MSK && known && !inU) ? ~0ull : ev[j];                // compare value
-        r[j] = (MSK && known && !inU) ? ~0ull : r[j];
+        ev[j] = (k.sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : x.sv[j];  // dict read of SCT
+        sv[j] = (MSK && known && !inU) ? ~0ull : ev[j];                  // compare value
+        r[j] = (MSK && known && !inU) ? ~0ull : x.r[j];
     }
     const int p = lane_id() & 3;
     k.rA = p == 0 ? r[0] : p == 1 ? r[2] : p == 2 ? r[4] : r[6];
@@ -545,6 +586,19 @@ __device__ __forceinline__ void q2_side(Q2Key &k, const DenseArgs &a, const Mask
     k.sB = p == 0 ? sv[1] : p == 1 ? sv[3] : p == 2 ? sv[5] : sv[7];
     k.eA = p == 0 ? ev[0] : p == 1 ? ev[2] : p == 2 ? ev[4] : ev[6];
     k.eB = p == 0 ? ev[1] : p == 1 ? ev[3] : p == 2 ? ev[5] : ev[7];
+}
+
+template <bool ANY_WARM, bool MSK>
+__device__ __forceinline__ void q2_side(Q2Key &k, const DenseArgs &a, const MaskArgs &mk,
+                                        uint64_t kmw, const uint64_t *__restrict__ key_off,
+                                        const uint8_t *__restrict__ key_type,
+                                        const uint64_t *__restrict__ R,
+                                        const uint64_t *__restrict__ sct,
+                                        const uint8_t *__restrict__ sct_ignore,
+                                        const uint64_t *__restrict__ req_txid) {
+    const Q2Raw x = q2_load<ANY_WARM, MSK>(k, a, mk, false, key_off, key_type, R, sct, sct_ignore,
+                                           req_txid);
+    q2_apply<ANY_WARM, MSK>(k, a, mk, x, kmw, key_type, sct, sct_ignore, req_txid);
 }
 
 template <bool ANY_WARM, bool MSK>
@@ -801,9 +855,14 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
     const bool any = a.n_entries != 0;
     Q8Chunk c0{};
     if (any) c0 = q8_load<true, false>(oc, eff, k.off, 0, a.n_entries);
+    // the request's side values: one group of scalar loads under the rows,
+    // used only past the barrier (one lgkmcnt wait, see q2_load)
+    Q2Raw x = q2_load<ANY_WARM, true>(k, a, mk, KM == 0, key_off, key_type, R, sct, sct_ignore,
+                                      req_txid);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KM == 0) kmw = key_word(mk, k.key, key_off);
-    q2_side<ANY_WARM, true>(k, a, mk, kmw, key_off, key_type, R, sct, sct_ignore, req_txid);
+    q2_pin(x);
+    if constexpr (KM == 0) kmw = x.kmw;
+    q2_apply<ANY_WARM, true>(k, a, mk, x, kmw, key_type, sct, sct_ignore, req_txid);
     if (KM == 0 && mixed(kmw)) {
         hand_on();
         return;

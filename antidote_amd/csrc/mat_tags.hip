@@ -232,13 +232,17 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
     const uint32_t D = log.n_dcs, W = n_words(D);
     const uint64_t lt = lanes_below();
-    const uint64_t n_items = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(*tl.in_n) : req.n_req;
+    const uint64_t n_items = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(ldc(tl.in_n)) : req.n_req;
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
 
     const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     for (uint64_t it = (uint64_t)blk * WPB + (uint64_t)w; it < n_items; it += nw) {
-        const uint64_t i = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(tl.in[it]) : it;
-        const uint64_t key = req.keys ? uniform_u64(req.keys[i]) : i;
+        // the per-request / per-key words below are read through the scalar
+        // cache (ldc: arrays this launch never writes); as plain loads in the
+        // grid-stride loop, whose stores may alias them, they were vector
+        // loads waited for one by one before the rows issued
+        const uint64_t i = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(ldc(tl.in + it)) : it;
+        const uint64_t key = req.keys ? uniform_u64(ldc(req.keys + i)) : i;
         LookupOut lk{};
         if constexpr (SV) {
             // get_from_snapshot_cache (materializer_vnode.erl:384-413) on the
@@ -270,30 +274,31 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
         // unconditionally (in-bounds dummies for absent columns): each
         // conditional load was waited for on its own before the next issued.
         const uint64_t *lenp = log.key_len ? log.key_len + key : log.key_off + key + 1;
-        const uint64_t off = uniform_u64(log.key_off[key]);
-        const uint64_t lv = uniform_u64(*lenp);
-        const uint32_t kt = __builtin_amdgcn_readfirstlane(
-            (uint32_t)(log.key_type ? log.key_type
-                                    : reinterpret_cast<const uint8_t *>(log.key_off))[key]);
-        const uint32_t si = SV ? (uint32_t)lk.ign : __builtin_amdgcn_readfirstlane(
-            (uint32_t)(req.sct_ignore ? req.sct_ignore
-                                      : reinterpret_cast<const uint8_t *>(req.R))[i]);
-        const uint64_t txv = uniform_u64((req.txid ? req.txid : req.R)[i]);
+        const uint64_t off = uniform_u64(ldc(log.key_off + key));
+        const uint64_t lv = uniform_u64(ldc(lenp));
+        const uint32_t kt = ldc_byte(
+            log.key_type ? log.key_type : reinterpret_cast<const uint8_t *>(log.key_off), key);
+        const uint32_t si = SV ? (uint32_t)lk.ign : ldc_byte(
+            req.sct_ignore ? req.sct_ignore : reinterpret_cast<const uint8_t *>(req.R), i);
+        const uint64_t txv = uniform_u64(ldc((req.txid ? req.txid : req.R) + i));
         // base state: CSR base_off, or AGN_SS_STATE(start, pairs) in
         // base_value (a snapshot cache's state arena, agn_ss_lookup)
         const bool packed = req.base_off == nullptr && req.base_value != nullptr;
         const uint64_t *bop = req.base_off ? req.base_off + i
                             : packed        ? reinterpret_cast<const uint64_t *>(req.base_value) + i
                                             : req.R + i;
-        const uint64_t b0v = SV ? (uint64_t)lk.base : uniform_u64(bop[0]);
-        const uint64_t b1v = uniform_u64((req.base_off ? bop + 1 : bop)[0]);
+        // SV: the lookup above wrote base_value (lk.base); otherwise read-only
+        const uint64_t b0v = SV ? (uint64_t)lk.base : uniform_u64(ldc(bop));
+        const uint64_t b1v = req.base_off ? uniform_u64(ldc(bop + 1)) : 0ull;
         const uint64_t n = log.key_len ? lv : lv - off;
 
         uint64_t kmw = 0, rmw = 0, smw = 0;
         if constexpr (MSK) {
-            kmw = uniform_u64(*(log.key_mask ? log.key_mask + key : req.R));
-            rmw = uniform_u64(*(req.R_mask ? req.R_mask + i : req.R));
-            smw = uniform_u64(*((req.sct && req.sct_mask) ? req.sct_mask + i : req.R));
+            kmw = uniform_u64(ldc(log.key_mask ? log.key_mask + key : req.R));
+            rmw = uniform_u64(ldc(req.R_mask ? req.R_mask + i : req.R));
+            // SV: the lookup above wrote the SCT mask word (sv.sctm)
+            const uint64_t *smp = (req.sct && req.sct_mask) ? req.sct_mask + i : req.R;
+            smw = uniform_u64(SV ? *smp : ldc(smp));
         }
 
         if (n != 0 && log.key_type != nullptr && kt != (uint32_t)(uint8_t)req.req_type) {

@@ -290,7 +290,9 @@ def cpu_baseline_gc(cfg, n_keys, target_s=2.0):
     n_rem = int(np.ctypeslib.as_array(C.cast(hl.rem_off, C.POINTER(C.c_uint32)),
                                       (E + 1,))[-1]) if tags else 0
     arrs = {"key_off": np.zeros(n_keys + 1, np.uint64), "oc": np.zeros(E * D, np.uint64),
-            "op_id": np.zeros(E, np.uint32), "txid": np.zeros(E, np.uint64)}
+            "op_id": np.zeros(E, np.uint32)}
+    if hl.txid:  # the generator writes TxIds only for some shapes
+        arrs["txid"] = np.zeros(E, np.uint64)
     if tags:
         arrs.update(tag=np.zeros(E, np.uint32), add_tok=np.zeros(E, np.uint64),
                     rem_off=np.zeros(E + 1, np.uint32), rem_tok=np.zeros(max(n_rem, 1), np.uint64))
