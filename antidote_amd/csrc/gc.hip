@@ -351,21 +351,32 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
     const uint64_t i = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
     if (i >= a.n_keys) return;
     const uint64_t K = a.n_keys;   // launch size (meta stride)
-    const uint64_t k = a.key_list ? uniform_u64(a.key_list[i]) : i;
+    const uint64_t k = a.key_list ? uniform_u64(ldc(a.key_list + i)) : i;
     const int lane = lane_id();
     const int sub = lane % LPO, slot = lane / LPO, d0 = sub * DPL;
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t D = a.D, W = a.W;
     constexpr bool tags = TAGS;
-    const uint64_t off = uniform_u64(a.key_off[k]);
-    const uint64_t n = uniform_u64(key_n(a.key_off, a.key_len, k));
-    const bool gc = a.key_list ? a.list_flags[i] != 0 : (prune == nullptr || prune[k] != 0);
-    const uint32_t tb = tags ? (uint32_t)uniform_u64(a.rem_off[off]) : 0u;
+    // The key's metadata: one group of unconditional scalar loads (absent
+    // columns from an in-bounds dummy) through the scalar cache (ldc) -- each
+    // of these words is read by the key's own wave before that wave writes
+    // it (in place) and written by no other wave.  As plain loads the GC
+    // flag byte and the ListLen were vector loads under branches, each waited
+    // for on its own: four round trips before the first row load issued.
+    const uint64_t off = uniform_u64(ldc(a.key_off + k));
+    const uint64_t lraw = uniform_u64(ldc(a.key_len ? a.key_len + k : a.key_off + k + 1));
+    const uint8_t *gfp = a.key_list ? a.list_flags
+                       : prune      ? prune
+                                    : reinterpret_cast<const uint8_t *>(a.key_off);
+    const uint32_t gfb = ldc_byte(gfp, a.key_list ? i : k);
     // the ETS ListLen, with the key's metadata: unconditional (a dummy word
     // when there is none), so it shares their round trip instead of costing
     // one of its own after the scan
     const uint32_t lc0 = __builtin_amdgcn_readfirstlane(
-        *(a.key_lcap ? a.key_lcap + k : reinterpret_cast<const uint32_t *>(a.key_off + k)));
+        ldc(a.key_lcap ? a.key_lcap + k : reinterpret_cast<const uint32_t *>(a.key_off + k)));
+    const uint64_t n = a.key_len ? lraw : lraw - off;
+    const bool gc = (a.key_list == nullptr && prune == nullptr) || gfb != 0u;
+    const uint32_t tb = tags ? __builtin_amdgcn_readfirstlane(ldc(a.rem_off + off)) : 0u;
     const uint32_t lc_in = a.key_lcap ? lc0 : 0u;
     if (lane == 0 && a.d_key_off) a.d_key_off[k] = off;
     if (!gc && !a.copy_unselected) {

@@ -499,9 +499,15 @@ __device__ __forceinline__ void q2_meta(Q2Key &k, uint64_t i, const uint64_t *__
 // before the first use -- left alone, the scheduler interleaved uses with the
 // loads and the warm masked prologue became three dependent scalar round
 // trips after the rows (warm masked cfg2 1.23x the dense warm kernel).
+// R's and SCT's DCs 2p, 2p+1 (p = lane & 3) -- the pair this lane compares
+// -- come as one 16-byte vector load each: as 16 uniform words apiece they
+// sat in SGPRs next to the kernel's pointer arguments, and the warm masked
+// kernel spilled 17 SGPRs to VGPR lanes (v_writelane / v_readlane, issue
+// stalls: SQ_WAIT_INST_ANY 1662 vs 990 quad-cycles per wave, warm masked cfg2
+// 1.26x the dense warm kernel).
 struct Q2Raw {
     uint64_t kmw, txv, rmw, smw;
-    uint64_t r[8], sv[8];
+    u64x2 rq, sq;        // per lane: R / SCT at DCs 2p, 2p+1
     uint32_t ktw, sibw;  // the dwords holding key_type[key] / sct_ignore[i]
 };
 
@@ -531,11 +537,10 @@ __device__ __forceinline__ Q2Raw q2_load(const Q2Key &k, const DenseArgs &a, con
         x.smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
     }
     const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        x.r[j] = uniform_u64(R[i * D + j]);
-        x.sv[j] = ANY_WARM ? uniform_u64(sct_p[i * D + j]) : 0ull;
-    }
+    const uint64_t pp = 2u * (uint64_t)(lane_id() & 3);
+    x.rq = *reinterpret_cast<const u64x2 *>(R + i * D + pp);
+    if constexpr (ANY_WARM) x.sq = *reinterpret_cast<const u64x2 *>(sct_p + i * D + pp);
+    else x.sq = u64x2{0ull, 0ull};
     return x;
 }
 
@@ -544,8 +549,6 @@ __device__ __forceinline__ Q2Raw q2_load(const Q2Key &k, const DenseArgs &a, con
 // loads' issue; a use of an asm output cannot move above the asm.
 __device__ __forceinline__ void q2_pin(Q2Raw &x) {
     asm volatile("" : "+s"(x.kmw), "+s"(x.txv), "+s"(x.rmw), "+s"(x.smw), "+s"(x.ktw), "+s"(x.sibw));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+s"(x.r[j]), "+s"(x.sv[j]));
 }
 
 template <bool ANY_WARM, bool MSK>
@@ -571,21 +574,17 @@ __device__ __forceinline__ void q2_apply(Q2Key &k, const DenseArgs &a, const Mas
     const bool known = !MSK || pr.uni || pr.U != 0ull;
     k.uni = known;
     k.noR = MSK && known && !pr.uni;
-    uint64_t r[D], sv[D], ev[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const bool inU = ((pr.U >> j) & 1ull) != 0ull;
-        ev[j] = (k.sct_ign || !((pr.Sm >> j) & 1ull)) ? 0ull : x.sv[j];  // dict read of SCT
-        sv[j] = (MSK && known && !inU) ? ~0ull : ev[j];                  // compare value
-        r[j] = (MSK && known && !inU) ? ~0ull : x.r[j];
-    }
-    const int p = lane_id() & 3;
-    k.rA = p == 0 ? r[0] : p == 1 ? r[2] : p == 2 ? r[4] : r[6];
-    k.rB = p == 0 ? r[1] : p == 1 ? r[3] : p == 2 ? r[5] : r[7];
-    k.sA = p == 0 ? sv[0] : p == 1 ? sv[2] : p == 2 ? sv[4] : sv[6];
-    k.sB = p == 0 ? sv[1] : p == 1 ? sv[3] : p == 2 ? sv[5] : sv[7];
-    k.eA = p == 0 ? ev[0] : p == 1 ? ev[2] : p == 2 ? ev[4] : ev[6];
-    k.eB = p == 0 ? ev[1] : p == 1 ? ev[3] : p == 2 ? ev[5] : ev[7];
+    // this lane's DCs dA = 2p, dB = 2p + 1
+    const uint32_t dA = 2u * (uint32_t)(lane_id() & 3), dB = dA + 1u;
+    const bool inA = ((pr.U >> dA) & 1ull) != 0ull, inB = ((pr.U >> dB) & 1ull) != 0ull;
+    // e = SCT as a dict read (a DC missing from it = 0); s = the compare
+    // value, r = R: +inf outside U on the dense scan of a masked key
+    k.eA = (k.sct_ign || !((pr.Sm >> dA) & 1ull)) ? 0ull : x.sq.x;
+    k.eB = (k.sct_ign || !((pr.Sm >> dB) & 1ull)) ? 0ull : x.sq.y;
+    k.sA = (MSK && known && !inA) ? ~0ull : k.eA;
+    k.sB = (MSK && known && !inB) ? ~0ull : k.eB;
+    k.rA = (MSK && known && !inA) ? ~0ull : x.rq.x;
+    k.rB = (MSK && known && !inB) ? ~0ull : x.rq.y;
 }
 
 template <bool ANY_WARM, bool MSK>
