@@ -52,81 +52,143 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
 // the scan routes the key as k_counter_key's MSK instantiations do: a key
 // whose entries share one DC set U inside R's runs the dense scan with R and
 // SCT neutralised (+inf) outside U, a mixed key the per-entry-mask scan.
+//
+// NP requests per wave (1 or 2).  A request is a chain of dependent round
+// trips -- its key, then the key's slot count and segment, then the slots
+// and the first chunk of rows.  With NP = 2 each stage's loads are issued
+// for both requests before either waits, and the second request's slots and
+// rows stay in flight while the first is served.  Stages: r6_meta (scalar:
+// slot count, segment, type, presence words, TxId; vector: R), r6_rows (the
+// slots, chunk 0), r6_serve.  Measured (SQ counters, profiles/r05/): at D = 8
+// the kernel is issue-bound rather than latency-bound -- 27 % of its wave
+// cycles issue, 21 % wait for an issue slot, at 5 waves per SIMD -- so the
+// pair (127 VGPRs, 4 waves) gains nothing there; what did gain was fewer
+// instructions: R as per-lane vector loads instead of 16 uniform words (they
+// sat in SGPRs beside the ~100 of kernel arguments and spilled) and the
+// lookup's first-clear-slot search in spread form (12.24 -> 10.90 ms for
+// 10M warm reads; the three batched kernels take 9.70).
 template <int D, bool MSK>
-__global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
-    constexpr uint64_t FULL = (1ull << D) - 1ull;
-    constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
-    constexpr int V = DCP;                                          // op slots per lane
-    constexpr int SPR = AGN_WAVE / DCP;                             // cache slots per register
-    constexpr int NR = (int)((NSLOT + SPR - 1) / SPR);
-    __shared__ uint64_t stage[DCP][AGN_WAVE];
-    const uint64_t i = blockIdx.x;
-    if (i >= a.n_req) return;
+struct R6Req {
+    static constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
+    static constexpr int SPR = AGN_WAVE / DCP;                             // cache slots per register
+    static constexpr int NR = (int)((NSLOT + SPR - 1) / SPR);
+    uint64_t i, key, off, n, kmw, rmw, txv;
+    uint32_t n0, nv, id0, kty;
+    uint64_t r[D < 8 ? D : 1];  // D < 8: R as uniform words (the row-per-lane scan's compare)
+    uint64_t rd;                // per lane: R at this lane's DC (the lookup's compare)
+    u64x2 rq;                   // D = 8, per lane: R at DCs 2p, 2p+1 (p = lane & 3)
+    uint64_t clk[NR], cmk[NR];  // the key's cache slots (lane = slot x DC)
+    int64_t lop, val;           // slot lane: its last op and value
+    Q8Chunk ch0;                // D = 8: the log's first 64-op chunk
+};
+
+template <int D, bool MSK>
+__device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, const agn_ss_cache &c,
+                                        const Read6Args &a) {
     const int lane = lane_id();
-    const int dl = lane % DCP, jl = lane / DCP;  // this lane's DC and slot
-    const uint64_t key = uniform_u64(a.keys[i]);
-    const uint32_t S = c.slots;
-    const uint32_t n0 = __builtin_amdgcn_readfirstlane(c.n[key]);
-    uint64_t r[D];
+    const int dl = lane % R6Req<D, MSK>::DCP;
+    const uint64_t i = q.i, key = q.key;
+    q.n0 = __builtin_amdgcn_readfirstlane(c.n[key]);
+    if constexpr (D < 8) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) r[j] = uniform_u64(a.R[i * D + j]);
+        for (int j = 0; j < D; ++j) q.r[j] = uniform_u64(a.R[i * D + j]);
+    }
+    q.rd = a.R[i * D + (uint64_t)(dl < D ? dl : D - 1)];
+    if constexpr (D == 8) q.rq = *reinterpret_cast<const u64x2 *>(a.R + i * D + 2u * (lane & 3));
     // MSK: the key's DC set and R's, with the metadata (unconditional, from a
     // dummy word when absent: a conditional scalar load waits on its own)
-    uint64_t kmw = 0, rmw = 0;
+    q.kmw = q.rmw = 0ull;
     if constexpr (MSK) {
-        kmw = uniform_u64(*(a.key_mask ? a.key_mask + key : a.R));
-        rmw = uniform_u64(*(a.R_mask ? a.R_mask + i : a.R));
+        q.kmw = uniform_u64(*(a.key_mask ? a.key_mask + key : a.R));
+        q.rmw = uniform_u64(*(a.R_mask ? a.R_mask + i : a.R));
     }
-    const uint64_t Rm = (MSK && a.R_mask) ? (rmw & FULL) : FULL;
     const KeyMeta km = key_meta(key, a.key_off, a.key_len, a.key_id0);
-    const uint64_t off = km.off, n = km.n;
-    // erlang:error(corrupted_ops_cache) (:190-191), read before any store
-    // (unconditional, from a dummy address when there is no type column: a
-    // conditional scalar load is waited for before the slot loads issue)
-    const uint32_t kty = byte_of(
-        a.key_type ? a.key_type : reinterpret_cast<const uint8_t *>(a.key_off), key);
-    const bool corrupt = n != 0 && a.key_type != nullptr && kty != (a.req_type & 0xffu);
-    const uint32_t nv = n0 < NSLOT ? n0 : NSLOT;
+    q.off = km.off;
+    q.n = km.n;
+    q.id0 = km.id0;
+    // key_type (corrupted_ops_cache, read before any store) and the TxId:
+    // unconditional, from dummy addresses when absent
+    q.kty = byte_of(a.key_type ? a.key_type : reinterpret_cast<const uint8_t *>(a.key_off), key);
+    q.txv = uniform_u64((a.txid ? a.txid : a.R)[i]);
+}
 
+template <int D, bool MSK>
+__device__ __forceinline__ void r6_rows(R6Req<D, MSK> &q, const agn_ss_cache &c,
+                                        const Read6Args &a) {
+    using Q = R6Req<D, MSK>;
+    constexpr uint64_t FULL = (1ull << D) - 1ull;
+    const int lane = lane_id();
+    const int dl = lane % Q::DCP, jl = lane / Q::DCP;
+    const uint64_t key = q.key;
+    const uint32_t S = c.slots;
+    const uint32_t nv = q.n0 < NSLOT ? q.n0 : NSLOT;
+    q.nv = nv;
     // the key's cache slots (rows past nv re-read slot 0: same lines, unused)
     const int dc = dl < D ? dl : D - 1;
-    uint64_t clk[NR];
 #pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        const uint32_t j = (uint32_t)(jl + q * SPR);
-        clk[q] = c.clock[(key * S + (j < nv ? j : 0u)) * D + (uint64_t)dc];
+    for (int r = 0; r < Q::NR; ++r) {
+        const uint32_t j = (uint32_t)(jl + r * Q::SPR);
+        q.clk[r] = c.clock[(key * S + (j < nv ? j : 0u)) * D + (uint64_t)dc];
     }
     // MSK: each slot's DC set (one word per slot; the slot's lanes share it)
-    uint64_t cmk[NR];
 #pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        const uint32_t j = (uint32_t)(jl + q * SPR);
-        cmk[q] = (MSK && c.clock_mask) ? (c.clock_mask[key * S + (j < nv ? j : 0u)] & FULL) : FULL;
+    for (int r = 0; r < Q::NR; ++r) {
+        const uint32_t j = (uint32_t)(jl + r * Q::SPR);
+        q.cmk[r] = (MSK && c.clock_mask) ? (c.clock_mask[key * S + (j < nv ? j : 0u)] & FULL) : FULL;
     }
     const uint32_t ls = (uint32_t)lane < nv ? (uint32_t)lane : 0u;
-    int64_t lop = c.last_op[key * S + ls], val = c.value[key * S + ls];
+    q.lop = c.last_op[key * S + ls];
+    q.val = c.value[key * S + ls];
     // D = 8: the log's first chunk is in flight with the slots.  Unconditional
     // (an empty key reads its own slot 0 instead): a load under a branch makes
     // the wait for the slots at the join wait for the chunk too.
-    Q8Chunk ch0;
     if constexpr (D == 8) {
-        const bool has = n != 0;
-        ch0 = q8_load<true, false>(has ? a.oc : c.clock + key * S * D,
-                                   has ? a.eff : c.value + key * S, has ? off : 0ull, 0,
-                                   has ? a.n_entries : 1ull);
+        const bool has = q.n != 0;
+        q.ch0 = q8_load<true, false>(has ? a.oc : c.clock + key * S * D,
+                                     has ? a.eff : c.value + key * S, has ? q.off : 0ull, 0,
+                                     has ? a.n_entries : 1ull);
     }
+}
+
+template <int D, bool MSK>
+__device__ __forceinline__ void r6_serve(R6Req<D, MSK> &q, const agn_ss_cache &c,
+                                         const Read6Args &a,
+                                         uint64_t (&stage)[R6Req<D, MSK>::DCP][AGN_WAVE]) {
+    using Q = R6Req<D, MSK>;
+    constexpr uint64_t FULL = (1ull << D) - 1ull;
+    constexpr int DCP = Q::DCP, V = DCP, SPR = Q::SPR, NR = Q::NR;
+    const int lane = lane_id();
+    const int dl = lane % DCP, jl = lane / DCP;  // this lane's DC and slot
+    const uint64_t i = q.i, key = q.key, off = q.off, n = q.n;
+    const uint32_t S = c.slots, n0 = q.n0, nv = q.nv;
+    const uint64_t Rm = (MSK && a.R_mask) ? (q.rmw & FULL) : FULL;
+    const bool corrupt = n != 0 && a.key_type != nullptr && q.kty != (a.req_type & 0xffu);
 
     // 1. get_from_snapshot_cache: the first slot <= R (vector_orddict:get_smaller)
-    uint64_t rd = r[0];
-#pragma unroll
-    for (int j = 1; j < D; ++j) rd = dl == j ? r[j] : rd;
+    uint64_t rd = q.rd;
     if (MSK && !((Rm >> dl) & 1ull)) rd = 0ull;  // a DC missing from R reads 0
     uint32_t st, is_first;
     bool sct_ign;
     int64_t base = 0;
-    uint64_t s[D];
+    // SCT (the hit slot's clock): D < 8 as uniform words, D = 8 this lane's
+    // pair of DCs 2p, 2p+1
+    uint64_t s[D < 8 ? D : 1];
 #pragma unroll
-    for (int j = 0; j < D; ++j) s[j] = 0ull;
+    for (int j = 0; j < (D < 8 ? D : 1); ++j) s[j] = 0ull;
+    uint64_t sqA = 0ull, sqB = 0ull;
+    // slots of nv with no DC above R, per register in spread form (bit g
+    // DCP: slot r SPR + g) -- a first-zero-group search on five scalar
+    // operations where the packed fold took ~30; ahead of the branch below,
+    // so the wait for the slots is not also the wait for chunk 0's rows
+    uint64_t okz[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const bool pres = !MSK || ((q.cmk[r] >> dl) & 1ull) != 0ull;
+        const uint64_t gt = group_any_spread<DCP>(ballot(dl < D && pres && q.clk[r] > rd));
+        const uint32_t lo = (uint32_t)(r * SPR);
+        const uint32_t cv = nv > lo ? (nv - lo < (uint32_t)SPR ? nv - lo : (uint32_t)SPR) : 0u;
+        okz[r] = ~gt & group_base<DCP>() & low_bits((uint64_t)cv * DCP);
+    }
     uint64_t smw = FULL;  // SCT's DC set (the hit slot's)
     uint32_t n1 = nv;  // the key's entries after the lookup
     if (n0 == 0) {     // absent: store the empty snapshot at vectorclock:new() (:395-402)
@@ -137,36 +199,40 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             c.n[key] = 1;
             if (MSK && c.clock_mask) c.clock_mask[key * S] = 0ull;
         }
-        clk[0] = jl == 0 ? 0ull : clk[0];
-        if (MSK && c.clock_mask) cmk[0] = jl == 0 ? 0ull : cmk[0];
+        q.clk[0] = jl == 0 ? 0ull : q.clk[0];
+        if (MSK && c.clock_mask) q.cmk[0] = jl == 0 ? 0ull : q.cmk[0];
         smw = 0ull;
-        lop = lane == 0 ? 0 : lop;
-        val = lane == 0 ? 0 : val;
+        q.lop = lane == 0 ? 0 : q.lop;
+        q.val = lane == 0 ? 0 : q.val;
         n1 = 1;
         st = AGN_SS_NEW;
         is_first = 1;
         sct_ign = true;
     } else {
-        uint64_t ok = 0;  // bit j: slot j <= R
+        int f = -1;  // the first slot <= R
 #pragma unroll
-        for (int q = 0; q < NR; ++q) {
-            const bool pres = !MSK || ((cmk[q] >> dl) & 1ull) != 0ull;
-            const uint64_t gt = group_any<DCP>(ballot(dl < D && pres && clk[q] > rd));
-            ok |= (~gt & low_bits(SPR)) << (q * SPR);
-        }
-        ok &= low_bits(nv);
-        if (ok) {
-            const int f = __builtin_ctzll(ok), q = f / SPR, l0 = (f % SPR) * DCP;
+        for (int r = NR - 1; r >= 0; --r)
+            if (okz[r]) f = r * SPR + __builtin_ctzll(okz[r]) / DCP;
+        if (f >= 0) {
+            const int fr = f / SPR, l0 = (f % SPR) * DCP;
+            if constexpr (D == 8) {
+                const int p = lane & 3;
+                uint64_t v = q.clk[0];
+                if constexpr (NR > 1) v = fr ? q.clk[1] : v;
+                sqA = shfl_u64(v, l0 + 2 * p);
+                sqB = shfl_u64(v, l0 + 2 * p + 1);
+            } else {
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
-                uint64_t v = readlane_u64(clk[0], l0 + j);
-                if constexpr (NR > 1) v = q ? readlane_u64(clk[1], l0 + j) : v;
-                s[j] = v;
+                for (int j = 0; j < D; ++j) {
+                    uint64_t v = readlane_u64(q.clk[0], l0 + j);
+                    if constexpr (NR > 1) v = fr ? readlane_u64(q.clk[1], l0 + j) : v;
+                    s[j] = v;
+                }
             }
-            base = (int64_t)readlane_u64((uint64_t)val, f);
+            base = (int64_t)readlane_u64((uint64_t)q.val, f);
             if constexpr (MSK) {
-                uint64_t mw = readlane_u64(cmk[0], l0);
-                if constexpr (NR > 1) mw = q ? readlane_u64(cmk[1], l0) : mw;
+                uint64_t mw = readlane_u64(q.cmk[0], l0);
+                if constexpr (NR > 1) mw = fr ? readlane_u64(q.cmk[1], l0) : mw;
                 smw = mw;
             }
             st = AGN_SS_HIT;
@@ -180,7 +246,6 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     }
 
     // 2. materialize/4 from the base (k_counter_key's body)
-    uint64_t ct[D];
     if (corrupt) {
         if (lane == 0) {
             a.value[i] = 0;
@@ -202,36 +267,29 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     uint64_t U = FULL, Sm = FULL;
     bool uni = true;
     if constexpr (MSK) {
-        U = a.oc_mask ? (a.key_mask ? (kmw & FULL) : 0ull) : FULL;
+        U = a.oc_mask ? (a.key_mask ? (q.kmw & FULL) : 0ull) : FULL;
         Sm = smw & FULL;
         uni = n == 0 || (U != 0ull && (U & ~Rm) == 0ull);
     }
-    // e = SCT as a dict read (missing DC = 0), where LastOpCt starts
-    // (materialize/4 :94-95); rc / sc = the compare values: +inf outside U on
-    // the dense scan of a masked key
-    uint64_t e[D], rc[D], sc[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const bool inU = ((U >> j) & 1ull) != 0ull;
-        e[j] = (sct_ign || !((Sm >> j) & 1ull)) ? 0ull : s[j];
-        sc[j] = (MSK && uni && !inU) ? ~0ull : e[j];
-        rc[j] = (MSK && uni && !inU) ? ~0ull : r[j];
-        ct[j] = e[j];
-    }
-    const uint64_t txr = a.txid ? uniform_u64(a.txid[i]) : 0ull;
+    const uint64_t txr = a.txid ? q.txv : 0ull;
     const uint64_t *tx = (txr != 0ull) ? a.log_txid : nullptr;
     int64_t sum = 0, first_excl = -1, first_err = -1;
     uint32_t cnt = 0;
-    uint64_t um = 0;            // MSK, mixed key: DCs of the included ops (per lane)
+    uint64_t um = 0;  // MSK, mixed key: DCs of the included ops (per lane)
+    uint64_t ct[D < 8 ? D : 1];
     uint64_t ctA = 0, ctB = 0;  // D = 8: quad rows, LastOpCt of DCs 2p, 2p+1 (p = lane & 3)
     if constexpr (D == 8) {
+        // e = SCT as a dict read (missing DC = 0), where LastOpCt starts
+        // (materialize/4 :94-95); r / s = the compare values: +inf outside U
+        // on the dense scan of a masked key
         const int p = lane & 3;
-        const uint64_t rA = p == 0 ? rc[0] : p == 1 ? rc[2 % D] : p == 2 ? rc[4 % D] : rc[6 % D];
-        const uint64_t rB = p == 0 ? rc[1 % D] : p == 1 ? rc[3 % D] : p == 2 ? rc[5 % D] : rc[7 % D];
-        const uint64_t sA = p == 0 ? sc[0] : p == 1 ? sc[2 % D] : p == 2 ? sc[4 % D] : sc[6 % D];
-        const uint64_t sB = p == 0 ? sc[1 % D] : p == 1 ? sc[3 % D] : p == 2 ? sc[5 % D] : sc[7 % D];
-        const uint64_t eA = p == 0 ? e[0] : p == 1 ? e[2 % D] : p == 2 ? e[4 % D] : e[6 % D];
-        const uint64_t eB = p == 0 ? e[1 % D] : p == 1 ? e[3 % D] : p == 2 ? e[5 % D] : e[7 % D];
+        const bool inA = ((U >> (2 * p)) & 1ull) != 0ull, inB = ((U >> (2 * p + 1)) & 1ull) != 0ull;
+        const uint64_t eA = (sct_ign || !((Sm >> (2 * p)) & 1ull)) ? 0ull : sqA;
+        const uint64_t eB = (sct_ign || !((Sm >> (2 * p + 1)) & 1ull)) ? 0ull : sqB;
+        const uint64_t sA = (MSK && uni && !inA) ? ~0ull : eA;
+        const uint64_t sB = (MSK && uni && !inB) ? ~0ull : eB;
+        const uint64_t rA = (MSK && uni && !inA) ? ~0ull : q.rq.x;
+        const uint64_t rB = (MSK && uni && !inB) ? ~0ull : q.rq.y;
         ctA = eA;
         ctB = eB;
         if (n != 0 && MSK && !uni) {
@@ -245,7 +303,7 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
                                       sA, sB, Rm, ctA, ctB, um, sum, cnt, first_excl, first_err);
         } else if (n != 0) {
 #define AGN_R6Q(W)                                                                             \
-    q8_fold<W>(ch0, tx, txr, off, 0, n, a.n_entries, rA, rB, sA, sB, ctA, ctB, sum, cnt,       \
+    q8_fold<W>(q.ch0, tx, txr, off, 0, n, a.n_entries, rA, rB, sA, sB, ctA, ctB, sum, cnt,     \
                first_excl, first_err);                                                         \
     scan_key_q8<W, true, false, true>(a.oc, a.eff, tx, txr, off, n, a.n_entries, rA, rB, sA, sB, \
                                       ctA, ctB, sum, cnt, first_excl, first_err)
@@ -256,11 +314,20 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
             }
 #undef AGN_R6Q
             if (MSK) {  // outside U: SCT's value (an op's row there is not in its dict)
-                ctA = ((U >> (2 * p)) & 1ull) ? ctA : eA;
-                ctB = ((U >> (2 * p + 1)) & 1ull) ? ctB : eB;
+                ctA = inA ? ctA : eA;
+                ctB = inB ? ctB : eB;
             }
         }
     } else {
+        uint64_t e[D], rc[D], sc[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const bool inU = ((U >> j) & 1ull) != 0ull;
+            e[j] = (sct_ign || !((Sm >> j) & 1ull)) ? 0ull : s[j];
+            sc[j] = (MSK && uni && !inU) ? ~0ull : e[j];
+            rc[j] = (MSK && uni && !inU) ? ~0ull : q.r[j];
+            ct[j] = e[j];
+        }
         if (MSK && !uni) {
             if (sct_ign)
                 scan_key_msk<D, false>(a.oc, a.oc_mask, a.eff, tx, txr, off, n, rc, sc, Rm, ct, um,
@@ -284,8 +351,8 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     int64_t hid;
     {
         const uint64_t pos = first_excl >= 0 ? (uint64_t)first_excl : n - 1;
-        if (km.id0 != AGN_ID0_NONE)  // op_id[off + pos] == id0 + pos (agn_log_index_ids)
-            hid = n ? (int64_t)((uint64_t)km.id0 + pos) : 0;
+        if (q.id0 != AGN_ID0_NONE)  // op_id[off + pos] == id0 + pos (agn_log_index_ids)
+            hid = n ? (int64_t)((uint64_t)q.id0 + pos) : 0;
         else
             hid = n ? (int64_t)a.op_id[uniform_u64(off + pos)] : 0;
     }
@@ -319,6 +386,7 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
 #pragma unroll
             for (int v = 0; v < V; ++v) m = umax64(m, stage[dl][jl * V + v]);
         }
+        __syncthreads();  // NP = 2: the next request writes stage
 #pragma unroll
         for (int x = DCP; x < AGN_WAVE; x <<= 1) m = umax64(m, shfl_xor_u64(m, x));
         ctl = ct_ign ? 0ull : m;
@@ -344,13 +412,13 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
     const bool gc = a.gc != nullptr && a.gc[i] != 0;
     bool pr = false;
     const bool refresh = (fl & AGN_F_NEWSS) && is_first && cnt >= AGN_MIN_OP_STORE_SS;
-    const int64_t lop0 = (int64_t)readlane_u64((uint64_t)lop, 0);
+    const int64_t lop0 = (int64_t)readlane_u64((uint64_t)q.lop, 0);
     if (st != AGN_SS_LOG && n != 0 && !(fl & (AGN_F_ERR_UNEXPECTED | AGN_F_CT_IGNORE)) &&
         (refresh || gc) && (hole - lop0 >= AGN_MIN_OP_STORE_SS || gc)) {
         // insert_bigger: prepend iff not le(LastOpCt, head clock) (dicts: DCs
         // of LastOpCt only, the head's missing ones read 0)
         const bool inct = !MSK || ((mo >> dl) & 1ull) != 0ull;
-        const uint64_t hv = (!MSK || ((cmk[0] >> dl) & 1ull)) ? clk[0] : 0ull;
+        const uint64_t hv = (!MSK || ((q.cmk[0] >> dl) & 1ull)) ? q.clk[0] : 0ull;
         const bool prepend = (ballot(jl == 0 && dl < D && inct && ctl > hv) & low_bits(DCP)) != 0ull;
         const uint32_t size1 = n1 + (prepend ? 1u : 0u);
         const bool collect = size1 >= AGN_SNAPSHOT_THRESHOLD || gc;
@@ -360,20 +428,20 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         const uint32_t new_n = kept + (prepend ? 1u : 0u);
         uint64_t m = ~0ull, pm = 0ull;  // CommitTime: min (missing = 0), its DC set
 #pragma unroll
-        for (int q = 0; q < NR; ++q) {
-            const uint32_t j = (uint32_t)(jl + q * SPR);
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t j = (uint32_t)(jl + r * SPR);
             if (j < kept) {
-                if (prepend && dl < D) c.clock[(key * S + j + 1) * D + (uint64_t)dl] = clk[q];
-                if (MSK && c.clock_mask && prepend && dl == 0) c.clock_mask[key * S + j + 1] = cmk[q];
-                const uint64_t v = (!MSK || ((cmk[q] >> dl) & 1ull)) ? clk[q] : 0ull;
+                if (prepend && dl < D) c.clock[(key * S + j + 1) * D + (uint64_t)dl] = q.clk[r];
+                if (MSK && c.clock_mask && prepend && dl == 0) c.clock_mask[key * S + j + 1] = q.cmk[r];
+                const uint64_t v = (!MSK || ((q.cmk[r] >> dl) & 1ull)) ? q.clk[r] : 0ull;
                 m = v < m ? v : m;
-                pm |= cmk[q];
+                pm |= q.cmk[r];
             }
         }
         if (prepend) {
             if ((uint32_t)lane < kept) {
-                c.last_op[key * S + (uint64_t)lane + 1] = lop;
-                c.value[key * S + (uint64_t)lane + 1] = val;
+                c.last_op[key * S + (uint64_t)lane + 1] = q.lop;
+                c.value[key * S + (uint64_t)lane + 1] = q.val;
             }
             if (jl == 0 && dl < D) c.clock[(key * S) * D + (uint64_t)dl] = ctl;
             if (lane == 0) {
@@ -412,6 +480,29 @@ __global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a) {
         if (a.dkeys) a.dkeys[i] = key;
         if (a.dprune) a.dprune[i] = pr ? 1 : 0;
     }
+}
+
+template <int D, bool MSK, int NP>
+__global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a, uint32_t xcd) {
+    using Q = R6Req<D, MSK>;
+    __shared__ uint64_t stage[Q::DCP][AGN_WAVE];
+    const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t i0 = (uint64_t)blk * NP;
+    if (i0 >= a.n_req) return;
+    Q q[NP];
+    // a missing second request (odd batch) re-reads the first's and is not served
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        q[p].i = i0 + (uint64_t)p < a.n_req ? i0 + (uint64_t)p : i0;
+        q[p].key = uniform_u64(a.keys[q[p].i]);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) r6_meta(q[p], c, a);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) r6_rows(q[p], c, a);
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+        if (p == 0 || i0 + (uint64_t)p < a.n_req) r6_serve(q[p], c, a, stage);
 }
 
 // read/6 for clocks of 9 .. 64 DCs (D > 8 has no register-resident dense
@@ -550,14 +641,32 @@ bool read6_supported(const agn_log &view, uint32_t D) {
     return view.crdt_type == AGN_COUNTER_PN && view.oc_mask == nullptr && D >= 1 && D <= 8;
 }
 
+// Requests per wave of k_read6: AGN_READ6_NP=1 / 2, else 2 for D < 8 from
+// kRead6PairFrom requests (a batch that fills the chip several times over;
+// a serving batch of a few requests keeps one per wave, its latency): 1M
+// reads at D = 3 0.94 vs 0.97 ms; at D = 8 (quad rows, 127 VGPRs paired)
+// 11.17 vs 10.90 ms for 10M (profiles/r05/ab_read6_*).  AGN_READ6_XCD=1:
+// the XCD-aware block order (xcd_block; 11.59 vs 11.47 ms at 10M, off).
+constexpr uint64_t kRead6PairFrom = 1u << 14;
+
 int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     if (a.n_req == 0) return AGN_OK;
     if (a.n_req > 0x7fffffffull) return fail(AGN_ENOTSUP, "read6: batch too large");
     const dim3 grid((unsigned)a.n_req), block(AGN_WAVE);
     const bool msk = a.oc_mask || a.R_mask || c.clock_mask;
+    const char *npv = AGN_KNOB("AGN_READ6_NP");
+    const bool pair = npv && npv[0] ? npv[0] == '2' : (a.n_dcs < 8 && a.n_req >= kRead6PairFrom);
+    const char *xv = AGN_KNOB("AGN_READ6_XCD");
+    const uint32_t xcd = (xv && xv[0] == '1') ? 1u : 0u;
+    const dim3 grid2((unsigned)((a.n_req + 1) / 2));
 #define AGN_R6(DV)                                                                             \
-    if (msk) hipLaunchKernelGGL((k_read6<DV, true>), grid, block, 0, st, c, a);                \
-    else hipLaunchKernelGGL((k_read6<DV, false>), grid, block, 0, st, c, a);                   \
+    if (pair) {                                                                                \
+        if (msk) hipLaunchKernelGGL((k_read6<DV, true, 2>), grid2, block, 0, st, c, a, xcd);    \
+        else hipLaunchKernelGGL((k_read6<DV, false, 2>), grid2, block, 0, st, c, a, xcd);       \
+    } else {                                                                                   \
+        if (msk) hipLaunchKernelGGL((k_read6<DV, true, 1>), grid, block, 0, st, c, a, xcd);     \
+        else hipLaunchKernelGGL((k_read6<DV, false, 1>), grid, block, 0, st, c, a, xcd);        \
+    }                                                                                          \
     break
 #define AGN_R6W(DPL, LPO)                                                                      \
     if (msk) hipLaunchKernelGGL((k_read6w<DPL, LPO, true>), grid, block, 0, st, c, a);          \

@@ -276,18 +276,22 @@ def test_cache_gpu_vs_oracle(eng, oracle_lib, D, sparse, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("split", ["0", "1"], ids=["fused", "batched"])
+@pytest.mark.parametrize("split,np_", [("0", "1"), ("0", "2"), ("1", "")],
+                         ids=["fused", "fused_pair", "batched"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
-def test_read_cached_vs_sequence(eng, monkeypatch, D, split):
+def test_read_cached_vs_sequence(eng, monkeypatch, D, split, np_):
     """agn_read_cached (read/6 in one kernel: lookup -> materialize from the
     cached base -> store policy) equals agn_ss_lookup -> agn_materialize ->
     agn_ss_store on two caches that start empty: every result field, the
     lookup status, the prune flags (per request vs per key), the GC
     thresholds and the cache contents, over rounds of batches on distinct
     keys with GC reads mixed in (cold reads, hits, stores, prunes).  split =
-    "0": the fused kernel; "1": agn_read_cached's bulk form (the batched
-    kernels with per-request prune flags, AGN_READ_CACHED_SPLIT=1)."""
+    "0": the fused kernel, one request per wave or two (AGN_READ6_NP; the
+    odd batch sizes leave the last wave one request); "1": agn_read_cached's
+    bulk form (the batched kernels with per-request prune flags,
+    AGN_READ_CACHED_SPLIT=1)."""
     monkeypatch.setenv("AGN_READ_CACHED_SPLIT", split)
+    monkeypatch.setenv("AGN_READ6_NP", np_)
     K = 3000
     log, req, _ = random_case(501 + D, _abi.COUNTER_PN, K, D, 90, txid=0.2, empty=0.05)
     rng = np.random.default_rng(D)
@@ -307,7 +311,7 @@ def test_read_cached_vs_sequence(eng, monkeypatch, D, split):
     ca, ba = cache()
     cb, bb = cache()
     for rnd in range(4):
-        nr = 1500 + 300 * rnd
+        nr = 1501 + 300 * rnd
         keys = rng.permutation(K)[:nr].astype(np.uint64)
         R = req.R[keys.astype(np.int64)] + rng.integers(0, 3, (nr, D)).astype(np.uint64)
         tx = req.txid[keys.astype(np.int64)].copy()
