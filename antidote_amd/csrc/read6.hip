@@ -82,9 +82,10 @@ struct R6Req {
     Q8Chunk ch0;                // D = 8: the log's first 64-op chunk
 };
 
-template <int D, bool MSK>
-__device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, const agn_ss_cache &c,
-                                        const Read6Args &a) {
+template <int D, bool MSK, class KA>
+__device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, KA &k) {
+    const auto &c = k.c;
+    const auto &a = k.a;
     const int lane = lane_id();
     const int dl = lane % R6Req<D, MSK>::DCP;
     const uint64_t i = q.i, key = q.key;
@@ -112,9 +113,10 @@ __device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, const agn_ss_cache &c,
     q.txv = uniform_u64((a.txid ? a.txid : a.R)[i]);
 }
 
-template <int D, bool MSK>
-__device__ __forceinline__ void r6_rows(R6Req<D, MSK> &q, const agn_ss_cache &c,
-                                        const Read6Args &a) {
+template <int D, bool MSK, class KA>
+__device__ __forceinline__ void r6_rows(R6Req<D, MSK> &q, KA &k) {
+    const auto &c = k.c;
+    const auto &a = k.a;
     using Q = R6Req<D, MSK>;
     constexpr uint64_t FULL = (1ull << D) - 1ull;
     const int lane = lane_id();
@@ -150,10 +152,11 @@ __device__ __forceinline__ void r6_rows(R6Req<D, MSK> &q, const agn_ss_cache &c,
     }
 }
 
-template <int D, bool MSK>
-__device__ __forceinline__ void r6_serve(R6Req<D, MSK> &q, const agn_ss_cache &c,
-                                         const Read6Args &a,
+template <int D, bool MSK, class KA>
+__device__ __forceinline__ void r6_serve(R6Req<D, MSK> &q, KA &k,
                                          uint64_t (&stage)[R6Req<D, MSK>::DCP][AGN_WAVE]) {
+    const auto &c = k.c;
+    const auto &a = k.a;
     using Q = R6Req<D, MSK>;
     constexpr uint64_t FULL = (1ull << D) - 1ull;
     constexpr int DCP = Q::DCP, V = DCP, SPR = Q::SPR, NR = Q::NR;
@@ -482,27 +485,51 @@ __device__ __forceinline__ void r6_serve(R6Req<D, MSK> &q, const agn_ss_cache &c
     }
 }
 
+// The kernel's parameters (~400 bytes) are read through the kernarg segment
+// pointer at each stage (kp(): an opaque copy, so a stage's loads are
+// neither hoisted to the kernel's entry nor shared with another stage's):
+// as by-value arguments they were all loaded at the entry and held in SGPRs
+// for the whole kernel, which spilled 34 of them to VGPR lanes (now 0; 84
+// VGPRs instead of 89).  Measured: 10.88 vs 10.90 ms for 10M warm reads, no
+// change -- the D = 8 gap to the batched kernels (9.66 ms) is in the memory
+// side, not issue: the fused kernel fetches 8.7 % and writes 43 % more than
+// the three kernels together (one request's 1-8 byte outputs per wave, on
+// a different L2 from its neighbours'; profiles/r05/ab_read6_*).
+struct R6Params {
+    agn_ss_cache c;
+    Read6Args a;
+    uint32_t xcd;
+};
+using R6K = const __attribute__((address_space(4))) R6Params;
+__device__ __forceinline__ R6K &kp() {
+    R6K *p = (R6K *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 template <int D, bool MSK, int NP>
-__global__ __launch_bounds__(64) void k_read6(agn_ss_cache c, Read6Args a, uint32_t xcd) {
+__global__ __launch_bounds__(64) void k_read6(R6Params) {
     using Q = R6Req<D, MSK>;
     __shared__ uint64_t stage[Q::DCP][AGN_WAVE];
-    const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    R6K &k0 = kp();
+    const uint32_t blk = k0.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint64_t n_req = k0.a.n_req;
     const uint64_t i0 = (uint64_t)blk * NP;
-    if (i0 >= a.n_req) return;
+    if (i0 >= n_req) return;
     Q q[NP];
     // a missing second request (odd batch) re-reads the first's and is not served
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-        q[p].i = i0 + (uint64_t)p < a.n_req ? i0 + (uint64_t)p : i0;
-        q[p].key = uniform_u64(a.keys[q[p].i]);
+        q[p].i = i0 + (uint64_t)p < n_req ? i0 + (uint64_t)p : i0;
+        q[p].key = uniform_u64(k0.a.keys[q[p].i]);
     }
 #pragma unroll
-    for (int p = 0; p < NP; ++p) r6_meta(q[p], c, a);
+    for (int p = 0; p < NP; ++p) r6_meta(q[p], kp());
 #pragma unroll
-    for (int p = 0; p < NP; ++p) r6_rows(q[p], c, a);
+    for (int p = 0; p < NP; ++p) r6_rows(q[p], kp());
 #pragma unroll
     for (int p = 0; p < NP; ++p)
-        if (p == 0 || i0 + (uint64_t)p < a.n_req) r6_serve(q[p], c, a, stage);
+        if (p == 0 || i0 + (uint64_t)p < n_req) r6_serve(q[p], kp(), stage);
 }
 
 // read/6 for clocks of 9 .. 64 DCs (D > 8 has no register-resident dense
@@ -659,13 +686,14 @@ int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     const char *xv = AGN_KNOB("AGN_READ6_XCD");
     const uint32_t xcd = (xv && xv[0] == '1') ? 1u : 0u;
     const dim3 grid2((unsigned)((a.n_req + 1) / 2));
+    const R6Params prm{c, a, xcd};
 #define AGN_R6(DV)                                                                             \
     if (pair) {                                                                                \
-        if (msk) hipLaunchKernelGGL((k_read6<DV, true, 2>), grid2, block, 0, st, c, a, xcd);    \
-        else hipLaunchKernelGGL((k_read6<DV, false, 2>), grid2, block, 0, st, c, a, xcd);       \
+        if (msk) hipLaunchKernelGGL((k_read6<DV, true, 2>), grid2, block, 0, st, prm);          \
+        else hipLaunchKernelGGL((k_read6<DV, false, 2>), grid2, block, 0, st, prm);             \
     } else {                                                                                   \
-        if (msk) hipLaunchKernelGGL((k_read6<DV, true, 1>), grid, block, 0, st, c, a, xcd);     \
-        else hipLaunchKernelGGL((k_read6<DV, false, 1>), grid, block, 0, st, c, a, xcd);        \
+        if (msk) hipLaunchKernelGGL((k_read6<DV, true, 1>), grid, block, 0, st, prm);           \
+        else hipLaunchKernelGGL((k_read6<DV, false, 1>), grid, block, 0, st, prm);              \
     }                                                                                          \
     break
 #define AGN_R6W(DPL, LPO)                                                                      \
