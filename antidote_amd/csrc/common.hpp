@@ -168,6 +168,21 @@ __device__ __forceinline__ uint32_t ldc_byte(const uint8_t *p, uint64_t idx) {
     return (__builtin_amdgcn_readfirstlane(w) >> ((uint32_t)(idx & 3u) * 8u)) & 0xffu;
 }
 
+// A kernel's by-value parameter block T (its only parameter), read through
+// the kernarg segment pointer.  Each call returns an opaque copy of the
+// pointer, so the loads of a field are issued where it is used and are not
+// shared with another call's: passed and used as ordinary arguments, every
+// field a kernel touches is loaded at its entry and held in SGPRs to the
+// end, and the ~100 dwords of this engine's argument structs spill the rest
+// of the kernel's scalar state to VGPR lanes (read6.hip, k_counter_q8e2).
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T &kparams() {
+    using P = const __attribute__((address_space(4))) T;
+    P *p = (P *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 // Scalar (wave-uniform) value: lets hipcc keep it in an SGPR.
 __device__ inline uint64_t uniform_u64(uint64_t v) {
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);

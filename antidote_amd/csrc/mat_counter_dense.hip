@@ -883,19 +883,38 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
 // side loads (R, SCT, the DC sets) under the chunks.  Mixed keys are handed
 // on to k_counter_q8m as in q8e.  (Round 3's two-request masked form carried
 // the per-entry-mask scan inline: 118 VGPRs, slower than one request.)
+// k_counter_q8e2's parameters as one block (kparams: each stage reads the
+// fields it uses; as 26 separate arguments the kernel spilled 66 SGPRs).
+struct Q8e2Params {
+    DenseArgs a;
+    MaskArgs mk;
+    const uint64_t *keys, *key_off, *key_len;
+    const uint8_t *key_type;
+    const uint32_t *key_id0;
+    const uint64_t *oc;
+    const uint32_t *op_id;
+    const int64_t *eff;
+    const uint64_t *log_txid, *R, *sct;
+    const uint8_t *sct_ignore;
+    const uint64_t *req_txid;
+    const int64_t *base_value;
+    int64_t *o_value, *o_hole;
+    uint64_t *o_lastct;
+    uint32_t *o_count, *o_flags, *o_err, *list, *list_n;
+};
+
+template <class T>
+__device__ __forceinline__ DenseArgs dense_of(const T &x) {
+    return DenseArgs{x.n_req, x.n_entries, x.req_type, x.xcd, x.pair, x.qnt, x.hints, x.ql_cap};
+}
+template <class T>
+__device__ __forceinline__ MaskArgs mask_of(const T &x) {
+    return MaskArgs{x.key_mask, x.oc_mask, x.R_mask, x.sct_mask, x.o_mask};
+}
+
 template <bool KEYS>
-__global__ __launch_bounds__(64) void k_counter_q8e2(
-    DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
-    const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
-    const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,
-    const uint64_t *__restrict__ oc, const uint32_t *__restrict__ op_id,
-    const int64_t *__restrict__ eff, const uint64_t *__restrict__ log_txid,
-    const uint64_t *__restrict__ R, const uint64_t *__restrict__ sct,
-    const uint8_t *__restrict__ sct_ignore, const uint64_t *__restrict__ req_txid,
-    const int64_t *__restrict__ base_value, int64_t *__restrict__ o_value,
-    int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
-    uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
-    uint32_t *__restrict__ o_err, uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
+__global__ __launch_bounds__(64) void k_counter_q8e2(Q8e2Params) {
+    const DenseArgs a = dense_of(kparams<Q8e2Params>().a);
     const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t blk = a.xcd ? xb : blockIdx.x;
     const uint64_t i0 = uniform_u64((uint64_t)blk * 2u);
@@ -903,25 +922,34 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(
     const bool two = i0 + 1u < a.n_req;
     const uint64_t i1 = two ? i0 + 1u : i0;
     Q2Key k0, k1;
-    q2_meta(k0, i0, KEYS ? keys : nullptr, key_off, key_len, key_id0);
-    q2_meta(k1, i1, KEYS ? keys : nullptr, key_off, key_len, key_id0);
+    {
+        const auto &p = kparams<Q8e2Params>();
+        q2_meta(k0, i0, KEYS ? p.keys : nullptr, p.key_off, p.key_len, p.key_id0);
+        q2_meta(k1, i1, KEYS ? p.keys : nullptr, p.key_off, p.key_len, p.key_id0);
+    }
     const bool any = a.n_entries != 0;
     Q8Chunk c0{}, c1{};
     if (any) {
-        c0 = q8_load<true, false>(oc, eff, k0.off, 0, a.n_entries);
-        c1 = q8_load<true, false>(oc, eff, k1.off, 0, a.n_entries);
+        const auto &p = kparams<Q8e2Params>();
+        c0 = q8_load<true, false>(p.oc, p.eff, k0.off, 0, a.n_entries);
+        c1 = q8_load<true, false>(p.oc, p.eff, k1.off, 0, a.n_entries);
     }
     __builtin_amdgcn_sched_barrier(0);
-    const uint64_t kmw0 = key_word(mk, k0.key, key_off), kmw1 = key_word(mk, k1.key, key_off);
-    q2_side<true, true>(k0, a, mk, kmw0, key_off, key_type, R, sct, sct_ignore, req_txid);
-    q2_side<true, true>(k1, a, mk, kmw1, key_off, key_type, R, sct, sct_ignore, req_txid);
+    const auto &ps = kparams<Q8e2Params>();
+    const MaskArgs mk = mask_of(ps.mk);
+    const uint64_t kmw0 = key_word(mk, k0.key, ps.key_off), kmw1 = key_word(mk, k1.key, ps.key_off);
+    q2_side<true, true>(k0, a, mk, kmw0, ps.key_off, ps.key_type, ps.R, ps.sct, ps.sct_ignore,
+                        ps.req_txid);
+    q2_side<true, true>(k1, a, mk, kmw1, ps.key_off, ps.key_type, ps.R, ps.sct, ps.sct_ignore,
+                        ps.req_txid);
     auto mixed = [&](const Q2Key &k, uint64_t kmw) {
         return !(mk.oc_mask == nullptr || (mk.key_mask && (kmw & 0xFFull)) || k.n == 0);
     };
     auto hand_on = [&](uint64_t i) {  // q8e's sub-lists
         if (lane_id() == 0) {
+            const auto &p = kparams<Q8e2Params>();
             const uint32_t sl = (uint32_t)(i % QL_S);
-            list[(uint64_t)sl * a.ql_cap + atomicAdd(list_n + sl * QL_STRIDE, 1u)] = (uint32_t)i;
+            p.list[(uint64_t)sl * a.ql_cap + atomicAdd(p.list_n + sl * QL_STRIDE, 1u)] = (uint32_t)i;
         }
     };
     const bool m0 = mixed(k0, kmw0), m1 = two && mixed(k1, kmw1);
@@ -933,16 +961,20 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(
     s1.ctA = k1.eA;
     s1.ctB = k1.eB;
     const bool d0 = any && !k0.corrupt && !m0, d1 = two && any && !k1.corrupt && !m1;
-    if (d0) q2_fold<true>(k0, c0, 0, log_txid, a.n_entries, s0);
-    if (d1) q2_fold<true>(k1, c1, 0, log_txid, a.n_entries, s1);
-    if (d0) q2_rest<true>(k0, oc, eff, log_txid, a.n_entries, s0);
-    if (d1) q2_rest<true>(k1, oc, eff, log_txid, a.n_entries, s1);
+    {
+        const auto &p = kparams<Q8e2Params>();
+        if (d0) q2_fold<true>(k0, c0, 0, p.log_txid, a.n_entries, s0);
+        if (d1) q2_fold<true>(k1, c1, 0, p.log_txid, a.n_entries, s1);
+        if (d0) q2_rest<true>(k0, p.oc, p.eff, p.log_txid, a.n_entries, s0);
+        if (d1) q2_rest<true>(k1, p.oc, p.eff, p.log_txid, a.n_entries, s1);
+    }
+    const auto &pe = kparams<Q8e2Params>();
     if (!m0)
-        q2_epilogue<true>(k0, s0, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count,
-                          o_flags, o_err, mk.o_mask);
+        q2_epilogue<true>(k0, s0, a.hints, pe.op_id, pe.base_value, pe.o_value, pe.o_hole,
+                          pe.o_lastct, pe.o_count, pe.o_flags, pe.o_err, pe.mk.o_mask);
     if (two && !m1)
-        q2_epilogue<true>(k1, s1, a.hints, op_id, base_value, o_value, o_hole, o_lastct, o_count,
-                          o_flags, o_err, mk.o_mask);
+        q2_epilogue<true>(k1, s1, a.hints, pe.op_id, pe.base_value, pe.o_value, pe.o_hole,
+                          pe.o_lastct, pe.o_count, pe.o_flags, pe.o_err, pe.mk.o_mask);
 }
 
 // The keys k_counter_q8e handed on (entries with different DC sets): the
@@ -1074,7 +1106,7 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     const bool two = tv && tv[0] == '1';
     const unsigned nb2 = (unsigned)((req.n_req + 1) / 2);
 #define AGN_Q8E2(K)                                                                             \
-    hipLaunchKernelGGL((k_counter_q8e2<K>), dim3(nb2), dim3(64), 0, st, AGN_ARGS)
+    hipLaunchKernelGGL((k_counter_q8e2<K>), dim3(nb2), dim3(64), 0, st, Q8e2Params{AGN_ARGS})
     if (rc == AGN_OK) {
         if (req.sct && two) {
             if (req.keys) { AGN_Q8E2(true); AGN_Q8M(true, true); }

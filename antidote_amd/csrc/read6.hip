@@ -501,11 +501,7 @@ struct R6Params {
     uint32_t xcd;
 };
 using R6K = const __attribute__((address_space(4))) R6Params;
-__device__ __forceinline__ R6K &kp() {
-    R6K *p = (R6K *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *p;
-}
+__device__ __forceinline__ R6K &kp() { return kparams<R6Params>(); }
 
 template <int D, bool MSK, int NP>
 __global__ __launch_bounds__(64) void k_read6(R6Params) {
@@ -668,21 +664,18 @@ bool read6_supported(const agn_log &view, uint32_t D) {
     return view.crdt_type == AGN_COUNTER_PN && view.oc_mask == nullptr && D >= 1 && D <= 8;
 }
 
-// Requests per wave of k_read6: AGN_READ6_NP=1 / 2, else 2 for D < 8 from
-// kRead6PairFrom requests (a batch that fills the chip several times over;
-// a serving batch of a few requests keeps one per wave, its latency): 1M
-// reads at D = 3 0.94 vs 0.97 ms; at D = 8 (quad rows, 127 VGPRs paired)
-// 11.17 vs 10.90 ms for 10M (profiles/r05/ab_read6_*).  AGN_READ6_XCD=1:
-// the XCD-aware block order (xcd_block; 11.59 vs 11.47 ms at 10M, off).
-constexpr uint64_t kRead6PairFrom = 1u << 14;
-
+// Requests per wave of k_read6: AGN_READ6_NP=2 takes two (opt-in).  Measured
+// against one, in one process (profiles/r05/ab_read6_*): 10M reads at D = 8
+// 11.00-11.17 vs 10.88-10.90 ms; 1M at D = 3 0.94-0.96 vs 0.94-0.97 ms.
+// AGN_READ6_XCD=1: the XCD-aware block order (xcd_block; 11.59 vs 11.47 ms at
+// 10M, off).
 int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     if (a.n_req == 0) return AGN_OK;
     if (a.n_req > 0x7fffffffull) return fail(AGN_ENOTSUP, "read6: batch too large");
     const dim3 grid((unsigned)a.n_req), block(AGN_WAVE);
     const bool msk = a.oc_mask || a.R_mask || c.clock_mask;
     const char *npv = AGN_KNOB("AGN_READ6_NP");
-    const bool pair = npv && npv[0] ? npv[0] == '2' : (a.n_dcs < 8 && a.n_req >= kRead6PairFrom);
+    const bool pair = npv && npv[0] == '2';
     const char *xv = AGN_KNOB("AGN_READ6_XCD");
     const uint32_t xcd = (xv && xv[0] == '1') ? 1u : 0u;
     const dim3 grid2((unsigned)((a.n_req + 1) / 2));
