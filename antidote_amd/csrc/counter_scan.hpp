@@ -82,8 +82,12 @@ __device__ __forceinline__ void load_row(const uint64_t *__restrict__ p, uint64_
 // of the aligned dword (byte arrays are read in 4-byte units; allocations are
 // rounded up far beyond that), so the check never waits on the vector-memory
 // queue, where it would drain the cross-key prefetch.
+// (ldc: the read-only per-key / per-request arrays load through the scalar
+// cache also where the kernel's pointers carry no __restrict__ -- read6.hip,
+// k_counter_q8e2's parameter block -- instead of as vector loads each waited
+// for before its readfirstlane)
 __device__ __forceinline__ uint32_t byte_of(const uint8_t *__restrict__ p, uint64_t idx) {
-    const uint32_t w = reinterpret_cast<const uint32_t *>(p)[idx >> 2];
+    const uint32_t w = ldc(reinterpret_cast<const uint32_t *>(p) + (idx >> 2));
     return (w >> ((uint32_t)(idx & 3u) * 8u)) & 0xffu;
 }
 
@@ -100,9 +104,9 @@ __device__ __forceinline__ KeyMeta key_meta(uint64_t key, const uint64_t *__rest
                                             const uint32_t *__restrict__ key_id0) {
     const uint64_t *lp = key_len ? key_len + key : key_off + key + 1;
     const uint32_t *ip = key_id0 ? key_id0 + key : reinterpret_cast<const uint32_t *>(key_off + key);
-    const uint64_t off = uniform_u64(key_off[key]);
-    const uint64_t l = uniform_u64(*lp);
-    const uint32_t id = __builtin_amdgcn_readfirstlane(*ip);
+    const uint64_t off = uniform_u64(ldc(key_off + key));
+    const uint64_t l = uniform_u64(ldc(lp));
+    const uint32_t id = __builtin_amdgcn_readfirstlane(ldc(ip));
     return KeyMeta{off, key_len ? l : l - off, key_id0 ? id : AGN_ID0_NONE};
 }
 

@@ -474,7 +474,7 @@ struct Q2Key {
 // agn_log.key_mask of a key (an in-bounds dummy when the log has none).
 __device__ __forceinline__ uint64_t key_word(const MaskArgs &mk, uint64_t key,
                                              const uint64_t *__restrict__ key_off) {
-    return uniform_u64(*(mk.key_mask ? mk.key_mask + key : key_off));
+    return uniform_u64(ldc(mk.key_mask ? mk.key_mask + key : key_off));
 }
 
 // The key's segment (the metadata the row loads depend on).
@@ -483,7 +483,7 @@ __device__ __forceinline__ void q2_meta(Q2Key &k, uint64_t i, const uint64_t *__
                                         const uint64_t *__restrict__ key_len,
                                         const uint32_t *__restrict__ key_id0) {
     k.i = i;
-    k.key = keys ? uniform_u64(keys[i]) : i;
+    k.key = keys ? uniform_u64(ldc(keys + i)) : i;
     const KeyMeta km = key_meta(k.key, key_off, key_len, key_id0);
     k.off = km.off;
     k.n = km.n;
@@ -523,18 +523,18 @@ __device__ __forceinline__ Q2Raw q2_load(const Q2Key &k, const DenseArgs &a, con
     const uint64_t i = k.i;
     Q2Raw x;
     const uint8_t *ktp = key_type ? key_type : reinterpret_cast<const uint8_t *>(key_off);
-    x.ktw = __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(ktp)[k.key >> 2]);
+    x.ktw = __builtin_amdgcn_readfirstlane(ldc(reinterpret_cast<const uint32_t *>(ktp) + (k.key >> 2)));
     const uint8_t *sip = sct_ignore ? sct_ignore : reinterpret_cast<const uint8_t *>(R);
-    x.sibw = ANY_WARM ? __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(sip)[i >> 2])
+    x.sibw = ANY_WARM ? __builtin_amdgcn_readfirstlane(ldc(reinterpret_cast<const uint32_t *>(sip) + (i >> 2)))
                       : 0u;
-    x.txv = uniform_u64((req_txid ? req_txid : R)[i]);
+    x.txv = uniform_u64(ldc((req_txid ? req_txid : R) + i));
     x.kmw = (MSK && with_km) ? key_word(mk, k.key, key_off) : 0ull;
     x.rmw = x.smw = 0ull;
     if constexpr (MSK) {
         // AGN_HINT_R_FULL: every R mask carries all D DCs (not read)
         const bool rfull = (a.hints & AGN_HINT_R_FULL) != 0u;
-        x.rmw = uniform_u64(*((mk.R_mask && !rfull) ? mk.R_mask + i : R));
-        x.smw = uniform_u64(*((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
+        x.rmw = uniform_u64(ldc((mk.R_mask && !rfull) ? mk.R_mask + i : R));
+        x.smw = uniform_u64(ldc((ANY_WARM && mk.sct_mask) ? mk.sct_mask + i : R));
     }
     const uint64_t *sct_p = (ANY_WARM && sct) ? sct : R;
     const uint64_t pp = 2u * (uint64_t)(lane_id() & 3);
@@ -701,8 +701,8 @@ __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s, uint32_t h
     if (k.id0 != AGN_ID0_NONE)
         hid = k.n ? (int64_t)((uint64_t)k.id0 + pos) : 0;
     else
-        hid = k.n ? (int64_t)op_id[uniform_u64(k.off + pos)] : 0;
-    const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)base_value[i]) : 0;
+        hid = k.n ? (int64_t)__builtin_amdgcn_readfirstlane(ldc(op_id + uniform_u64(k.off + pos))) : 0;
+    const int64_t base = base_value ? (int64_t)uniform_u64((uint64_t)ldc(base_value + i)) : 0;
     const int64_t total = wave_sum_dpp(s.sum);
     const bool ct_ign = k.sct_ign && s.cnt == 0u;
     uint64_t mo = 0;
@@ -743,6 +743,38 @@ __device__ __forceinline__ void q2_epilogue(const Q2Key &k, Q2Acc &s, uint32_t h
         o_flags[i] = fl;
         if (MSK && o_mask && !full) o_mask[i] = mo;
     }
+}
+
+// k_counter_q8e2's parameters as one block (kparams: each stage reads the
+// fields it uses; as 26 separate arguments it spilled 62 SGPRs, 43-47 so).
+// k_counter_quad2 keeps its by-value arguments: read this way its dense warm
+// form ran 9.47 against 8.32 ms (the parameter loads joined the prologue's
+// dependent chain; profiles/r05/ab_masked_warm_quad2_kparams.log).
+struct Q2Params {
+    DenseArgs a;
+    MaskArgs mk;
+    const uint64_t *keys, *key_off, *key_len;
+    const uint8_t *key_type;
+    const uint32_t *key_id0;
+    const uint64_t *oc;
+    const uint32_t *op_id;
+    const int64_t *eff;
+    const uint64_t *log_txid, *R, *sct;
+    const uint8_t *sct_ignore;
+    const uint64_t *req_txid;
+    const int64_t *base_value;
+    int64_t *o_value, *o_hole;
+    uint64_t *o_lastct;
+    uint32_t *o_count, *o_flags, *o_err, *list, *list_n;
+};
+
+template <class T>
+__device__ __forceinline__ DenseArgs dense_of(const T &x) {
+    return DenseArgs{x.n_req, x.n_entries, x.req_type, x.xcd, x.pair, x.qnt, x.hints, x.ql_cap};
+}
+template <class T>
+__device__ __forceinline__ MaskArgs mask_of(const T &x) {
+    return MaskArgs{x.key_mask, x.oc_mask, x.R_mask, x.sct_mask, x.o_mask};
 }
 
 template <bool ANY_WARM, bool MSK>
@@ -883,38 +915,9 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
 // side loads (R, SCT, the DC sets) under the chunks.  Mixed keys are handed
 // on to k_counter_q8m as in q8e.  (Round 3's two-request masked form carried
 // the per-entry-mask scan inline: 118 VGPRs, slower than one request.)
-// k_counter_q8e2's parameters as one block (kparams: each stage reads the
-// fields it uses; as 26 separate arguments the kernel spilled 66 SGPRs).
-struct Q8e2Params {
-    DenseArgs a;
-    MaskArgs mk;
-    const uint64_t *keys, *key_off, *key_len;
-    const uint8_t *key_type;
-    const uint32_t *key_id0;
-    const uint64_t *oc;
-    const uint32_t *op_id;
-    const int64_t *eff;
-    const uint64_t *log_txid, *R, *sct;
-    const uint8_t *sct_ignore;
-    const uint64_t *req_txid;
-    const int64_t *base_value;
-    int64_t *o_value, *o_hole;
-    uint64_t *o_lastct;
-    uint32_t *o_count, *o_flags, *o_err, *list, *list_n;
-};
-
-template <class T>
-__device__ __forceinline__ DenseArgs dense_of(const T &x) {
-    return DenseArgs{x.n_req, x.n_entries, x.req_type, x.xcd, x.pair, x.qnt, x.hints, x.ql_cap};
-}
-template <class T>
-__device__ __forceinline__ MaskArgs mask_of(const T &x) {
-    return MaskArgs{x.key_mask, x.oc_mask, x.R_mask, x.sct_mask, x.o_mask};
-}
-
 template <bool KEYS>
-__global__ __launch_bounds__(64) void k_counter_q8e2(Q8e2Params) {
-    const DenseArgs a = dense_of(kparams<Q8e2Params>().a);
+__global__ __launch_bounds__(64) void k_counter_q8e2(Q2Params) {
+    const DenseArgs a = dense_of(kparams<Q2Params>().a);
     const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
     const uint32_t blk = a.xcd ? xb : blockIdx.x;
     const uint64_t i0 = uniform_u64((uint64_t)blk * 2u);
@@ -923,19 +926,19 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(Q8e2Params) {
     const uint64_t i1 = two ? i0 + 1u : i0;
     Q2Key k0, k1;
     {
-        const auto &p = kparams<Q8e2Params>();
+        const auto &p = kparams<Q2Params>();
         q2_meta(k0, i0, KEYS ? p.keys : nullptr, p.key_off, p.key_len, p.key_id0);
         q2_meta(k1, i1, KEYS ? p.keys : nullptr, p.key_off, p.key_len, p.key_id0);
     }
     const bool any = a.n_entries != 0;
     Q8Chunk c0{}, c1{};
     if (any) {
-        const auto &p = kparams<Q8e2Params>();
+        const auto &p = kparams<Q2Params>();
         c0 = q8_load<true, false>(p.oc, p.eff, k0.off, 0, a.n_entries);
         c1 = q8_load<true, false>(p.oc, p.eff, k1.off, 0, a.n_entries);
     }
     __builtin_amdgcn_sched_barrier(0);
-    const auto &ps = kparams<Q8e2Params>();
+    const auto &ps = kparams<Q2Params>();
     const MaskArgs mk = mask_of(ps.mk);
     const uint64_t kmw0 = key_word(mk, k0.key, ps.key_off), kmw1 = key_word(mk, k1.key, ps.key_off);
     q2_side<true, true>(k0, a, mk, kmw0, ps.key_off, ps.key_type, ps.R, ps.sct, ps.sct_ignore,
@@ -947,7 +950,7 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(Q8e2Params) {
     };
     auto hand_on = [&](uint64_t i) {  // q8e's sub-lists
         if (lane_id() == 0) {
-            const auto &p = kparams<Q8e2Params>();
+            const auto &p = kparams<Q2Params>();
             const uint32_t sl = (uint32_t)(i % QL_S);
             p.list[(uint64_t)sl * a.ql_cap + atomicAdd(p.list_n + sl * QL_STRIDE, 1u)] = (uint32_t)i;
         }
@@ -962,13 +965,13 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(Q8e2Params) {
     s1.ctB = k1.eB;
     const bool d0 = any && !k0.corrupt && !m0, d1 = two && any && !k1.corrupt && !m1;
     {
-        const auto &p = kparams<Q8e2Params>();
+        const auto &p = kparams<Q2Params>();
         if (d0) q2_fold<true>(k0, c0, 0, p.log_txid, a.n_entries, s0);
         if (d1) q2_fold<true>(k1, c1, 0, p.log_txid, a.n_entries, s1);
         if (d0) q2_rest<true>(k0, p.oc, p.eff, p.log_txid, a.n_entries, s0);
         if (d1) q2_rest<true>(k1, p.oc, p.eff, p.log_txid, a.n_entries, s1);
     }
-    const auto &pe = kparams<Q8e2Params>();
+    const auto &pe = kparams<Q2Params>();
     if (!m0)
         q2_epilogue<true>(k0, s0, a.hints, pe.op_id, pe.base_value, pe.o_value, pe.o_hole,
                           pe.o_lastct, pe.o_count, pe.o_flags, pe.o_err, pe.mk.o_mask);
@@ -1100,13 +1103,14 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     const unsigned mb = QL_S * 16u;  // a multiple of QL_S
 #define AGN_Q8M(W, K)                                                                           \
     hipLaunchKernelGGL((k_counter_q8m<W, K>), dim3(mb), dim3(64), 0, st, AGN_ARGS)
-    // warm: two requests per wave with AGN_Q8E_TWO=1 (k_counter_q8e2; not
-    // yet measured against one request per wave, so not the default)
+    // warm: two requests per wave (k_counter_q8e2; AGN_Q8E_TWO=0: one).
+    // Warm masked cfg2 8.55 ms against q8e's 9.27 and the dense warm
+    // kernel's 8.27 (profiles/r05/ab_masked_warm_q8e2_ldc.log)
     const char *tv = AGN_KNOB("AGN_Q8E_TWO");
-    const bool two = tv && tv[0] == '1';
+    const bool two = !(tv && tv[0] == '0');
     const unsigned nb2 = (unsigned)((req.n_req + 1) / 2);
 #define AGN_Q8E2(K)                                                                             \
-    hipLaunchKernelGGL((k_counter_q8e2<K>), dim3(nb2), dim3(64), 0, st, Q8e2Params{AGN_ARGS})
+    hipLaunchKernelGGL((k_counter_q8e2<K>), dim3(nb2), dim3(64), 0, st, Q2Params{AGN_ARGS})
     if (rc == AGN_OK) {
         if (req.sct && two) {
             if (req.keys) { AGN_Q8E2(true); AGN_Q8M(true, true); }

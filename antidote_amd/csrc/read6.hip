@@ -89,10 +89,14 @@ __device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, KA &k) {
     const int lane = lane_id();
     const int dl = lane % R6Req<D, MSK>::DCP;
     const uint64_t i = q.i, key = q.key;
-    q.n0 = __builtin_amdgcn_readfirstlane(c.n[key]);
+    // the key's slot count through the scalar cache with the segment words
+    // (one wait for all): this launch writes c.n, but only key's own wave
+    // writes c.n[key], after this read (a batch names distinct keys), and the
+    // scalar cache starts every launch empty
+    q.n0 = __builtin_amdgcn_readfirstlane(ldc(c.n + key));
     if constexpr (D < 8) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) q.r[j] = uniform_u64(a.R[i * D + j]);
+        for (int j = 0; j < D; ++j) q.r[j] = uniform_u64(ldc(a.R + i * D + j));
     }
     q.rd = a.R[i * D + (uint64_t)(dl < D ? dl : D - 1)];
     if constexpr (D == 8) q.rq = *reinterpret_cast<const u64x2 *>(a.R + i * D + 2u * (lane & 3));
@@ -100,8 +104,8 @@ __device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, KA &k) {
     // dummy word when absent: a conditional scalar load waits on its own)
     q.kmw = q.rmw = 0ull;
     if constexpr (MSK) {
-        q.kmw = uniform_u64(*(a.key_mask ? a.key_mask + key : a.R));
-        q.rmw = uniform_u64(*(a.R_mask ? a.R_mask + i : a.R));
+        q.kmw = uniform_u64(ldc(a.key_mask ? a.key_mask + key : a.R));
+        q.rmw = uniform_u64(ldc(a.R_mask ? a.R_mask + i : a.R));
     }
     const KeyMeta km = key_meta(key, a.key_off, a.key_len, a.key_id0);
     q.off = km.off;
@@ -110,7 +114,7 @@ __device__ __forceinline__ void r6_meta(R6Req<D, MSK> &q, KA &k) {
     // key_type (corrupted_ops_cache, read before any store) and the TxId:
     // unconditional, from dummy addresses when absent
     q.kty = byte_of(a.key_type ? a.key_type : reinterpret_cast<const uint8_t *>(a.key_off), key);
-    q.txv = uniform_u64((a.txid ? a.txid : a.R)[i]);
+    q.txv = uniform_u64(ldc((a.txid ? a.txid : a.R) + i));
 }
 
 template <int D, bool MSK, class KA>
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(64) void k_read6(R6Params) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         q[p].i = i0 + (uint64_t)p < n_req ? i0 + (uint64_t)p : i0;
-        q[p].key = uniform_u64(k0.a.keys[q[p].i]);
+        q[p].key = uniform_u64(ldc(k0.a.keys + q[p].i));
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) r6_meta(q[p], kp());

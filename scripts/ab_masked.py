@@ -41,6 +41,9 @@ VARIANTS = {
     "mixed_km1": ("mixed", {"AGN_Q8E_KM": "1"}, 0),
     "mixed_hint": ("mixed", {}, 0x4),   # AGN_HINT_MIXED: k_counter_key
     "masked_two": ("masked", {"AGN_Q8E_TWO": "1"}, 0x2),  # warm: k_counter_q8e2
+    # warm masked batches default to k_counter_q8e2 (round 5); one request
+    # per wave (k_counter_q8e) with the bench's hints
+    "masked_one": ("masked", {"AGN_Q8E_TWO": "0"}, HINTS),
     # round 5: the dense kernel one request per wave (k_counter_key quad rows;
     # warm dense batches default to two per wave, k_counter_quad2), and the
     # masked batch through k_counter_quad2's MSK form
