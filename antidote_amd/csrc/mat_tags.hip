@@ -48,19 +48,30 @@ constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t NIL = 0xffffffffu;
 
 
+// The candidate table: 5.5 KB per wave at CAP = 256 (CAP hash buckets,
+// 16-bit chain links).  The fast pass's occupancy is set by it: at 7 KB
+// (2 CAP buckets, 32-bit links) 22 one-wave blocks fit a CU, 5.5 per SIMD,
+// below the 7 its 73 VGPRs allow.
 template <int CAP>
 struct CandLds {
+    static_assert(CAP < 0xffff, "16-bit chain links");
     uint64_t tok[CAP];
     uint32_t tag[CAP];
     uint32_t ord[CAP];   // B + position (base pairs: index < B); DEAD bit
-    uint32_t nxt[CAP];   // hash chain
-    uint32_t head[2 * CAP];
+    uint32_t head[CAP];  // hash buckets (chain heads, NIL = empty)
+    uint16_t nxt[CAP];   // hash chain, 0xffff = end
 };
 
 template <int CAP>
 __device__ __forceinline__ uint32_t hbucket(uint64_t t) {
-    constexpr int LOG = __builtin_ctz(2 * CAP);
+    constexpr int LOG = __builtin_ctz(CAP);
     return (uint32_t)((t * 0x9E3779B97F4A7C15ull) >> (64 - LOG));
+}
+
+template <int CAP>
+__device__ __forceinline__ uint32_t chain_next(const CandLds<CAP> &L, uint32_t x) {
+    const uint32_t v = L.nxt[x];
+    return v == 0xffffu ? NIL : v;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -75,14 +86,14 @@ __device__ __forceinline__ uint64_t lanes_below() {
 
 template <int CAP>
 __device__ __forceinline__ void heads_clear(CandLds<CAP> &L) {
-    for (int s = lane_id(); s < 2 * CAP; s += AGN_WAVE) L.head[s] = NIL;
+    for (int s = lane_id(); s < CAP; s += AGN_WAVE) L.head[s] = NIL;
     wave_sync();
 }
 
 template <int CAP>
 __device__ __forceinline__ void link(CandLds<CAP> &L, uint32_t s, uint64_t t) {
     const uint32_t prev = atomicExch(&L.head[hbucket<CAP>(t)], s);
-    L.nxt[s] = prev;
+    L.nxt[s] = (uint16_t)prev;  // NIL -> 0xffff
 }
 
 // Stable in-place compaction of the live candidates [0, used); returns the
@@ -597,7 +608,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
                     const bool einc = (im >> sidx) & 1ull;
                     if (has && einc) {
                         const uint32_t qpos = B + (uint32_t)(c0 + sidx);
-                        for (uint32_t x = L.head[hbucket<CAP>(t)]; x != NIL; x = L.nxt[x]) {
+                        for (uint32_t x = L.head[hbucket<CAP>(t)]; x != NIL; x = chain_next(L, x)) {
                             if (L.tok[x] != t) continue;
                             if (SET && L.tag[x] != etag) continue;
                             const uint32_t o = L.ord[x];
@@ -767,7 +778,7 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
         if (e != hipSuccess) return e;
     }
     // the overflow pass grid-strides over a list of at most n_req keys: a
-    // resident grid of up to 256 one-wave blocks (112 KB of LDS each), no
+    // resident grid of up to 256 one-wave blocks (88 KB of LDS each), no
     // more than the batch -- a serving batch of ~10 reads must not occupy
     // every CU's LDS, while other partitions' batches wait, to find the list
     // empty
