@@ -181,7 +181,19 @@ __global__ __launch_bounds__(256) void k_gst_scalar(uint64_t *vec, uint64_t *out
 }
 
 // try_store/2's vectorclock:ge(Cur, Deps) with the origin entry zeroed on
-// both sides: one wave per transaction, lanes over DCs, one ballot.
+// both sides.  A group of G lanes per transaction (G = pow2 >= D, at most
+// 64; 64 / G transactions per wave, so a wave reads 64 consecutive clock
+// words), lanes over DCs, one ballot folded per group.  The waves of a
+// resident grid stride over tiles of 64 / G transactions, U tiles per step
+// with all their loads issued before the first compare, and the partition
+// clocks (a few KB: P x D words and masks) are staged in LDS once per block
+// when they fit (STAGE), so a tile's only memory round trip is its own
+// words.  One wave per transaction (round 4) ran 3.6e9 waves/s against the
+// dispatcher: 0.036 of 8 TB/s at D = 8 (profiles/r05/bench_dep_check*.log).
+constexpr int DEP_U = 4;
+constexpr size_t DEP_LDS = 48u << 10;  // bytes of partition clocks staged per block
+
+template <int G, bool STAGE>
 __global__ __launch_bounds__(256) void k_dep_check(uint32_t D, uint64_t n,
                                                    const uint64_t *__restrict__ deps,
                                                    const uint64_t *__restrict__ dm,
@@ -191,25 +203,68 @@ __global__ __launch_bounds__(256) void k_dep_check(uint32_t D, uint64_t n,
                                                    const uint64_t *__restrict__ pc,
                                                    const uint64_t *__restrict__ pm,
                                                    uint8_t *__restrict__ ok) {
-    const uint64_t t = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (t >= n) return;
-    const int lane = lane_id();
+    extern __shared__ uint64_t sh[];  // STAGE: pc [n_parts][D], then pm [n_parts][W]
+    constexpr int TPW = AGN_WAVE / G;  // transactions per tile (one wave)
     const uint32_t W = n_words(D);
-    const uint64_t p = part[t];
-    const uint32_t o = origin[t];
-    bool bad = p >= n_parts;
-    if (!bad) {
-        for (uint32_t d = lane; d < D; d += AGN_WAVE) {
-            if (d == o) continue;
-            const bool pa = !dm || ((dm[t * W + (d >> 6)] >> (d & 63)) & 1ull);
-            if (!pa) continue;
-            const bool pb = !pm || ((pm[p * W + (d >> 6)] >> (d & 63)) & 1ull);
-            const uint64_t b = pb ? pc[p * D + d] : 0ull;
-            if (deps[t * D + d] > b) bad = true;
+    const uint64_t *cpc = pc, *cpm = pm;
+    if constexpr (STAGE) {
+        const uint64_t nc = n_parts * D, nm = pm ? n_parts * W : 0;
+        for (uint64_t x = threadIdx.x; x < nc; x += blockDim.x) sh[x] = pc[x];
+        for (uint64_t x = threadIdx.x; x < nm; x += blockDim.x) sh[nc + x] = pm[x];
+        __syncthreads();
+        cpc = sh;
+        cpm = pm ? sh + nc : nullptr;
+    }
+    const int lane = lane_id();
+    const int g = lane / G, gl = lane % G;
+    const uint64_t nt = (n + TPW - 1) / TPW;                       // tiles
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (uint64_t tile = w; tile < nt; tile += waves * DEP_U) {
+        uint64_t t[DEP_U], p[DEP_U], dv[DEP_U], dmw[DEP_U];
+        uint32_t o[DEP_U];
+        bool live[DEP_U];
+        const uint32_t dl = (uint32_t)gl < D ? (uint32_t)gl : D - 1u;  // D <= G: lane gl's DC
+#pragma unroll
+        for (int u = 0; u < DEP_U; ++u) {  // the step's words, all issued before any compare
+            const uint64_t tu = (tile + (uint64_t)u * waves) * TPW + (uint64_t)g;
+            live[u] = tu < n;
+            t[u] = live[u] ? tu : 0ull;
+            p[u] = part[t[u]];
+            o[u] = origin[t[u]];
+            dv[u] = deps[t[u] * D + dl];
+            dmw[u] = dm ? dm[t[u] * W + (dl >> 6)] : ~0ull;
+        }
+        bool bad[DEP_U];
+#pragma unroll
+        for (int u = 0; u < DEP_U; ++u) {
+            bad[u] = live[u] && p[u] >= n_parts;
+            const uint64_t pp = p[u];
+            if (!live[u] || bad[u]) continue;  // an unknown partition: not applicable
+            if (D <= (uint32_t)G) {  // one DC per lane, its words preloaded above
+                const uint32_t d = (uint32_t)gl;
+                if (d < D && d != o[u] && ((dmw[u] >> (d & 63)) & 1ull)) {
+                    const bool pb = !cpm || ((cpm[pp * W + (d >> 6)] >> (d & 63)) & 1ull);
+                    const uint64_t b = pb ? cpc[pp * D + d] : 0ull;
+                    if (dv[u] > b) bad[u] = true;
+                }
+                continue;
+            }
+            for (uint32_t d = (uint32_t)gl; d < D; d += G) {
+                if (d == o[u]) continue;
+                const bool pa = !dm || ((dm[t[u] * W + (d >> 6)] >> (d & 63)) & 1ull);
+                const bool pb = !cpm || ((cpm[pp * W + (d >> 6)] >> (d & 63)) & 1ull);
+                const uint64_t b = pb ? cpc[pp * D + d] : 0ull;
+                if (pa && deps[t[u] * D + d] > b) bad[u] = true;
+            }
+        }
+        const uint64_t gm = (G == AGN_WAVE ? ~0ull : ((1ull << G) - 1ull)) << (g * G);
+#pragma unroll
+        for (int u = 0; u < DEP_U; ++u) {
+            const uint64_t any = ballot(bad[u]);
+            if (live[u] && gl == 0) ok[t[u]] = (any & gm) ? 0 : 1;
         }
     }
-    const uint64_t any = ballot(bad);
-    if (lane == 0) ok[t] = any ? 0 : 1;
 }
 
 __global__ void k_select_base(uint32_t D, uint64_t n_req, const uint64_t *cache_off,
@@ -326,9 +381,37 @@ int launch_dep_check(uint32_t D, uint64_t n, const uint64_t *deps, const uint64_
                      const uint32_t *origin, const uint32_t *part, uint64_t n_parts,
                      const uint64_t *pc, const uint64_t *pm, uint8_t *ok, hipStream_t s) {
     if (n == 0) return AGN_OK;
-    if ((n + 3) / 4 > 0x7fffffffull) return fail(AGN_EINVAL, "dep_check: batch too large");
-    hipLaunchKernelGGL(k_dep_check, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, D, n, deps,
-                       dm, origin, part, n_parts, pc, pm, ok);
+    const uint32_t G = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16
+                     : D <= 32 ? 32 : 64;
+    const uint64_t W = n_words(D);
+    const size_t stage = (size_t)(n_parts * D + (pm ? n_parts * W : 0)) * 8u;
+    const bool st = n_parts > 0 && stage <= DEP_LDS;
+    // a resident grid: the tiles (64 / G transactions each) over 4-wave
+    // blocks, at most 8 blocks per CU
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint64_t tiles = (n + (AGN_WAVE / G) - 1) / (AGN_WAVE / G);
+    const uint64_t want = (tiles + 4 * DEP_U - 1) / (4 * DEP_U);
+    const uint64_t cap = (uint64_t)(cus > 0 ? cus : 256) * 8u;
+    const unsigned nb = (unsigned)(want < cap ? want : cap);
+#define AGN_DEP(GV)                                                                             \
+    do {                                                                                        \
+        if (st) hipLaunchKernelGGL((k_dep_check<GV, true>), dim3(nb), dim3(256), stage, s, D, n, \
+                                   deps, dm, origin, part, n_parts, pc, pm, ok);                 \
+        else hipLaunchKernelGGL((k_dep_check<GV, false>), dim3(nb), dim3(256), 0, s, D, n, deps, \
+                                dm, origin, part, n_parts, pc, pm, ok);                          \
+    } while (0)
+    switch (G) {
+        case 1: AGN_DEP(1); break;
+        case 2: AGN_DEP(2); break;
+        case 4: AGN_DEP(4); break;
+        case 8: AGN_DEP(8); break;
+        case 16: AGN_DEP(16); break;
+        case 32: AGN_DEP(32); break;
+        default: AGN_DEP(64); break;
+    }
+#undef AGN_DEP
     AGN_HIP(hipGetLastError());
     return AGN_OK;
 }

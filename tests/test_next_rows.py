@@ -133,6 +133,23 @@ def test_dep_check_gpu_vs_oracle(eng, oracle_lib, D, sparse, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("D,sparse,n,P", [(8, False, 300_000, 5000), (5, True, 123_457, 3),
+                                          (64, True, 70_001, 100), (16, False, 99_999, 1)])
+def test_dep_check_gpu_bulk_vs_oracle(eng, oracle_lib, D, sparse, n, P):
+    """The resident-grid kernel at bulk size: many tiles per wave (4 per step),
+    ragged tails, partition clocks staged in LDS (P x D words <= 48 KB) or read
+    from memory (P = 5000 at D = 8: 320 KB)."""
+    deps, dm, origin, part, pc, pm = dep_case(D * 17 + n, D, n, P, sparse)
+    want = dep_oracle(oracle_lib, D, deps, dm, origin, part, pc, pm)
+    assert 0 < want.mean() < 1
+    bufs = [eng.upload(x) if x is not None else None for x in (deps, dm, origin, part, pc, pm)]
+    out = eng.empty(n)
+    eng.dep_check(D, n, *[b.ptr if b is not None else None for b in bufs[:4]], pc.shape[0],
+                  bufs[4].ptr, bufs[5].ptr if bufs[5] is not None else None, out.ptr)
+    assert np.array_equal(eng.download(out, np.uint8, (n,)), want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("D,E,p_absent", [(1, 3, 0.0), (5, 100, 0.3), (256, 256, 0.0),
                                           (300, 17, 0.5), (4, 8, 1.0)])
 def test_gst_scalar_gpu_vs_oracle(eng, oracle_lib, D, E, p_absent):
