@@ -763,20 +763,20 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
 
 // agn_read_cached's batch size from which it runs the three batched kernels
 // (k_ss_lookup -> the counter kernel -> k_ss_store, per-request prune flags)
-// instead of the fused one: same results; the batched kernels serve 8
-// requests per wave in the cache steps and two per wave in a warm scan, so
-// they win from ~32k requests (warm cfg2 keys, batched vs fused: 10k 28 vs
-// 24 us, 30k 48.6 vs 48.5, 100k 116 vs 125, 300k 309 vs 354, 1M 1.05 vs
-// 1.17 ms, 10M 10.2 vs 11.6 ms; profiles/r02/read_cached_split.log), while
-// the fused kernel's single launch wins below.  AGN_READ_CACHED_SPLIT=<n>
-// moves the switch (0: never).
-static uint64_t read_cached_split() {
+// instead of the fused one: same results.  D = 8 (quad rows): never -- the
+// fused kernel wins at every size since round 5 (warm cfg2 keys, fused vs
+// batched: 100k 0.099 vs 0.111 ms, 1M 0.97 vs 1.00, 10M 9.45 vs 9.70;
+// profiles/r05/ab_read6_sizes.log).  D < 8: from 2^15 requests, where the
+// batched kernels' 8 requests per wave in the cache steps and two per wave in
+// the scan win (D = 3: 100k 0.090 vs 0.090 ms, 1M 0.90 vs 0.84, 10M 8.99 vs
+// 8.20).  AGN_READ_CACHED_SPLIT=<n> moves the switch (0: never).
+static uint64_t read_cached_split(uint32_t D) {
     const char *v = AGN_KNOB("AGN_READ_CACHED_SPLIT");
     if (v && v[0]) {
         const uint64_t n = strtoull(v, nullptr, 10);
         return n ? n : ~0ull;
     }
-    return 1ull << 15;
+    return D == 8 ? ~0ull : 1ull << 15;
 }
 
 static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_req,
@@ -914,7 +914,7 @@ int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint6
     rc = use_device(ctx);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    if (n_req >= read_cached_split()) return read_cached_seq(cache, log, n_req, keys, R, txid,
+    if (n_req >= read_cached_split(log->n_dcs)) return read_cached_seq(cache, log, n_req, keys, R, txid,
                                                              should_gc, out, status, prune,
                                                              threshold, st);
     Read6Args a{};  // dense: the mask pointers stay null

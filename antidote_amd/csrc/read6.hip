@@ -15,7 +15,7 @@
 // k_ss_store (cache_dev.hpp, per-request prune flags), in one launch instead
 // of three kernels and two copies: for the read batcher requests are read
 // from, and results written to, device-visible pinned host memory;
-// agn_read_cached runs it over device arrays below 2^15 requests.
+// agn_read_cached runs it over device arrays (for D < 8 below 2^15 requests).
 #include "cache_dev.hpp"
 #include "counter_scan.hpp"
 #include "filter.hpp"
@@ -507,8 +507,12 @@ struct R6Params {
 using R6K = const __attribute__((address_space(4))) R6Params;
 __device__ __forceinline__ R6K &kp() { return kparams<R6Params>(); }
 
+// One request per wave on a dense log: a budget of 6 waves per SIMD (80
+// VGPRs, 4 spilled to scratch outside the scan; 84 and 5 waves without it):
+// 10M warm reads 9.53 against 10.23 ms, under the batched kernels' 9.68
+// (profiles/r05/ab_read6_cfg2_10M_w6.log).  The masked form would spill 38.
 template <int D, bool MSK, int NP>
-__global__ __launch_bounds__(64) void k_read6(R6Params) {
+__global__ __launch_bounds__(64, (NP == 1 && !MSK) ? 6 : 1) void k_read6(R6Params) {
     using Q = R6Req<D, MSK>;
     __shared__ uint64_t stage[Q::DCP][AGN_WAVE];
     R6K &k0 = kp();

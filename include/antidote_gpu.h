@@ -599,11 +599,11 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
  * results in out (value, hole, lastct, count, flags, err_pos), status[n_req]
  * (AGN_SS_*), prune[n_req] (per request, unlike agn_ss_store's per key) and
  * threshold[n_keys][D].  Same results, cache contents and prune flags as the
- * three calls; AGN_ENOTSUP for another type or shape.  Below 2^15 requests
- * one launch, the key's cache slots held in registers (21 us for 10k keys,
- * cfg1, D = 3, where the three calls take 35 us); from 2^15 requests the
- * batched kernels, which are faster in bulk (10M keys: 10.2 vs 11.6 ms);
- * AGN_READ_CACHED_SPLIT=<n> moves the switch (0: always one launch).  Reads
+ * three calls; AGN_ENOTSUP for another type or shape.  One launch, the
+ * key's cache slots held in registers (21 us for 10k keys, cfg1, D = 3, where
+ * the three calls take 35 us; 10M keys at D = 8: 9.5 vs 9.7 ms); for D < 8
+ * from 2^15 requests the batched kernels, which are faster there in bulk;
+ * AGN_READ_CACHED_SPLIT=<n> sets the switch (0: always one launch).  Reads
  * at most 16 slots of a key (caches written by these entry points hold at
  * most SNAPSHOT_THRESHOLD - 1). */
 int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,

@@ -7,7 +7,7 @@ for all.  Two priming reads store every key's snapshot; each timed read is
 then a cache hit with nothing to store (steady state), so every variant must
 produce identical results.
 
-  python scripts/ab_read6.py [config=2] [n_keys] [variants=prev,np1,np2,np2x,seq]
+  python scripts/ab_read6.py [config=2] [n_keys] [variants=prev,np1,np2,np2x,seq,name=lib.so]
 """
 import ctypes as C
 import json
@@ -39,16 +39,21 @@ VARS = {
     "seq": ("cur", {"AGN_READ_CACHED_SPLIT": "1"}),
     "default": ("cur", {}),
 }
+# name=path entries of the variant list: another library's fused kernel
+EXTRA = dict(x.split("=", 1) for x in ONLY if "=" in x)
+ONLY = [x.split("=", 1)[0] for x in ONLY]
+VARS.update({n: (n, {"AGN_READ_CACHED_SPLIT": "0"}) for n in EXTRA})
 VARS = {k: v for k, v in VARS.items() if k in ONLY}
 KNOBS = sorted({k for _, e in VARS.values() for k in e})
 
 eng = Engine(0)
-prev = pctx = None
-if any(lib == "prev" for lib, _ in VARS.values()):
-    prev = C.CDLL(os.path.join(ROOT, "tools", "libagn_prev.so"), mode=os.RTLD_LOCAL)
-    _abi.bind(prev, {k: v for k, v in _abi.PROTOTYPES.items() if hasattr(prev, k)})
-    pctx = C.c_void_p()
-    assert prev.agn_open(0, C.byref(pctx)) == 0
+LIBS = {}
+for name, path in ([("prev", "tools/libagn_prev.so")] if "prev" in VARS else []) + list(EXTRA.items()):
+    lib = C.CDLL(os.path.join(ROOT, path), mode=os.RTLD_LOCAL)
+    _abi.bind(lib, {k: v for k, v in _abi.PROTOTYPES.items() if hasattr(lib, k)})
+    ctx = C.c_void_p()
+    assert lib.agn_open(0, C.byref(ctx)) == 0
+    LIBS[name] = (lib, ctx)
 sp = torch.cuda.current_stream().cuda_stream
 g = _abi.AgnGenCfg(crdt_type=1, n_dcs=D, n_keys=K, ops_per_key=cfg["ops_per_key"],
                    n_elems=0, seed=cfg["seed"], key_base=0, key_stride=1, warm=0)
@@ -70,8 +75,9 @@ def set_env(env):
         os.environ.pop(k, None)
     os.environ.update(env)
     env_changed()
-    if prev is not None and hasattr(prev, "agn_env_reload"):
-        prev.agn_env_reload()
+    for lib, _ in LIBS.values():
+        if hasattr(lib, "agn_env_reload"):
+            lib.agn_env_reload()
 
 
 def run(lib):
@@ -79,9 +85,10 @@ def run(lib):
         eng.read_cached(cache, dl, K, dkeys.ptr, dr.R, dr.txid, None, res, bufs["status"].ptr,
                         bufs["prune"].ptr, bufs["thr"].ptr, sp)
     else:
-        rc = prev.agn_read_cached(pctx, C.byref(cache), C.byref(dl), K, dkeys.ptr, dr.R, dr.txid,
-                                  None, C.byref(res.struct), bufs["status"].ptr, bufs["prune"].ptr,
-                                  bufs["thr"].ptr, sp)
+        L, ctx = LIBS[lib]
+        rc = L.agn_read_cached(ctx, C.byref(cache), C.byref(dl), K, dkeys.ptr, dr.R, dr.txid,
+                               None, C.byref(res.struct), bufs["status"].ptr, bufs["prune"].ptr,
+                               bufs["thr"].ptr, sp)
         assert rc == 0
 
 

@@ -366,10 +366,11 @@ def test_read_cached_vs_sequence(eng, monkeypatch, D, split, np_):
 
 @pytest.mark.gpu
 def test_read_cached_default_dispatch(eng, monkeypatch):
-    """A batch above the fused/batched switch (2^15 requests) through
-    agn_read_cached's default dispatch equals the fused kernel forced on it
-    (AGN_READ_CACHED_SPLIT=0): outputs, status, prune flags, thresholds and
-    the caches, over a cold round and a warm round with GC reads."""
+    """A bulk batch (36k requests, D = 8) through agn_read_cached's default
+    dispatch (the fused kernel: D = 8 never switches since round 5) equals
+    the batched kernels forced on it (AGN_READ_CACHED_SPLIT=1): outputs,
+    status, prune flags, thresholds and the caches, over a cold round and a
+    warm round with GC reads."""
     K, D = 40_000, 8
     log, req, _ = random_case(977, _abi.COUNTER_PN, K, D, 12, txid=0.2, empty=0.05)
     dlog = eng.upload_log(log)
@@ -396,7 +397,7 @@ def test_read_cached_default_dispatch(eng, monkeypatch):
             gc = (rng.random(nr) < 0.2).astype(np.uint8)
             dk, dR, dtx, dgc = (eng.upload(x) for x in (keys, np.ascontiguousarray(R), tx, gc))
             got = []
-            for (c, _b), split in zip(caches, (None, "0")):
+            for (c, _b), split in zip(caches, (None, "1")):
                 if split is None:
                     monkeypatch.delenv("AGN_READ_CACHED_SPLIT", raising=False)
                 else:
