@@ -931,7 +931,8 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     # ignore flag and the base value per request
     wbytes = algorithmic_bytes(cfg, n_keys) + n_keys * (8 * D + 1 + 8)
     # PMC bytes of the warm k_counter_quad2 launches (scripts/gpu.sh pmcwarm:
-    # the steps launches after the 2 priming ones, before the read_cached ones)
+    # the steps launches after the 2 priming ones; agn_read_cached runs the
+    # fused kernel at D = 8, so they are the last quad2 launches)
     wtraffic, wsrc = pmc_traffic(cfg_id, n_keys, f"cfg{cfg_id}_warm") if cfg_id else \
         (None, "null: config id not given")
     return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,
