@@ -61,14 +61,13 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
 // for both requests before either waits, and the second request's slots and
 // rows stay in flight while the first is served.  Stages: r6_meta (scalar:
 // slot count, segment, type, presence words, TxId; vector: R), r6_rows (the
-// slots, chunk 0), r6_serve.  Measured (SQ counters, profiles/r05/): at D = 8
-// the kernel is issue-bound rather than latency-bound -- 27 % of its wave
-// cycles issue, 21 % wait for an issue slot, at 5 waves per SIMD -- so the
-// pair (127 VGPRs, 4 waves) gains nothing there; what did gain was fewer
-// instructions: R as per-lane vector loads instead of 16 uniform words (they
-// sat in SGPRs beside the ~100 of kernel arguments and spilled) and the
-// lookup's first-clear-slot search in spread form (12.24 -> 10.90 ms for
-// 10M warm reads; the three batched kernels take 9.70).
+// slots, chunk 0), r6_serve.  Measured (10M warm reads at D = 8, one
+// process; profiles/r05/ab_read6_*): the pair (127 VGPRs,
+// 4 waves per SIMD) gains nothing; what did: R as per-lane vector loads
+// instead of 16 uniform words (they sat in SGPRs beside the kernel's
+// arguments and spilled), the lookup's first-clear-slot search in spread
+// form, the per-key words through the scalar cache, and a 6-wave register
+// budget -- 12.2 -> 9.45 ms, under the three batched kernels' 9.70.
 template <int D, bool MSK>
 struct R6Req {
     static constexpr int DCP = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : 8;  // pow2 >= D
@@ -521,11 +520,8 @@ __device__ __forceinline__ void r6_serve(R6Req<D, MSK> &q, KA &k,
 // neither hoisted to the kernel's entry nor shared with another stage's):
 // as by-value arguments they were all loaded at the entry and held in SGPRs
 // for the whole kernel, which spilled 34 of them to VGPR lanes (now 0; 84
-// VGPRs instead of 89).  Measured: 10.88 vs 10.90 ms for 10M warm reads, no
-// change -- the D = 8 gap to the batched kernels (9.66 ms) is in the memory
-// side, not issue: the fused kernel fetches 8.7 % and writes 43 % more than
-// the three kernels together (one request's 1-8 byte outputs per wave, on
-// a different L2 from its neighbours'; profiles/r05/ab_read6_*).
+// VGPRs instead of 89; by itself 10.88 vs 10.90 ms for 10M warm reads, but
+// it is what lets the 6-wave budget below fit).
 struct R6Params {
     agn_ss_cache c;
     Read6Args a;
