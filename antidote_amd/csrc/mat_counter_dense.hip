@@ -777,8 +777,12 @@ __device__ __forceinline__ MaskArgs mask_of(const T &x) {
     return MaskArgs{x.key_mask, x.oc_mask, x.R_mask, x.sct_mask, x.o_mask};
 }
 
+// The dense warm form runs at 6 waves per SIMD: 80 VGPRs and 2 scratch
+// spills instead of 84 VGPRs (5 waves) and 24 spilled SGPRs, 8.13 against
+// 8.33 ms on warm cfg2 (profiles/r05/ab_quad2_w6.log).  The masked forms spill
+// far more under that budget and keep the default.
 template <bool ANY_WARM, bool MSK>
-__global__ __launch_bounds__(64) void k_counter_quad2(
+__global__ __launch_bounds__(64, (ANY_WARM && !MSK) ? 6 : 1) void k_counter_quad2(
     DenseArgs a, MaskArgs mk, const uint64_t *__restrict__ keys,
     const uint64_t *__restrict__ key_off, const uint64_t *__restrict__ key_len,
     const uint8_t *__restrict__ key_type, const uint32_t *__restrict__ key_id0,

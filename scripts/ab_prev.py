@@ -1,7 +1,8 @@
 """A/B the current library against tools/libagn_prev.so (an earlier commit,
 scripts/build_prev.sh) on BASELINE cfg2, one process, interleaved rounds with
 rotating order; both libraries share the process's HIP runtime, so the same
-device log / request / result buffers feed both."""
+device log / request / result buffers feed both.  WARM=1: warm requests
+(snapshot-carrying, the k_counter_quad2 path for counters)."""
 import ctypes as C
 import os
 import sys
@@ -37,7 +38,7 @@ for a in (sys.argv[2:] or ["prev=tools/libagn_prev.so"]):
 sp = torch.cuda.current_stream().cuda_stream
 g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=cfg["n_dcs"], n_keys=K,
                    ops_per_key=cfg["ops_per_key"], n_elems=cfg["n_elems"], seed=cfg["seed"],
-                   key_base=0, key_stride=1, warm=0)
+                   key_base=0, key_stride=1, warm=int(os.environ.get("WARM", "0")))
 dl, dr = eng.gen_dev(g)
 cap = None
 if cfg["crdt_type"] != 1:
