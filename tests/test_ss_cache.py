@@ -293,7 +293,8 @@ def test_read_cached_vs_sequence(eng, monkeypatch, D, split, np_):
     monkeypatch.setenv("AGN_READ_CACHED_SPLIT", split)
     monkeypatch.setenv("AGN_READ6_NP", np_)
     K = 3000
-    log, req, _ = random_case(501 + D, _abi.COUNTER_PN, K, D, 90, txid=0.2, empty=0.05)
+    # 0..150 ops per key: one, two and three 64-op chunks
+    log, req, _ = random_case(501 + D, _abi.COUNTER_PN, K, D, 150, txid=0.2, empty=0.05)
     rng = np.random.default_rng(D)
     dlog = eng.upload_log(log)
     dlog.struct.oc_mask = None
