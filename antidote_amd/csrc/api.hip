@@ -85,10 +85,14 @@ void EnvKnob::refresh(uint32_t g) {
     std::lock_guard<std::mutex> lk(g_env_mu);
     if (gen_.load(std::memory_order_relaxed) == g) return;
     const char *v = getenv(name_);
-    set_ = v != nullptr;
-    if (v) {
-        strncpy(val_, v, sizeof val_ - 1);
-        val_[sizeof val_ - 1] = 0;
+    const char *cur = val_.load(std::memory_order_relaxed);
+    // a new snapshot only when the value changed; the old one is kept (leaked
+    // on purpose: readers may hold it; reloads happen between test phases)
+    if (!v) {
+        val_.store(nullptr, std::memory_order_release);
+    } else if (!cur || std::strcmp(cur, v) != 0) {
+        const char *copy = strdup(v);
+        if (copy) val_.store(copy, std::memory_order_release);
     }
     gen_.store(g, std::memory_order_release);
 }
@@ -172,6 +176,10 @@ static bool mixed_log(agn_ctx *ctx, const agn_log *log) {
 
 static int validate(const agn_log *log, const agn_read *req, const agn_result *out) {
     if (!log || !req || !out) return fail(AGN_EINVAL, "null descriptor");
+    // byte arrays are read by the kernels as aligned dwords (scalar loads
+    // ignore the address's low two bits)
+    if (misaligned4(log->key_type) || misaligned4(req->sct_ignore))
+        return fail(AGN_EINVAL, "key_type / sct_ignore must be 4-byte aligned");
     if (log->n_dcs == 0 || log->n_dcs > 256) return fail(AGN_EINVAL, "n_dcs=%u not in [1,256]", log->n_dcs);
     if (log->crdt_type != AGN_COUNTER_PN && !is_tag_type(log->crdt_type))
         return fail(AGN_EINVAL, "unknown crdt_type %u", log->crdt_type);
@@ -394,13 +402,24 @@ int agn_log_index_masks(agn_ctx *ctx, const agn_log *log, uint64_t *out, void *s
         return fail(AGN_EINVAL, "index_masks: n_dcs=%u not in [1,64]", log->n_dcs);
     int rc = use_device(ctx);
     if (rc) return rc;
+    // the mixed-key count (a kernel-choice heuristic for later reads of this
+    // index; results never depend on it) is read back synchronously -- not
+    // inside a stream capture, where the index is then left unregistered
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess)
+        cap = hipStreamCaptureStatusNone;
+    const bool count = log->oc_mask && cap == hipStreamCaptureStatusNone;
     uint64_t mixed = 0;
-    rc = launch_index_masks(*log, out, log->oc_mask ? &mixed : nullptr, (hipStream_t)stream);
+    rc = launch_index_masks(*log, out, count ? &mixed : nullptr, (hipStream_t)stream);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(ctx->mi_mu);
     int slot = -1;
     for (int i = 0; i < agn_ctx::kMaskIdx && slot < 0; ++i)
         if (ctx->mi[i].key_mask == out) slot = i;
+    if (!count && log->oc_mask) {  // no count: forget a stale one for this buffer
+        if (slot >= 0) ctx->mi[slot] = {};
+        return AGN_OK;
+    }
     if (slot < 0) slot = (int)(ctx->mi_next++ % agn_ctx::kMaskIdx);
     ctx->mi[slot] = {out, log->n_keys, mixed};
     ctx->mi_any.store(true, std::memory_order_release);
@@ -965,6 +984,8 @@ int agn_prune_ops(agn_ctx *ctx, const agn_log *log, const uint8_t *prune,
         return fail(AGN_EINVAL, "prune_ops: out lacks an array the log has");
     if (log->n_entries > 0x7fffffffull || log->n_keys > 0x7fffffffull)
         return fail(AGN_ENOTSUP, "prune_ops: log too large for one pass");
+    if (misaligned4(prune) || misaligned4(log->key_type))
+        return fail(AGN_EINVAL, "prune_ops: prune / key_type must be 4-byte aligned");
     int rc = use_device(ctx);
     if (rc) return rc;
     out->crdt_type = log->crdt_type;

@@ -681,7 +681,9 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
     size_t o_keys_saved = 0, o_pr_saved = 0;
     {
         std::shared_lock<std::shared_mutex> hold;
-        rc = oplog_begin_read(B->log, B->stream, 0, nullptr, nullptr, hold);
+        uint64_t n_mixed = 0;
+        rc = oplog_begin_read(B->log, B->stream, 0, nullptr, nullptr, hold, sparse ? n : 0,
+                              keys.data(), &n_mixed);
         if (rc) return rc;
         // in = keys R Rm txid gc | scratch = sct sctm ign base first
         // out = value hole lastct lastct_mask count flags err_pos status prune
@@ -736,8 +738,7 @@ int run_batch_cached(agn_batcher *B, std::vector<Pending *> &b) {
         req.base_value = (const int64_t *)(d + o_base);
         // many of the batch's keys with entries of different DC sets (e.g.
         // soon after a DC joined): the counter kernel scans them in one pass
-        if (sparse && many_mixed(oplog_mixed_keys(B->log, n, keys.data()), n))
-            req.hints |= AGN_HINT_MIXED;
+        if (sparse && many_mixed(n_mixed, n)) req.hints |= AGN_HINT_MIXED;
         agn_result res;
         std::memset(&res, 0, sizeof res);
         res.value = (int64_t *)(d + o_val);
@@ -805,7 +806,9 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
     for (uint64_t i = 0; i < n; ++i) keys[i] = b[i]->rd->key;
     // flush + exact key lengths + the arena held shared until the batch is done
     std::shared_lock<std::shared_mutex> hold;
-    int rc = oplog_begin_read(B->log, B->stream, tags ? n : 0, keys.data(), lens.data(), hold);
+    uint64_t n_mixed = 0;
+    int rc = oplog_begin_read(B->log, B->stream, tags ? n : 0, keys.data(), lens.data(), hold,
+                              tags ? 0 : n, keys.data(), &n_mixed);
     if (rc) return rc;
     uint64_t ncap = 0;
     if (tags)
@@ -888,8 +891,7 @@ int run_batch(agn_batcher *B, std::vector<Pending *> &b) {
             for (uint32_t x = 0; m && x < W && rfull; ++x) rfull = (m[x] & full[x]) == full[x];
         }
         req.hints = AGN_HINT_CT_FLAG | (rfull ? AGN_HINT_R_FULL : 0u);
-        if (!tags && many_mixed(oplog_mixed_keys(B->log, n, keys.data()), n))
-            req.hints |= AGN_HINT_MIXED;
+        if (!tags && many_mixed(n_mixed, n)) req.hints |= AGN_HINT_MIXED;
     }
     if (tags) {
         req.base_off = (const uint64_t *)(d + o_boff);

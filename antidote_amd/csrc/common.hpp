@@ -23,18 +23,20 @@ extern std::atomic<uint32_t> g_env_gen;
 class EnvKnob {
   public:
     explicit EnvKnob(const char *name) : name_(name) {}
-    const char *get() {  // the variable's value, nullptr when unset
+    // the variable's value, nullptr when unset: an immutable snapshot that
+    // stays valid for the life of the process (a reload publishes a new one
+    // and never frees the old, so a caller may keep the pointer)
+    const char *get() {
         const uint32_t g = g_env_gen.load(std::memory_order_acquire);
         if (gen_.load(std::memory_order_acquire) != g) refresh(g);
-        return set_ ? val_ : nullptr;
+        return val_.load(std::memory_order_acquire);
     }
 
   private:
     void refresh(uint32_t g);  // api.hip
     const char *name_;
     std::atomic<uint32_t> gen_{0};
-    bool set_ = false;
-    char val_[48] = {};
+    std::atomic<const char *> val_{nullptr};
 };
 // getenv(NAME) through a per-call-site cached knob
 #define AGN_KNOB(NAME)                     \
@@ -157,12 +159,14 @@ __host__ __device__ inline uint64_t key_n(const uint64_t *key_off, const uint64_
 // where the kernel stores through other pointers that might alias it (a
 // grid-stride loop), which otherwise keeps it a vector load.  Never use it
 // on an array the same launch writes.
+inline bool misaligned4(const void *p) { return ((uintptr_t)p & 3u) != 0; }
 template <class T>
 __device__ __forceinline__ T ldc(const T *p) {
     return *(const __attribute__((address_space(4))) T *)p;
 }
 // A byte of a read-only byte array (key_type, sct_ignore) by ldc of its
-// aligned dword (byte arrays are allocated in whole dwords or more).
+// aligned dword (byte arrays are allocated in whole dwords or more; the ABI
+// requires them 4-byte aligned and validates it with misaligned4).
 __device__ __forceinline__ uint32_t ldc_byte(const uint8_t *p, uint64_t idx) {
     const uint32_t w = ldc(reinterpret_cast<const uint32_t *>(p) + (idx >> 2));
     return (__builtin_amdgcn_readfirstlane(w) >> ((uint32_t)(idx & 3u) * 8u)) & 0xffu;
@@ -251,10 +255,14 @@ inline unsigned resident_grid(K kernel, unsigned threads, uint64_t work_blocks) 
 
 // oplog.hip internals used by the read batcher.
 void oplog_shape(const agn_oplog *L, uint32_t *crdt, uint32_t *D, int *sparse, uint64_t *K);
+// mixed (optional): how many of mixed_keys[0..nm) hold entries with
+// different DC sets, counted under the writer lock before `hold` is taken
+// (the lock order is wmu before rw; nothing may take wmu under `hold`).
 int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *keys,
-                     uint32_t *lens, std::shared_lock<std::shared_mutex> &hold);
+                     uint32_t *lens, std::shared_lock<std::shared_mutex> &hold,
+                     uint64_t nm = 0, const uint64_t *mixed_keys = nullptr,
+                     uint64_t *mixed = nullptr);
 void oplog_view(const agn_oplog *L, agn_log *v);
-uint64_t oplog_mixed_keys(agn_oplog *L, uint64_t n, const uint64_t *keys);
 agn_ctx *oplog_ctx(const agn_oplog *L);
 
 // Launchers (defined in the .hip files).

@@ -901,6 +901,7 @@ int agn_oplog_prune(agn_oplog *L, const uint8_t *prune, const uint64_t *threshol
     if (!L) return fail(AGN_EINVAL, "oplog_prune: null oplog");
     if (!threshold) return fail(AGN_EINVAL, "oplog_prune: threshold required");
     if (L->sparse && !threshold_mask) return fail(AGN_EINVAL, "oplog_prune: sparse log needs threshold_mask");
+    if (misaligned4(prune)) return fail(AGN_EINVAL, "oplog_prune: prune must be 4-byte aligned");
     int rc = use_device(L->ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(L->wmu);
@@ -1023,8 +1024,22 @@ namespace agn {
 // writes each requested key's length into lens[n] -- so the lengths are
 // exactly those of the device log the read's kernel will see (a concurrent
 // append only stages on the host; its flush waits for `hold`).
+// How many of keys[0..n) hold entries with different DC sets (umask 0, not
+// empty): the read batcher's AGN_HINT_MIXED decision, from the host's copy
+// of agn_log.key_mask -- no device read.  Caller holds L->wmu.
+static uint64_t mixed_keys_locked(const agn_oplog *L, uint64_t n, const uint64_t *keys) {
+    if (!L->sparse || L->umask.empty()) return 0;
+    uint64_t m = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t k = keys[i];
+        m += k < L->K && L->umask[k] == 0 && L->len[k] != 0;
+    }
+    return m;
+}
+
 int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *keys,
-                     uint32_t *lens, std::shared_lock<std::shared_mutex> &hold) {
+                     uint32_t *lens, std::shared_lock<std::shared_mutex> &hold,
+                     uint64_t nm, const uint64_t *mixed_keys, uint64_t *mixed) {
     int rc = use_device(L->ctx);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(L->wmu);
@@ -1040,25 +1055,12 @@ int oplog_begin_read(agn_oplog *L, hipStream_t st, uint64_t n, const uint64_t *k
         if (rc) return rc;
         AGN_HIP(hipStreamSynchronize(st));
     }
+    if (mixed) *mixed = mixed_keys_locked(L, nm, mixed_keys);
     hold = std::shared_lock<std::shared_mutex>(L->rw);
     for (uint64_t i = 0; i < n; ++i) lens[i] = dlen_of(L, keys[i]);
     return AGN_OK;
 }
 void oplog_view(const agn_oplog *L, agn_log *v) { fill_view(L, v); }
-
-// How many of keys[0..n) hold entries with different DC sets (umask 0, not
-// empty): the read batcher's AGN_HINT_MIXED decision, from the host's copy
-// of agn_log.key_mask -- no device read.
-uint64_t oplog_mixed_keys(agn_oplog *L, uint64_t n, const uint64_t *keys) {
-    if (!L->sparse || L->umask.empty()) return 0;
-    std::lock_guard<std::mutex> g(L->wmu);
-    uint64_t m = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t k = keys[i];
-        m += k < L->K && L->umask[k] == 0 && L->len[k] != 0;
-    }
-    return m;
-}
 
 int oplog_prune_keys(agn_oplog *L, uint64_t n, const uint64_t *h_keys, const uint64_t *d_keys,
                      const uint8_t *d_flags, const uint64_t *thr, const uint64_t *thr_mask,

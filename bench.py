@@ -423,9 +423,91 @@ def main():
     if rank == 0:
         if configs:
             line["configs"] = configs
-        print(json.dumps(line), flush=True)
+        detail = write_detail(line)
+        print(json.dumps(compact_line(line, detail)), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# the driver parses the last stdout line from an ~8 KB tail: the final line
+# carries the headline's roofline + cpu_baseline in full and one short summary
+# per sub-config; everything else (warm / gc / presence / build / samples)
+# goes to the detail file named in the line
+LINE_MAX_BYTES = 7000
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+             "higher_is_better", "scaling", "vs_baseline", "dtype", "data",
+             "vc_compares_per_s", "config", "roofline", "cpu_baseline")
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms",
+             "algorithmic_bytes", "kernel_src_sha16")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "value_mt", "mt_threads")
+
+
+def _short(s, n=160):
+    return s if not isinstance(s, str) or len(s) <= n else s[:n - 3] + "..."
+
+
+def summarize_sub(sub):
+    """One sub-config as the final line carries it: kernel, its time and
+    roofline fraction, PMC traffic / algorithmic bytes, the step time and
+    the CPU baseline's value."""
+    roof = sub.get("roofline") or {}
+    cpu = sub.get("cpu_baseline") or {}
+    alg, traffic = roof.get("algorithmic_bytes"), roof.get("traffic")
+    return {"value": sub.get("value"), "unit": sub.get("unit"),
+            "ms_per_step": sub.get("ms_per_step"), "kernel": _short(roof.get("kernel"), 60),
+            "kernel_ms": roof.get("kernel_ms"), "frac": roof.get("frac"),
+            "algorithmic_bytes": alg, "traffic": traffic,
+            "traffic_ratio": traffic / alg if traffic and alg else None,
+            "cpu_value": cpu.get("value"),
+            "workload": _short(sub.get("config", {}).get("workload"), 120)}
+
+
+def compact_line(line, detail_path=None):
+    """The driver's line (< LINE_MAX_BYTES): the headline's own keys with its
+    full roofline and cpu_baseline, plus summarize_sub() per sub-config."""
+    out = {k: line[k] for k in HEAD_KEYS if k in line}
+    out["config"] = dict(out.get("config", {}))
+    if out.get("roofline"):
+        roof = {k: line["roofline"][k] for k in ROOF_KEYS if k in line["roofline"]}
+        if roof.get("traffic") and roof.get("algorithmic_bytes"):
+            roof["traffic_ratio"] = roof["traffic"] / roof["algorithmic_bytes"]
+        roof["traffic_source"] = _short(line["roofline"].get("traffic_source"), 120)
+        out["roofline"] = roof
+    if out.get("cpu_baseline"):
+        cpu = {k: line["cpu_baseline"][k] for k in CPU_KEYS if k in line["cpu_baseline"]}
+        cpu["sample"] = _short(cpu.get("sample"), 200)
+        cpu["erlang"] = "not reproducible offline (no Erlang runtime)"
+        out["cpu_baseline"] = cpu
+    build = line.get("build") or {}
+    out["build"] = {k: build[k] for k in ("lib_sha16", "csrc_sha16") if k in build}
+    if line.get("configs"):
+        out["configs"] = {n: summarize_sub(s) for n, s in line["configs"].items()}
+    if detail_path:
+        out["detail"] = detail_path
+    s = json.dumps(out)
+    if len(s) > LINE_MAX_BYTES:  # never lose the headline to its sub-lines
+        for sub in out.get("configs", {}).values():
+            sub.pop("workload", None)
+        if len(json.dumps(out)) > LINE_MAX_BYTES:
+            out.pop("configs", None)
+    return out
+
+
+def write_detail(line):
+    """The full line (every sub-line's warm / gc / presence / build objects)
+    as gpurun_out/bench_detail_<time>.json; returns its repo-relative path
+    (None if it could not be written)."""
+    rel = os.path.join("gpurun_out", time.strftime("bench_detail_%Y%m%dT%H%M%S.json",
+                                                   time.gmtime()))
+    try:
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, rel), "w") as f:
+            json.dump(line, f, indent=1)
+    except OSError as e:
+        print(f"bench: detail not written: {e}", file=sys.stderr)
+        return None
+    print(f"bench: full detail in {rel}", file=sys.stderr)
+    return rel
 
 
 def sub_configs(a, world):

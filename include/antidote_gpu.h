@@ -87,7 +87,8 @@ typedef struct agn_log {
     uint64_t n_entries;
     const uint64_t *key_off;  /* [n_keys+1] CSR, or segment starts when key_len != NULL */
     const uint64_t *key_len;  /* [n_keys] entries in use per segment, or NULL (CSR) */
-    const uint8_t *key_type;  /* [n_keys] type of the key's ops or AGN_TYPE_MIXED; NULL: all crdt_type */
+    const uint8_t *key_type;  /* [n_keys] type of the key's ops or AGN_TYPE_MIXED; NULL: all crdt_type;
+                                 4-byte aligned (AGN_EINVAL otherwise) */
     const uint64_t *oc;       /* [n_entries * D] OpSSCommit */
     const uint64_t *oc_mask;  /* [n_entries * W] presence, NULL = dense */
     const uint32_t *op_id;    /* [n_entries] per-key op number (ets update_counter, :630) */
@@ -133,7 +134,8 @@ typedef struct agn_read {
     const uint64_t *R_mask;     /* [n_req * W] or NULL (dense) */
     const uint64_t *sct;        /* [n_req * D] SnapshotCommitTime of the base snapshot, NULL = all ignore */
     const uint64_t *sct_mask;   /* [n_req * W] or NULL */
-    const uint8_t *sct_ignore;  /* [n_req] 1 = ignore (with sct != NULL), NULL = none ignored */
+    const uint8_t *sct_ignore;  /* [n_req] 1 = ignore (with sct != NULL), NULL = none ignored;
+                                   4-byte aligned (AGN_EINVAL otherwise) */
     const uint64_t *txid;       /* [n_req] reading TxId (0 = ignore) or NULL = all ignore */
     uint32_t req_type;          /* Type argument of materialize/4 */
     uint32_t hints;             /* ABI v5 (was padding; 0 = none): AGN_HINT_* promises
@@ -338,7 +340,8 @@ int agn_oplog_flush(agn_oplog *log, agn_log *view, void *stream);
  * so reads on any stream see the pruned log.  When the arenas hold more than
  * twice the slots the keys want, the call first re-lays them out into fresh
  * arenas (allocating everything before changing anything; skipped if memory
- * is short).  out_flags (device, may be NULL) as agn_prune_ops. */
+ * is short).  out_flags (device, may be NULL) as agn_prune_ops.  prune
+ * (device, [n_keys]) must be 4-byte aligned. */
 int agn_oplog_prune(agn_oplog *log, const uint8_t *prune, const uint64_t *threshold,
                     const uint64_t *threshold_mask, uint32_t *out_flags, void *stream);
 /* Host-side accounting: entries in use, allocated slots, removal tokens. */
@@ -678,7 +681,7 @@ int agn_log_ingest(agn_ctx *ctx, const agn_log_records *recs, uint32_t crdt_type
  * (src/materializer.erl:101-106) in log order.  threshold[n_keys][D] (+ mask,
  * NULL = dense; missing entries read 0) is vectorclock:min over the kept
  * snapshots' commit times (:523-527), computed by the caller.  Keys with
- * prune[k] == 0 are copied unchanged.
+ * prune[k] == 0 are copied unchanged; prune must be 4-byte aligned.
  * Out-of-place: `out` (host descriptor of device arrays) must provide
  * key_off[n_keys+1], oc, op_id (+ oc_mask, txid, eff, tag, add_tok,
  * rem_off[n_entries+1], rem_tok when `log` has them) with at least the input

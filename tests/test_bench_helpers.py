@@ -75,3 +75,35 @@ def test_algorithmic_bytes_match_design():
     c3 = bench.CONFIGS[3]
     b0 = bench.algorithmic_bytes(c3, 1000)
     assert bench.algorithmic_bytes(c3, 1000, n_rem=10, n_live=5) == b0 + 80 + 60
+
+
+def test_final_line_fits_driver_tail():
+    """The default run's final stdout line, built from a recorded full line
+    (round 5's closing run: headline + nine sub-lines, 20.5 KB), stays under
+    8000 bytes and keeps the headline's roofline / cpu_baseline whole and one
+    summary per sub-config."""
+    full = json.load(open(os.path.join(ROOT, "profiles", "r05", "bench_default_closing.json")))
+    out = bench.compact_line(full, "gpurun_out/bench_detail_x.json")
+    s = json.dumps(out)
+    assert len(s) < 8000, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "dtype", "config"):
+        assert out[k] == full[k]
+    roof = out["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
+              "algorithmic_bytes"):
+        assert roof[k] == full["roofline"][k]
+    assert roof["traffic_ratio"] == pytest.approx(roof["traffic"] / roof["algorithmic_bytes"])
+    for k in ("value", "unit", "cores", "kind"):
+        assert out["cpu_baseline"][k] == full["cpu_baseline"][k]
+    assert set(out["configs"]) == set(full["configs"])
+    for name, sub in out["configs"].items():
+        src = full["configs"][name]
+        assert sub["frac"] == src["roofline"]["frac"]
+        assert sub["kernel_ms"] == src["roofline"]["kernel_ms"]
+        assert sub["ms_per_step"] == src["ms_per_step"]
+        assert sub["cpu_value"] == (src.get("cpu_baseline") or {}).get("value")
+    # a line that would not fit drops sub-line detail, never the headline
+    big = dict(full, configs={f"c{i}": full["configs"]["cfg3_gc"] for i in range(60)})
+    out = bench.compact_line(big)
+    assert len(json.dumps(out)) < 8000 and out["roofline"]["frac"] == full["roofline"]["frac"]

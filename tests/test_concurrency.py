@@ -104,3 +104,66 @@ def test_batcher_sizes_outputs_under_concurrent_appends(eng, crdt):
             assert not errs, errs[0]
             final = [bt.read(k, R=big, out_cap=N)["out_n"] for k in range(K)]
             assert final == appended
+
+
+def test_batched_reads_concurrent_with_prune_sparse_log(eng):
+    """Lock order: a batcher worker reading a sparse log
+    counts the batch's mixed-DC-set keys (AGN_HINT_MIXED) under the writer
+    lock before it takes the arena shared, so a concurrent agn_oplog_prune
+    (writer lock, then the arena exclusively) cannot deadlock with it.  8
+    reader threads and one pruning / appending thread on one sparse
+    counter_pn log; every thread must finish, and every read's value is the
+    sum of the effects appended before it (nothing is ever pruned: the
+    thresholds are all 0)."""
+    D, K = 4, 8
+    W = 1
+    big = np.full(D, 10 ** 12, np.uint64)
+    with OpLog(eng, _abi.COUNTER_PN, D, K, sparse=True, init_slots=4) as ol:
+        # half the keys hold entries of two DC sets (umask 0: "mixed")
+        for j in range(64):
+            k = j % K
+            m = 0b1111 if (k % 2 == 0 or j % 3) else 0b0111
+            ol.append(np.array([k], np.uint64), np.full((1, D), 100 + j, np.uint64),
+                      oc_mask=np.array([[m]], np.uint64), eff=np.array([1], np.int64))
+        prune = eng.upload(np.ones(K, np.uint8))
+        thr = eng.upload(np.zeros((K, D), np.uint64))
+        tmask = eng.upload(np.full((K, W), ~np.uint64(0), np.uint64))
+        with Batcher(ol, max_batch=8, max_wait_us=50) as bt:
+            stop = threading.Event()
+            errs = []
+            n_app = [8] * K
+
+            def gc():
+                try:
+                    for j in range(300):
+                        ol.prune(prune.ptr, thr.ptr, tmask.ptr)
+                        k = j % K
+                        ol.append(np.array([k], np.uint64), np.full((1, D), 1000 + j, np.uint64),
+                                  oc_mask=np.array([[0b1011 if j % 2 else 0b1111]], np.uint64),
+                                  eff=np.array([1], np.int64))
+                        n_app[k] += 1
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+                finally:
+                    stop.set()
+
+            def reader(t):
+                try:
+                    while not stop.is_set():
+                        k = t % K
+                        lo = n_app[k]
+                        r = bt.read(k, R=big, R_mask=np.array([0b1111], np.uint64))
+                        # an append may land before its count does
+                        assert lo <= r["value"] <= n_app[k] + 1, (k, lo, r["value"])
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+            ts = [threading.Thread(target=gc, daemon=True)] + \
+                [threading.Thread(target=reader, args=(t,), daemon=True) for t in range(8)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(timeout=90)
+            assert not any(t.is_alive() for t in ts), "deadlock: reader / prune threads stuck"
+            assert not errs, errs[0]
+            assert [bt.read(k, R=big, R_mask=np.array([0b1111], np.uint64))["value"]
+                    for k in range(K)] == n_app
