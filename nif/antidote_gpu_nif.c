@@ -751,27 +751,46 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
                             atom(env, due[0] ? "true" : "false"));
 }
 
-/* the state pairs of a set/register result -> orddict [{Elem, [Tok]}] /
- * sorted [{Value, Token}] (decoded through the interners) */
+/* qsort by Erlang term order of `key`: set_aw groups {Elem, [Tok]} by Elem,
+ * register_mv pairs {V, Tok} as lists:sort/1 orders them */
+typedef struct {
+    ERL_NIF_TERM key, term;
+} sort_item;
+static int cmp_item(const void *a, const void *b) {
+    return enif_compare(((const sort_item *)a)->key, ((const sort_item *)b)->key);
+}
+
+/* the state pairs of a set/register result -> the reference's value: the
+ * set_aw orddict [{Elem, [Tok]}] (sorted by Elem; tokens in fold order) /
+ * the register_mv list of {Value, Token}, sorted (decoded through the
+ * interners, whose ids do not follow term order); 0 when out of memory */
 static ERL_NIF_TERM state_term(ErlNifEnv *env, part_res *p, uint32_t type, uint32_t n,
                                const uint32_t *tag, const uint64_t *tok) {
-    ERL_NIF_TERM l = enif_make_list(env, 0);
+    sort_item *v = enif_alloc(sizeof(sort_item) * (n + 1));
+    if (!v) return 0;
+    uint32_t m = 0;
     if (type == AGN_REGISTER_MV) {
-        for (uint32_t i = n; i-- > 0;)
-            l = enif_make_list_cell(env, enif_make_tuple2(env, id_term(env, p->tags, tag[i]),
-                                                         id_term(env, p->toks, tok[i])), l);
-        return l;
+        for (uint32_t i = 0; i < n; ++i, ++m) {
+            v[m].term = enif_make_tuple2(env, id_term(env, p->tags, tag[i]), id_term(env, p->toks, tok[i]));
+            v[m].key = v[m].term;
+        }
+    } else {
+        /* pairs come grouped by element, tokens in fold order */
+        for (uint32_t i = 0; i < n;) {
+            uint32_t j = i;
+            while (j < n && tag[j] == tag[i]) ++j;
+            ERL_NIF_TERM toks = enif_make_list(env, 0);
+            for (uint32_t x = j; x-- > i;) toks = enif_make_list_cell(env, id_term(env, p->toks, tok[x]), toks);
+            v[m].key = id_term(env, p->tags, tag[i]);
+            v[m].term = enif_make_tuple2(env, v[m].key, toks);
+            ++m;
+            i = j;
+        }
     }
-    /* pairs come grouped by element (sorted), tokens in fold order */
-    uint32_t i = n;
-    while (i > 0) {
-        uint32_t j = i;
-        while (j > 0 && tag[j - 1] == tag[i - 1]) --j;
-        ERL_NIF_TERM toks = enif_make_list(env, 0);
-        for (uint32_t x = i; x-- > j;) toks = enif_make_list_cell(env, id_term(env, p->toks, tok[x]), toks);
-        l = enif_make_list_cell(env, enif_make_tuple2(env, id_term(env, p->tags, tag[i - 1]), toks), l);
-        i = j;
-    }
+    qsort(v, m, sizeof *v, cmp_item);
+    ERL_NIF_TERM l = enif_make_list(env, 0);
+    for (uint32_t i = m; i-- > 0;) l = enif_make_list_cell(env, v[i].term, l);
+    enif_free(v);
     return l;
 }
 
@@ -790,6 +809,7 @@ static ERL_NIF_TERM read_result(ErlNifEnv *env, part_res *p, uint32_t type, uint
     ERL_NIF_TERM v = type == AGN_COUNTER_PN
                          ? enif_make_int64(env, o->value)
                          : state_term(env, p, type, o->out_n, o->out_tag, o->out_tok);
+    if (!v) return error_tuple(env, AGN_ENOMEM);
     ERL_NIF_TERM lct = (o->flags & AGN_F_CT_IGNORE) ? atom(env, "ignore") : clock_pairs(env, p, ct, ctm);
     ERL_NIF_TERM res[6] = {atom(env, "ok"), v, enif_make_int64(env, o->hole), lct,
                            atom(env, (o->flags & AGN_F_NEWSS) ? "true" : "false"),

@@ -1,13 +1,20 @@
 /*
- * Declarations-only stand-in for <erl_nif.h>, used by tests/test_nif_syntax.py
- * to syntax-check nif/antidote_gpu_nif.c with `gcc -fsyntax-only` in an image
- * without Erlang/OTP.  It declares exactly the erl_nif API subset the shim
- * uses, with the documented signatures (erl_nif(3)); it is never linked, and
- * the real header comes with Erlang/OTP where the shim is built (nif/Makefile).
- * Test infrastructure only.
+ * A minimal, runnable stand-in for <erl_nif.h> -- TEST INFRASTRUCTURE ONLY.
+ *
+ * This image has no Erlang/OTP.  The NIF (nif/antidote_gpu_nif.c) is
+ * compiled against this header twice by the tests:
+ *   - `gcc -fsyntax-only -Wall -Wextra -Werror` (tests/test_nif_syntax.py);
+ *   - linked with tests/nif_rt/erl_nif_rt.c, a small term runtime (integers,
+ *     atoms, tuples, lists, binaries, resources with destructors, exceptions,
+ *     enif_term_to_binary as an injective byte encoding), into
+ *     tests/nif_rt/libagn_nif_rt.so, whose NIF functions the GPU tests call
+ *     through ctypes (tests/test_nif_exec.py) -- so the NIF's C runs.
+ * It declares exactly the erl_nif API subset the NIF uses, with the
+ * documented signatures (erl_nif(3)).  Where the NIF is built for real
+ * (nif/Makefile) OTP's own header is used instead.
  */
-#ifndef AGN_ERL_NIF_DECLS_H
-#define AGN_ERL_NIF_DECLS_H
+#ifndef AGN_ERL_NIF_RT_H
+#define AGN_ERL_NIF_RT_H
 #include <stddef.h>
 #include <stdint.h>
 
@@ -54,6 +61,7 @@ int enif_get_list_length(ErlNifEnv *env, ERL_NIF_TERM term, unsigned *len);
 int enif_is_empty_list(ErlNifEnv *env, ERL_NIF_TERM term);
 int enif_is_list(ErlNifEnv *env, ERL_NIF_TERM term);
 int enif_is_identical(ERL_NIF_TERM lhs, ERL_NIF_TERM rhs);
+int enif_compare(ERL_NIF_TERM lhs, ERL_NIF_TERM rhs);
 int enif_inspect_binary(ErlNifEnv *env, ERL_NIF_TERM bin_term, ErlNifBinary *bin);
 int enif_term_to_binary(ErlNifEnv *env, ERL_NIF_TERM term, ErlNifBinary *bin);
 size_t enif_binary_to_term(ErlNifEnv *env, const unsigned char *data, size_t size,
@@ -71,7 +79,16 @@ void *enif_realloc(void *ptr, size_t size);
 void enif_free(void *ptr);
 ERL_NIF_TERM enif_raise_exception(ErlNifEnv *env, ERL_NIF_TERM reason);
 
-#define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                 \
-    static const void *agn_nif_syntax_check_##NAME[] = {(const void *)FUNCS,      \
-                                                        (const void *)LOAD};
+/* The module's function table and load callback, for the runtime's loader
+ * (rt_nif_entry); OTP's macro builds its ErlNifEntry instead. */
+#define ERL_NIF_INIT(NAME, FUNCS, LOAD, RELOAD, UPGRADE, UNLOAD)                       \
+    int rt_nif_entry(const ErlNifFunc **rt_funcs_, int *rt_n_,                         \
+                     int (**rt_load_)(ErlNifEnv *, void **, ERL_NIF_TERM));             \
+    int rt_nif_entry(const ErlNifFunc **rt_funcs_, int *rt_n_,                         \
+                     int (**rt_load_)(ErlNifEnv *, void **, ERL_NIF_TERM)) {            \
+        *rt_funcs_ = FUNCS;                                                            \
+        *rt_n_ = (int)(sizeof(FUNCS) / sizeof((FUNCS)[0]));                            \
+        *rt_load_ = LOAD;                                                              \
+        return 0;                                                                      \
+    }
 #endif

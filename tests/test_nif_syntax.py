@@ -1,6 +1,6 @@
 """The Erlang binding (nif/antidote_gpu_nif.c) cannot be built here (no
 Erlang/OTP, no erl_nif.h); it is at least compiled for syntax and warnings
-against the erl_nif API subset it uses (tests/nif_syntax/erl_nif.h,
+against the erl_nif API subset it uses (tests/nif_rt/erl_nif.h,
 declarations only), and it must bind only symbols include/antidote_gpu.h
 declares."""
 import os
@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc absent")
 def test_nif_compiles_cleanly():
     r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
-                        "-I", os.path.join(ROOT, "tests", "nif_syntax"),
+                        "-I", os.path.join(ROOT, "tests", "nif_rt"),
                         os.path.join(ROOT, "nif", "antidote_gpu_nif.c")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
