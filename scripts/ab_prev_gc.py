@@ -4,7 +4,11 @@ tools/libagn_prev.so (scripts/build_prev.sh), one process, interleaved rounds,
 the same device log / thresholds / output arrays for both; the outputs must
 be identical.
 
-  python scripts/ab_prev_gc.py [config=3]
+  python scripts/ab_prev_gc.py [config=3] [name=path ...]
+
+name=path: more libraries (default prev=tools/libagn_prev.so), e.g. the
+diagnostic builds of scripts/build_diag_gc.sh (their outputs differ by
+design: `identical` is reported, not asserted).
 """
 import ctypes as C
 import os
@@ -25,10 +29,14 @@ K, D, N = cfg["n_keys"], cfg["n_dcs"], cfg["ops_per_key"]
 E = K * N
 tags = cfg["crdt_type"] != 1
 eng = Engine(0)
-prev = C.CDLL(os.path.join(ROOT, "tools", "libagn_prev.so"), mode=os.RTLD_LOCAL)
-_abi.bind(prev, {k: v for k, v in _abi.PROTOTYPES.items() if hasattr(prev, k)})
-pctx = C.c_void_p()
-assert prev.agn_open(0, C.byref(pctx)) == 0
+LIBS = {}
+for a in (sys.argv[2:] or ["prev=tools/libagn_prev.so"]):
+    name, path = a.split("=", 1)
+    lib = C.CDLL(os.path.join(ROOT, path), mode=os.RTLD_LOCAL)
+    _abi.bind(lib, {k: v for k, v in _abi.PROTOTYPES.items() if hasattr(lib, k)})
+    ctx = C.c_void_p()
+    assert lib.agn_open(0, C.byref(ctx)) == 0
+    LIBS[name] = (lib, ctx)
 sp = torch.cuda.current_stream().cuda_stream
 g = _abi.AgnGenCfg(crdt_type=cfg["crdt_type"], n_dcs=D, n_keys=K, ops_per_key=N,
                    n_elems=cfg["n_elems"], seed=cfg["seed"], key_base=0, key_stride=1, warm=0)
@@ -57,8 +65,8 @@ def run(lib):
         rc = eng.lib.agn_prune_ops(eng.ctx, C.byref(dl), None, dr.R, None, C.byref(s), None,
                                    tot.ptr, sp)
     else:
-        rc = prev.agn_prune_ops(pctx, C.byref(dl), None, dr.R, None, C.byref(s), None, tot.ptr,
-                                sp)
+        lib, ctx = LIBS[lib]
+        rc = lib.agn_prune_ops(ctx, C.byref(dl), None, dr.R, None, C.byref(s), None, tot.ptr, sp)
     assert rc == 0
 
 
@@ -68,10 +76,11 @@ def snapshot():
         {"key_len": eng.download(key_len, np.uint64, (K,))}
 
 
-times = {"cur": [], "prev": []}
+names = ["cur"] + list(LIBS)
+times = {v: [] for v in names}
 outs = {}
 for rnd in range(10):
-    for v in (("cur", "prev") if rnd % 2 == 0 else ("prev", "cur")):
+    for v in names[rnd % len(names):] + names[:rnd % len(names)]:
         b, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         b.record()
         run(v)
@@ -81,12 +90,12 @@ for rnd in range(10):
             times[v].append(b.elapsed_time(e))
         if rnd == 0:
             outs[v] = snapshot()
-same = all(np.array_equal(outs["cur"][n], outs["prev"][n]) for n in outs["cur"])
 kept, kept_rem = (int(x) for x in eng.download(tot, np.uint64, (2,)))
 per_f = 4 + 8 + (16 if tags else 8)
 alg = E * 8 * D + kept * per_f * 2 + kept * 8 * D + 16 * kept_rem + K * (8 + 8 * D + 16)
 for v, t in times.items():
     ms = float(np.median(t))
+    same = all(np.array_equal(outs["cur"][n], outs[v][n]) for n in outs["cur"])
     print(f"cfg{c} gc {v:5s} median {ms:.3f} ms  min {min(t):.3f}  "
           f"{alg / ms / 1e6:.0f} GB/s  {alg / ms / 1e6 / HBM_PEAK_GBS:.3f} of 8 TB/s  identical={same}",
           flush=True)
