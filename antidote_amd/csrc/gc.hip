@@ -324,6 +324,46 @@ __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32
 
 constexpr int PT = 4;  // removal tokens a lane buffers per entry
 
+// Staged field stores (k_prune_inplace, set/register): the kept entries' per-entry fields
+// (op id, txid, effect or tag + add token + token start) go to a per-wave LDS
+// ring and leave it in runs of 33-64 entries whose ends fall on 32-entry
+// (128-byte) boundaries, lane = entry: every interior line of the field
+// arrays is written whole by one store instruction, where the head lanes of
+// an iteration stored <= 32 scattered words each (every other lane at
+// LPO = 2) and left partial lines at both ends of every iteration.  Delaying
+// a store is safe in place: a destination is never above its source and
+// later iterations read only higher sources.  AGN_PRUNE_STAGE=0 at build time
+// keeps the direct stores (A/B).
+#ifndef AGN_PRUNE_STAGE
+#define AGN_PRUNE_STAGE 1
+#endif
+constexpr bool PRUNE_STAGE = AGN_PRUNE_STAGE != 0;
+constexpr uint32_t SRING = 128;  // ring slots: < 64 pending + one iteration's kept
+
+// The kept entries' removal tokens the same way (set/register, lists of <= PT
+// tokens): a 512-token ring leaving in runs of 113-128 tokens that end on a
+// 16-token (128-byte) boundary; an iteration that copies its lists another
+// way (longer lists, AGN_PRUNE_TCOOP) first empties the ring.
+// AGN_PRUNE_STAGE_TOK=0 at build time keeps the direct token stores (A/B).
+#ifndef AGN_PRUNE_STAGE_TOK
+#define AGN_PRUNE_STAGE_TOK 1
+#endif
+constexpr uint32_t TRING = 512;
+template <bool ON>
+struct TokRing {
+    uint64_t t[ON ? TRING : 1];
+};
+
+template <bool ON>
+struct FieldRing {
+    static constexpr uint32_t N = ON ? SRING : 1u;
+    uint64_t tx[N];
+    uint64_t w64[N];  // add token (set/register) or effect (counter)
+    uint32_t id[N];
+    uint32_t tg[N];   // set/register: tag
+    uint32_t ro[N];   // set/register: the entry's token start
+};
+
 // CTL (dense rows, 8 DCs per lane-slice): an iteration's rows are read
 // lane-contiguously -- load j covers bytes [1 KiB j, 1 KiB (j+1)), whole
 // lines, lane l holding DCs 2p, 2p+1 (p = l mod P, P = D / 2) of op
@@ -357,6 +397,14 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
     const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     const uint32_t D = a.D, W = a.W;
     constexpr bool tags = TAGS;
+    // staged stores for set/register (counter_pn: measured 0.7 % slower on
+    // cfg2's GC, profiles/r06/ab_gc_staged_cfg2.log)
+    constexpr bool STG = PRUNE_STAGE && TAGS;
+    __shared__ FieldRing<STG> rings[STG ? WPB : 1];
+    FieldRing<STG> &ring = rings[(STG && WPB > 1) ? (threadIdx.x >> 6) : 0];
+    constexpr bool STOK = STG && AGN_PRUNE_STAGE_TOK;
+    __shared__ TokRing<STOK> trings[STOK ? WPB : 1];
+    TokRing<STOK> &tring = trings[(STOK && WPB > 1) ? (threadIdx.x >> 6) : 0];
     // The key's metadata: one group of unconditional scalar loads (absent
     // columns from an in-bounds dummy) through the scalar cache (ldc) -- each
     // of these words is read by the key's own wave before that wave writes
@@ -411,6 +459,38 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
     uint64_t written = 0;
     uint32_t rwritten = 0, first_id = AGN_ID0_NONE, last_id = 0;
     bool consec = true;
+    // staged fields: ring head slot, pending entries, destination of the head
+    uint32_t sh = 0, sp = 0;
+    uint64_t sbase = off;
+    // lanes < cnt store the ring's first cnt pending entries (lane = entry)
+    auto flush = [&](uint32_t cnt) {
+        if ((uint32_t)lane < cnt) {
+            const uint32_t q = (sh + (uint32_t)lane) & (SRING - 1u);
+            const uint64_t d = sbase + (uint64_t)lane;
+            a.d_op_id[d] = ring.id[q];
+            if (a.d_txid) a.d_txid[d] = ring.tx[q];
+            if constexpr (TAGS) {
+                a.d_tag[d] = ring.tg[q];
+                a.d_add[d] = ring.w64[q];
+                a.d_rem_off[d] = ring.ro[q];
+            } else {
+                a.d_eff[d] = (int64_t)ring.w64[q];
+            }
+        }
+        sh = (sh + cnt) & (SRING - 1u);
+        sp -= cnt;
+        sbase += cnt;
+    };
+    // staged tokens: ring head slot, pending tokens, destination of the head
+    uint32_t th = 0, tp = 0, tsbase = tb;
+    auto tflush = [&](uint32_t cnt) {
+        for (uint32_t c = 0; c < cnt; c += AGN_WAVE)
+            if (c + (uint32_t)lane < cnt)
+                a.d_tok[tsbase + c + (uint32_t)lane] = tring.t[(th + c + (uint32_t)lane) & (TRING - 1u)];
+        th = (th + cnt) & (TRING - 1u);
+        tp -= cnt;
+        tsbase += cnt;
+    };
     // PF: the next iteration's rows are requested once this iteration's
     // filter has decided, so they are in flight while its fields, removal
     // tokens and stores wait (the next rows are above every destination of
@@ -638,7 +718,20 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             __builtin_amdgcn_wave_barrier();
             if (kp && (uint32_t)sub < W) a.d_mask[dst * W + (uint32_t)sub] = mw;
         }
-        if (head) {
+        if (STG) {
+            if (head) {
+                const uint32_t q = (sh + sp + rank) & (SRING - 1u);
+                ring.id[q] = id;
+                ring.tx[q] = tx;
+                if constexpr (TAGS) {
+                    ring.tg[q] = tg;
+                    ring.w64[q] = ad;
+                    ring.ro[q] = tdst;
+                } else {
+                    ring.w64[q] = (uint64_t)ef;
+                }
+            }
+        } else if (head) {
             a.d_op_id[dst] = id;
             if (a.d_txid) a.d_txid[dst] = tx;
             if constexpr (TAGS) {
@@ -647,6 +740,11 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             } else {
                 a.d_eff[dst] = ef;
             }
+        }
+        if (STOK && (coop || long_list) && tp) {
+            tflush(tp);  // the other copies start right after the ring's range
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
         if (tags) {
             if (coop) {
@@ -660,7 +758,14 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
                     coop_store(base);
                 }
             } else if (!long_list) {
-                if (head) {
+                if (STOK) {
+                    if (head) {
+#pragma unroll
+                        for (int x = 0; x < PT; ++x)
+                            if ((uint32_t)x < rl_)
+                                tring.t[(th + (tdst - tsbase) + (uint32_t)x) & (TRING - 1u)] = tk[x];
+                    }
+                } else if (head) {
 #pragma unroll
                     for (int x = 0; x < PT; ++x)
                         if ((uint32_t)x < rl_) a.d_tok[tdst + x] = tk[x];
@@ -685,11 +790,15 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
                     }
                 }
             }
-            if (head) {
+            if (!STG && head) {
                 a.d_rem_off[dst] = tdst;
                 a.d_rem_off[dst + 1] = tdst + rl_;
             }
             rwritten += (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
+            if (STOK) {
+                if (coop || long_list) tsbase = tb + rwritten;  // copied directly
+                else tp += T;
+            }
         }
         // consecutive-id index over the kept ids, in position order
         if (nk) {
@@ -707,6 +816,28 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
         written += nk;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        if (STOK) {
+            while (tp >= 2u * (uint32_t)AGN_WAVE) {
+                tflush(2u * (uint32_t)AGN_WAVE - ((tsbase + 2u * (uint32_t)AGN_WAVE) & 15u));
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (STG) {
+            sp += nk;
+            // runs ending on a 32-entry boundary: 33..64 entries
+            while (sp >= (uint32_t)AGN_WAVE) {
+                flush((uint32_t)AGN_WAVE - (uint32_t)((sbase + (uint64_t)AGN_WAVE) & 31u));
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+    if (STOK) tflush(tp);
+    if (STG) {
+        flush(sp);
+        // the token end of the last kept entry (each staged entry carried its start)
+        if (tags && lane == 0) a.d_rem_off[off + written] = tb + rwritten;
     }
     if (lane == 0) {
         const uint32_t l = (uint32_t)written;
@@ -719,7 +850,7 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
         a.d_key_len[k] = written;
         if (a.key_id0) a.key_id0[k] = id0;
         if (a.key_lcap) a.key_lcap[k] = lc;
-        if (tags && l == 0) a.d_rem_off[off] = tb;  // an empty segment keeps its token base
+        if (tags && l == 0 && !STG) a.d_rem_off[off] = tb;  // an empty segment keeps its token base
         if (meta) {
             meta[i] = l;
             meta[K + i] = rwritten;

@@ -29,9 +29,14 @@ K, D, N = cfg["n_keys"], cfg["n_dcs"], cfg["ops_per_key"]
 E = K * N
 tags = cfg["crdt_type"] != 1
 eng = Engine(0)
-LIBS = {}
+from antidote_amd._lib import env_changed  # noqa: E402
+
+LIBS, ENVS = {}, {}
 for a in (sys.argv[2:] or ["prev=tools/libagn_prev.so"]):
     name, path = a.split("=", 1)
+    if path.startswith("env:"):  # name=env:K=V[,K=V]: the current library with knobs
+        ENVS[name] = dict(kv.split("=", 1) for kv in path[4:].split(","))
+        continue
     lib = C.CDLL(os.path.join(ROOT, path), mode=os.RTLD_LOCAL)
     _abi.bind(lib, {k: v for k, v in _abi.PROTOTYPES.items() if hasattr(lib, k)})
     ctx = C.c_void_p()
@@ -60,8 +65,16 @@ s.key_len = key_len.ptr
 tot = eng.empty(16)
 
 
+KNOBS = {k for e in ENVS.values() for k in e}
+
+
 def run(lib):
-    if lib == "cur":
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    if lib in ENVS:
+        os.environ.update(ENVS[lib])
+    env_changed()
+    if lib == "cur" or lib in ENVS:
         rc = eng.lib.agn_prune_ops(eng.ctx, C.byref(dl), None, dr.R, None, C.byref(s), None,
                                    tot.ptr, sp)
     else:
@@ -76,7 +89,7 @@ def snapshot():
         {"key_len": eng.download(key_len, np.uint64, (K,))}
 
 
-names = ["cur"] + list(LIBS)
+names = ["cur"] + list(LIBS) + list(ENVS)
 times = {v: [] for v in names}
 outs = {}
 for rnd in range(10):

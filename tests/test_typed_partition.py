@@ -273,6 +273,15 @@ def test_typed_partition_vs_reference(eng, seed):
                 assert (int(ln[k]), int(ll[k])) == tuple(vn.ops_cache[k][1]), (t, k)
     finally:
         part.close()
-    print(f"served={served} raised={raised} mixed={len(mixed)} diverged={len(diverged)} "
-          f"quirk={len(quirk)} mistyped_log_reads={log_typed}")
-    assert served > 400 and raised > 30 and len(quirk) <= K // 4, (served, raised, len(quirk))
+    got = dict(served=served, raised=raised, mixed=len(mixed), diverged=len(diverged),
+               quirk=len(quirk), mistyped_log_reads=log_typed)
+    print(" ".join(f"{k}={v}" for k, v in got.items()))
+    # the workload is deterministic: every count -- the excluded keys included
+    # (`diverged` only ever holds keys that got an op of another type, asserted
+    # above) -- is pinned, so a regression that moved a key in or out of the
+    # comparison shows (profiles/r06: the GPU run that recorded them)
+    assert got == EXPECT[seed], (got, EXPECT[seed])
+
+
+EXPECT = {1: dict(served=662, raised=71, mixed=3, diverged=3, quirk=0, mistyped_log_reads=3),
+          2: dict(served=631, raised=100, mixed=3, diverged=3, quirk=0, mistyped_log_reads=5)}
