@@ -310,9 +310,6 @@ struct InplaceArgs {
     // engine-owned log: meta has 6 rows, the last two the key's live range
     // start after the prune (entry slot, token slot; arenas < 2^32 slots)
     int meta6;
-    // set/register removal tokens of an iteration's kept entries copied by
-    // the whole wave (lane = token) instead of by each entry's head lane
-    int tcoop;
 };
 
 __device__ __forceinline__ uint32_t resize_list_len_dev(uint32_t new_len, uint32_t list_len) {
@@ -343,7 +340,7 @@ constexpr uint32_t SRING = 128;  // ring slots: < 64 pending + one iteration's k
 // The kept entries' removal tokens the same way (set/register, lists of <= PT
 // tokens): a 512-token ring leaving in runs of 113-128 tokens that end on a
 // 16-token (128-byte) boundary; an iteration that copies its lists another
-// way (longer lists, AGN_PRUNE_TCOOP) first empties the ring.
+// way (a list longer than PT) first empties the ring.
 // AGN_PRUNE_STAGE_TOK=0 at build time keeps the direct token stores (A/B).
 #ifndef AGN_PRUNE_STAGE_TOK
 #define AGN_PRUNE_STAGE_TOK 1
@@ -643,43 +640,8 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
         }
         const uint32_t tdst = tb + rwritten + (tincl - rl_);
         const uint32_t T = tags ? (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63) : 0u;
-        // tcoop: the iteration's kept tokens as one run, lane = token (its
-        // owner entry by a binary search over the lanes' inclusive scan),
-        // TM per lane per round -- one round trip for the whole iteration
-        // where the head-lane copy serialises one round trip per kept entry
-        // once any list is longer than PT.  In place a token's destination
-        // is never above its source and sources rise with the token index,
-        // so a round's stores never reach a later round's sources
-        constexpr int TM = 4;
-        const bool coop = tags && a.tcoop;
-        uint64_t cv[TM];
-        auto coop_load = [&](uint32_t base) {
-#pragma unroll
-            for (int m = 0; m < TM; ++m) {
-                const uint32_t t = base + (uint32_t)(m * AGN_WAVE + lane);
-                int lo = 0;  // first lane whose inclusive count exceeds t
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1) {
-                    const uint32_t v = (uint32_t)__shfl((int)tincl, lo + step - 1, AGN_WAVE);
-                    lo = v <= t ? lo + step : lo;
-                }
-                const int ow = lo < AGN_WAVE ? lo : AGN_WAVE - 1;
-                const uint32_t o0 = (uint32_t)__shfl((int)r0, ow, AGN_WAVE);
-                const uint32_t oi = (uint32_t)__shfl((int)tincl, ow, AGN_WAVE);
-                const uint32_t ol = (uint32_t)__shfl((int)rl_, ow, AGN_WAVE);
-                cv[m] = t < T ? a.tok[o0 + (t - (oi - ol))] : 0ull;
-            }
-        };
-        auto coop_store = [&](uint32_t base) {
-#pragma unroll
-            for (int m = 0; m < TM; ++m) {
-                const uint32_t t = base + (uint32_t)(m * AGN_WAVE + lane);
-                if (t < T) a.d_tok[tb + rwritten + t] = cv[m];
-            }
-        };
-        if (coop) coop_load(0u);
-        const bool long_list = tags && !coop && ballot(head && rl_ > (uint32_t)PT) != 0ull;
-        if (tags && !coop && !long_list && head) {
+        const bool long_list = tags && ballot(head && rl_ > (uint32_t)PT) != 0ull;
+        if (tags && !long_list && head) {
 #pragma unroll
             for (int x = 0; x < PT; ++x) tk[x] = (uint32_t)x < rl_ ? a.tok[r0 + x] : 0ull;
         }
@@ -741,23 +703,13 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
                 a.d_eff[dst] = ef;
             }
         }
-        if (STOK && (coop || long_list) && tp) {
+        if (STOK && long_list && tp) {
             tflush(tp);  // the other copies start right after the ring's range
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
         }
         if (tags) {
-            if (coop) {
-                coop_store(0u);
-                for (uint32_t base = TM * AGN_WAVE; base < T; base += TM * AGN_WAVE) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    coop_load(base);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    coop_store(base);
-                }
-            } else if (!long_list) {
+            if (!long_list) {
                 if (STOK) {
                     if (head) {
 #pragma unroll
@@ -796,7 +748,7 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
             }
             rwritten += (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
             if (STOK) {
-                if (coop || long_list) tsbase = tb + rwritten;  // copied directly
+                if (long_list) tsbase = tb + rwritten;  // copied directly
                 else tp += T;
             }
         }
@@ -1582,8 +1534,6 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.xcd = xcd_remap() ? 1 : 0;
     const char *lf = AGN_KNOB("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
-    const char *tc = AGN_KNOB("AGN_PRUNE_TCOOP");  // A/B knob: 0 | 1
-    a.tcoop = (tc && tc[0] == '1') ? 1 : 0;
     a.meta6 = 0;
     return a;
 }

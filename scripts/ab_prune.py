@@ -58,10 +58,6 @@ def main():
                 ("ct", {"AGN_PRUNE_CT": "1", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "1"}),
                 ("pf4", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "1", "AGN_PRUNE_MINW": "1"}),
                 ("pf_ef", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "3", "AGN_PRUNE_MINW": "1"}),
-                ("pf_tcoop", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "1", "AGN_PRUNE_MINW": "1",
-                              "AGN_PRUNE_TCOOP": "1"}),
-                ("ef_tcoop", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "3", "AGN_PRUNE_MINW": "1",
-                              "AGN_PRUNE_TCOOP": "1"}),
                 ("mw6", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "6"}),
                 ("mw8", {"AGN_PRUNE_CT": "0", "AGN_PRUNE_PF": "0", "AGN_PRUNE_MINW": "8"})]
     os.environ["AGN_PRUNE_WPB"] = "1"
@@ -71,7 +67,7 @@ def main():
     chk = ["key_len", "oc", "op_id"] + (["eff"] if cfg["crdt_type"] == 1 else ["tag", "add_tok", "rem_tok"])
     for r in range(rounds):
         for name, env in (variants if r % 2 == 0 else variants[::-1]):
-            os.environ.update({"AGN_PRUNE_TCOOP": "0", **env})
+            os.environ.update(env)
             env_changed()
             eng.prune_ops(din, None, dr.R, None, out)
             torch.cuda.synchronize()

@@ -155,7 +155,7 @@ def test_prune_gpu_vs_oracle(eng, oracle_lib, crdt, D, sparse):
 @pytest.mark.parametrize("crdt,D,sparse", CASES + [(_abi.COUNTER_PN, 256, True),
                                                    (_abi.SET_AW, 100, False),
                                                    (_abi.COUNTER_PN, 8, False)])
-@pytest.mark.parametrize("ct", ["0", "1", "pf0", "pf1", "pf2", "pf3", "mw8", "tc1"])
+@pytest.mark.parametrize("ct", ["0", "1", "pf0", "pf1", "pf2", "pf3", "mw8"])
 def test_prune_segmented_gpu_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sparse, ct):
     """agn_prune_ops with out.key_len: the one-pass segmented form -- every
     key's kept entries at its input segment start, bit-exact with the
@@ -164,8 +164,7 @@ def test_prune_segmented_gpu_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sp
     "pf1" / "pf2": the next iteration's rows prefetched (AGN_PRUNE_PF; "pf3"
     with the next fields predicted; "pf0" none, the default being 1 for
     set/register); "mw8":
-    the register budget of 8 waves per SIMD (AGN_PRUNE_MINW, spills); "tc1":
-    removal tokens copied by the whole wave (AGN_PRUNE_TCOOP)."""
+    the register budget of 8 waves per SIMD (AGN_PRUNE_MINW, spills)."""
     from test_id_index import expected_index
     monkeypatch.setenv("AGN_PRUNE_CT", ct if ct in ("0", "1") else "0")
     if ct.startswith("pf"):
@@ -173,7 +172,6 @@ def test_prune_segmented_gpu_vs_oracle(eng, oracle_lib, monkeypatch, crdt, D, sp
     else:
         monkeypatch.delenv("AGN_PRUNE_PF", raising=False)
     monkeypatch.setenv("AGN_PRUNE_MINW", ct[2:] if ct.startswith("mw") else "1")
-    monkeypatch.setenv("AGN_PRUNE_TCOOP", "1" if ct == "tc1" else "0")
     log, _req, _ = random_case(91 * D + crdt + sparse, crdt, 200, D, 150 if D <= 16 else 60,
                                sparse=sparse, multi=0.2 if crdt == _abi.SET_AW else 0.0,
                                empty=0.1, txid=0.3)
