@@ -36,7 +36,12 @@ def main():
     print(f"{'line':18s} {'bench kernel_ms':>15s} {'trace mean ms':>13s} {'launches':>8s} {'ratio':>6s}  frac")
     for name, pat in KERNELS.items():
         x = lines.get(name)
-        if not x or "roofline" not in x:
+        if not x:
+            continue
+        # full sub-lines carry a roofline object; the final line's compact
+        # summaries (bench.compact_line) carry kernel_ms / frac directly
+        roof = x.get("roofline") or x
+        if "kernel_ms" not in roof:
             continue
         dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
                for r in rows if pat in r["Kernel_Name"]]
@@ -44,10 +49,10 @@ def main():
             print(f"{name:18s} no trace launches for {pat!r}")
             continue
         full = [t for t in dur if t >= max(dur) / 2]
-        km = x["roofline"]["kernel_ms"]
+        km = roof["kernel_ms"]
         mean = statistics.mean(full)
         print(f"{name:18s} {km:15.4f} {mean:13.4f} {len(full):8d} {km / mean:6.3f}  "
-              f"{x['roofline']['frac']:.3f}")
+              f"{roof['frac']:.3f}")
 
 
 if __name__ == "__main__":
