@@ -459,6 +459,7 @@ def summarize_sub(sub):
             "algorithmic_bytes": alg, "traffic": traffic,
             "traffic_ratio": traffic / alg if traffic and alg else None,
             "cpu_value": cpu.get("value"),
+            **({"exchange_verified": sub["exchange_verified"]} if "exchange_verified" in sub else {}),
             "workload": _short(sub.get("config", {}).get("workload"), 120)}
 
 
@@ -480,6 +481,9 @@ def compact_line(line, detail_path=None):
         out["cpu_baseline"] = cpu
     build = line.get("build") or {}
     out["build"] = {k: build[k] for k in ("lib_sha16", "csrc_sha16") if k in build}
+    if line.get("gst"):  # N > 1: the collective's own check and its epoch
+        out["gst"] = {k: line["gst"][k] for k in ("exchange", "exchange_verified", "rccl_ranks",
+                                                   "epoch_latency_us") if k in line["gst"]}
     if line.get("configs"):
         out["configs"] = {n: summarize_sub(s) for n, s in line["configs"].items()}
     if detail_path:

@@ -107,3 +107,13 @@ def test_final_line_fits_driver_tail():
     big = dict(full, configs={f"c{i}": full["configs"]["cfg3_gc"] for i in range(60)})
     out = bench.compact_line(big)
     assert len(json.dumps(out)) < 8000 and out["roofline"]["frac"] == full["roofline"]["frac"]
+
+
+def test_final_line_keeps_the_exchange_check():
+    """N > 1: the GST exchange's own verification survives the compaction
+    (the headline's gst object and cfg5's sub-line)."""
+    full = json.load(open(os.path.join(ROOT, "profiles", "r06", "bench_n2_gloo_detail.json")))
+    out = bench.compact_line(full)
+    assert len(json.dumps(out)) < 8000
+    assert out["gst"]["exchange_verified"] is True and out["n_gpus"] == 2
+    assert out["configs"]["cfg5"]["exchange_verified"] is True
