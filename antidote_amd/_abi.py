@@ -184,6 +184,7 @@ PROTOTYPES = {
                                   C.POINTER(C.c_uint64)]),
     "agn_oplog_key_meta": (C.c_int, [P, C.c_uint64, P, P, P, P]),
     "agn_oplog_gc_due": (C.c_int, [P, C.c_uint64, P, P]),
+    "agn_oplog_set_counter": (C.c_int, [P, C.c_uint64, P, P]),
     "agn_interner_create": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(P)]),
     "agn_interner_destroy": (C.c_int, [P]),
     "agn_intern": (C.c_int, [P, P, C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
     constexpr bool tags = TAGS;
     // staged stores for set/register (counter_pn: measured 0.7 % slower on
     // cfg2's GC, profiles/r06/ab_gc_staged_cfg2.log)
-    constexpr bool STG = PRUNE_STAGE && TAGS;
+    constexpr bool STG = PRUNE_STAGE && TAGS && MINW < 6;  // (the register-budget A/B forms: direct)
     __shared__ FieldRing<STG> rings[STG ? WPB : 1];
     FieldRing<STG> &ring = rings[(STG && WPB > 1) ? (threadIdx.x >> 6) : 0];
     constexpr bool STOK = STG && AGN_PRUNE_STAGE_TOK;

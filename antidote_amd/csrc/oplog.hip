@@ -979,6 +979,17 @@ int agn_oplog_stats(const agn_oplog *Lc, uint64_t *entries, uint64_t *slots, uin
     return AGN_OK;
 }
 
+int agn_oplog_set_counter(agn_oplog *L, uint64_t n, const uint64_t *keys, const uint32_t *counter) {
+    if (!L) return fail(AGN_EINVAL, "oplog_set_counter: null oplog");
+    if (n && (!keys || !counter)) return fail(AGN_EINVAL, "oplog_set_counter: null argument");
+    std::lock_guard<std::mutex> g(L->wmu);
+    for (uint64_t i = 0; i < n; ++i)
+        if (keys[i] >= L->K)
+            return fail(AGN_EINVAL, "oplog_set_counter: key %llu >= n_keys", (unsigned long long)keys[i]);
+    for (uint64_t i = 0; i < n; ++i) L->counter[keys[i]] = counter[i];
+    return AGN_OK;
+}
+
 int agn_oplog_key_meta(agn_oplog *L, uint64_t n, const uint64_t *keys, uint32_t *out_len,
                        uint32_t *out_list_len, uint32_t *out_counter) {
     if (!L) return fail(AGN_EINVAL, "oplog_key_meta: null oplog");

@@ -415,6 +415,14 @@ class OpLog:
               "agn_oplog_gc_due")
         return out.astype(bool)
 
+    def set_counter(self, keys, counters):
+        """agn_oplog_set_counter: each key's op counter (the next op gets
+        counter + 1) -- one counter per key across several logs."""
+        keys = np.ascontiguousarray(np.atleast_1d(keys), np.uint64)
+        ctr = np.ascontiguousarray(np.atleast_1d(counters), np.uint32)
+        check(self.eng.lib.agn_oplog_set_counter(self.h, len(keys), _ptr(keys), _ptr(ctr)),
+              "agn_oplog_set_counter")
+
     def key_meta(self, keys=None):
         """Per key: (Length, ListLen, op counter) of the ETS tuple it mirrors."""
         keys = np.arange(self.n_keys, dtype=np.uint64) if keys is None else \

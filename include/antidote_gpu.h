@@ -360,6 +360,15 @@ int agn_oplog_key_meta(agn_oplog *log, uint64_t n, const uint64_t *keys, uint32_
  * (agn_oplog_append's out_gc_due reports the same condition, but the entry is
  * then already in the log.) */
 int agn_oplog_gc_due(agn_oplog *log, uint64_t n, const uint64_t *keys, uint8_t *out_due);
+/* Sets each key's op counter (element 3 of the ETS tuple, :630): the next
+ * op appended to the key gets counter + 1.  For a caller that keeps one
+ * counter per key across several logs -- the NIF's partition holds one log
+ * per CRDT type where the reference keeps ONE tuple per key for every type
+ * (:621-647) -- so op ids (and op_insert_gc's NewId rem OPS_THRESHOLD
+ * trigger) follow the reference's single counter.  Ids may then have gaps in
+ * one log (the consecutive-id index drops such keys by itself). */
+int agn_oplog_set_counter(agn_oplog *log, uint64_t n, const uint64_t *keys,
+                          const uint32_t *counter);
 /* Batched materialize/4 over the oplog's current contents (req / out as
  * agn_materialize, device pointers, req->keys indexing the oplog's keys).
  * Staged appends are flushed first (read-your-writes: update/2 is a

@@ -105,6 +105,7 @@ typedef struct {
 } part_sub;
 
 #define NTYPES 4 /* indexed by AGN_COUNTER_PN .. AGN_REGISTER_MV */
+#define NO_HOME 0xFFu
 
 typedef struct {
     ctx_res *ctx;           /* kept alive while the partition lives */
@@ -114,6 +115,14 @@ typedef struct {
     uint32_t type, D, W;    /* type: the one part_open created */
     uint64_t K;
     int cached;
+    /* The reference keeps ONE ETS tuple per key for every type (:621-647):
+     * one op counter (element 3, :630) and one {Length, ListLen}.  Per key:
+     * the counter across this partition's per-type logs (set on a log before
+     * each append, agn_oplog_set_counter) and the type of the key's first op,
+     * whose log's ListLen is the tuple's (only a GC read changes ListLen, and
+     * one over ops of two types raises). */
+    uint32_t *kcnt;
+    uint8_t *khome;         /* NO_HOME until the key's first op */
     pthread_mutex_t gc_mu;
     /* the original effect term (external format) of every op whose effect the
      * engine could not encode (an invalid entry), by (key, type, op id): a read
@@ -218,6 +227,8 @@ static void part_dtor(ErlNifEnv *env, void *obj) {
     pthread_mutex_destroy(&p->sub_mu);
     for (size_t i = 0; i < p->n_inv; ++i) enif_release_binary(&p->inv[i].eff);
     enif_free(p->inv);
+    enif_free(p->kcnt);
+    enif_free(p->khome);
     pthread_mutex_destroy(&p->inv_mu);
     if (p->ctx) enif_release_resource(p->ctx);
 }
@@ -575,6 +586,14 @@ static ERL_NIF_TERM nif_part_open(ErlNifEnv *env, int argc, const ERL_NIF_TERM a
     p->ctx = c;
     enif_keep_resource(c);
     part_sub *s;
+    p->kcnt = enif_alloc(K * sizeof *p->kcnt);
+    p->khome = enif_alloc(K);
+    if (!p->kcnt || !p->khome) {
+        enif_release_resource(p);  /* the destructor frees what was allocated */
+        return error_tuple(env, AGN_ENOMEM);
+    }
+    memset(p->kcnt, 0, K * sizeof *p->kcnt);
+    memset(p->khome, NO_HOME, K);
     int rc = agn_interner_create(1, K, &p->keys);
     if (!rc) rc = agn_interner_create(1, D, &p->dcs);
     if (!rc) rc = agn_interner_create(1, UINT64_MAX / 2, &p->txids);
@@ -728,13 +747,12 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
         memcpy(oc + (size_t)i * D, row, D * 8);
         memcpy(ocm + (size_t)i * W, mask, W * 8);
     }
+    /* the key's one counter across the per-type logs (the ETS tuple's) */
+    rc = agn_oplog_set_counter(sb->log, 1, &k, &p->kcnt[k]);
     /* an invalid op's effect term is recorded under the id the append gives
      * it (the key's op counter + 1; one writer) before a read can see it */
-    uint32_t next = 0;
-    if (invalid) {
-        rc = agn_oplog_key_meta(sb->log, 1, &k, NULL, NULL, &next);
-        if (!rc) rc = inv_put(env, p, k, type, next + 1, argv[5]);
-    }
+    const uint32_t next = p->kcnt[k];
+    if (!rc && invalid) rc = inv_put(env, p, k, type, next + 1, argv[5]);
     if (!rc)
         rc = agn_oplog_append(sb->log, n, keys, same, oc, ocm, txids,
                               type == AGN_COUNTER_PN ? eff : NULL,
@@ -743,6 +761,10 @@ static ERL_NIF_TERM nif_part_update(ErlNifEnv *env, int argc, const ERL_NIF_TERM
                               type == AGN_COUNTER_PN ? NULL : E->rem_off,
                               type == AGN_COUNTER_PN ? NULL : E->rem, ids, due);
     if (rc && invalid) inv_drop(p, k, type, next + 1);
+    if (!rc) {
+        p->kcnt[k] = ids[0];
+        if (p->khome[k] == NO_HOME) p->khome[k] = (uint8_t)type;
+    }
     enif_free(E);
     enif_free(oc);
     enif_free(ocm);
@@ -896,7 +918,12 @@ static ERL_NIF_TERM part_read_common(ErlNifEnv *env, part_res *p, ERL_NIF_TERM k
     int other = 0;
     rc = other_type_ops(p, k, type, &other);
     if (rc) return error_tuple(env, rc);
-    if (other) return enif_raise_exception(env, atom(env, "corrupted_ops_cache"));
+    if (other) {
+        /* op_insert_gc's GC read: the op's id was taken (ets:update_counter,
+         * :630) before the read (:640) raises, so the next op's id is one on */
+        if (gc) p->kcnt[k]++;
+        return enif_raise_exception(env, atom(env, "corrupted_ops_cache"));
+    }
     part_sub *sb = sub_get(p, type);
     if (!sb) {
         /* no op of this type was ever written: materialize/4 of an empty ops
@@ -1092,14 +1119,32 @@ static ERL_NIF_TERM nif_part_gc_due(ErlNifEnv *env, int argc, const ERL_NIF_TERM
     part_res *p;
     uint32_t type;
     uint64_t k;
-    uint8_t due = 0;
     if (argc != 3 || !get_part(env, argv[0], &p) || !type_of(env, argv[2], &type))
         return enif_make_badarg(env);
     int rc = key_index(env, p, argv[1], &k);
-    part_sub *s = sub_get(p, type);
-    /* no log of the type yet: the key's first op (id 1, Length 0) is not due */
-    if (!rc && s) rc = agn_oplog_gc_due(s->log, 1, &k, &due);
     if (rc) return error_tuple(env, rc);
+    /* op_insert_gc's trigger for the key's next op (:635) on the ONE tuple the
+     * reference keeps per key: Length = its ops of every type, ListLen = the
+     * home type's log's, NewId = the shared counter + 1.  For a key whose ops
+     * are all of one type this is that log's own agn_oplog_gc_due.  A key
+     * with no op yet (id 1, Length 0 < ListLen) is not due; nor is the op
+     * Type's own -- the trigger does not depend on the new op's type. */
+    (void)type;
+    uint8_t due = 0;
+    if (p->khome[k] != NO_HOME) {
+        uint32_t total = 0, lcap = 0;
+        for (uint32_t t = AGN_COUNTER_PN; t <= AGN_REGISTER_MV && !rc; ++t) {
+            part_sub *s = sub_get(p, t);
+            uint32_t len = 0, ll = 0;
+            if (!s) continue;
+            rc = agn_oplog_key_meta(s->log, 1, &k, &len, &ll, NULL);
+            total += len;
+            if (t == p->khome[k]) lcap = ll;
+        }
+        if (rc) return error_tuple(env, rc);
+        const uint32_t list_len = lcap > AGN_OPS_THRESHOLD ? lcap : AGN_OPS_THRESHOLD;
+        due = total >= list_len || (p->kcnt[k] + 1u) % AGN_OPS_THRESHOLD == 0;
+    }
     return atom(env, due ? "true" : "false");
 }
 
