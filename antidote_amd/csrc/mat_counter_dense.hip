@@ -1035,7 +1035,8 @@ inline bool sparse_batch(const agn_log &log, const agn_read &req, const agn_resu
 }
 
 int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u, req.hints};
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_xcd(req.n_req) ? 1u : 0u, 0u, 1u,
+                req.hints};
     const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + 1) / 2;
     if (nb > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
@@ -1075,7 +1076,8 @@ inline bool early_chunk() {
 }
 
 int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, 0u, 1u, req.hints};
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_xcd(req.n_req) ? 1u : 0u, 0u, 1u,
+                req.hints};
     const MaskArgs mk = mask_args(log, req, out);
     if (req.n_req > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
                                                (unsigned long long)req.n_req);
@@ -1193,7 +1195,7 @@ int counter_variant() {
 template <int D, int WPB, int VAR, bool KEYS, bool MSK>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     const char *qv = AGN_KNOB("AGN_COUNTER_QUAD_NT");
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, xcd_remap() ? 1u : 0u, pair_chunks(),
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_xcd(req.n_req) ? 1u : 0u, pair_chunks(),
                 (qv && qv[0] >= '0' && qv[0] <= '3') ? (uint32_t)(qv[0] - '0') : 1u};
     const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;

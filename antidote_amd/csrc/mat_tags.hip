@@ -751,6 +751,12 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     }
 }
 
+// The XCD-aware block order for the tags pass: kept for up to 32 DCs, the
+// plain order for wider clocks (cfg4, D = 64: 9.08 / 9.08 against 9.25 /
+// 9.23 ms on two boxes; cfg3, D = 16: 6.63 vs 6.64 and 6.97 vs 6.68 --
+// profiles/r06/ab_xcd_remap.log).  AGN_XCD_REMAP=0|1 overrides.
+inline bool tags_xcd(uint32_t D) { return xcd_remap_or(D <= 32); }
+
 // FAST_WPB: one wave per block measured 0.7-1.4 % faster than 4 (cfg3/cfg4,
 // profiles/r01/ab_tags_wpb_unbiased.log)
 constexpr int FAST_CAP = 256, SLOW_CAP = 4096, FAST_WPB = 1, RBATCH = 2;
@@ -773,7 +779,7 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
         hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, WARM,
                                    false, CT, MSK>),
                            dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, fast,
-                           xcd_remap() ? 1u : 0u, TagServe{});
+                           tags_xcd(log.n_dcs) ? 1u : 0u, TagServe{});
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
