@@ -226,11 +226,12 @@ inline bool xcd_remap_or(bool dflt) {
     const char *v = AGN_KNOB("AGN_XCD_REMAP");
     return (v && (v[0] == '0' || v[0] == '1')) ? v[0] == '1' : dflt;
 }
-// Bulk dense counter batches (>= 2^20 requests) stream their rows faster in
-// the plain block order: cfg2 cold 7.65 / 7.70 against 7.85 ms, warm 7.97 /
-// 8.05 against 8.13 on two boxes, masked cfg2 (k_counter_q8e) 7.83 against
-// 8.04 (profiles/r06/ab_xcd_remap.log); small batches keep the XCD-aware
-// order (cfg1: 6.5 % faster with it).
+// Bulk counter batches (>= 2^20 requests) leave the XCD-aware order: dense
+// cfg2 7.65 / 7.70 against 7.85 ms in the identity order, warm 7.97 / 8.05
+// against 8.13, masked (k_counter_q8e) 7.83 against 8.04
+// (profiles/r06/ab_xcd_remap.log), and the dense / warm kernels faster still
+// in runs of 64 blocks per XCD (mat_counter_dense.hip counter_order); small
+// batches keep the XCD-aware order (cfg1: 6.5 % faster with it).
 inline bool counter_xcd(uint64_t n_req) { return xcd_remap_or(n_req < (1ull << 20)); }
 
 // Grid sizing for the streaming kernels: enough waves to fill 256 CUs.

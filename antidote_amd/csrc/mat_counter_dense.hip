@@ -41,11 +41,41 @@ namespace {
 // (uint32 words: one 128-byte line each)
 constexpr uint32_t QL_S = 1024, QL_STRIDE = 32;
 
+// Chunked XCD order: runs of g consecutive logical blocks per XCD, the eight
+// XCDs on neighbouring runs (a super-run of 8g blocks), so a per-request
+// line stays in one L2 while the chip streams one region at a time; blocks
+// past the last whole super-run keep the identity order.
+__device__ inline uint32_t xcd_chunk_block(uint32_t b, uint32_t nb, uint32_t g) {
+    const uint32_t sup = AGN_XCDS * g;
+    if (b >= (nb / sup) * sup) return b;
+    const uint32_t x = b % AGN_XCDS, idx = b / AGN_XCDS;
+    return ((idx / g) * AGN_XCDS + x) * g + idx % g;
+}
+// A launch's block order: 0 identity, 1 xcd_block, g >= 2 xcd_chunk_block.
+__device__ inline uint32_t block_order(uint32_t mode, uint32_t b, uint32_t nb) {
+    return mode == 0u ? b : mode == 1u ? xcd_block(b, nb) : xcd_chunk_block(b, nb, mode);
+}
+// The counter launchers' block order (block_order's mode): the XCD-aware
+// order for small batches (counter_xcd), else runs of `bulk` blocks per XCD
+// (AGN_XCD_CHUNK=g overrides; 0 or AGN_XCD_REMAP=0: the identity order).
+// Same-box A/Bs (profiles/r06/ab_xcd_chunk.log): dense cfg2 runs of 64
+// 7.57 ms against 7.83 identity and 7.92 XCD-aware; the masked q8e (whose
+// hand-on queue follows the block order) is fastest in the identity order.
+inline uint32_t counter_order(uint64_t n_req, uint32_t bulk) {
+    if (counter_xcd(n_req)) return 1u;
+    const char *v = AGN_KNOB("AGN_XCD_REMAP");
+    if (v && v[0] == '0') return 0u;
+    const char *c = AGN_KNOB("AGN_XCD_CHUNK");
+    const unsigned long g = c ? strtoul(c, nullptr, 10) : bulk;
+    return (g >= 2ul && g <= 4096ul) ? (uint32_t)g : 0u;
+}
+constexpr uint32_t BULK_CHUNK = 64;
+
 struct DenseArgs {
     uint64_t n_req;
     uint64_t n_entries;
     uint32_t req_type;
-    uint32_t xcd;  // 1: XCD-aware block order (xcd_block)
+    uint32_t xcd;  // block_order mode: 0 identity, 1 xcd_block, g >= 2 runs of g per XCD
     uint32_t pair; // 1: D <= 4 keys longer than a chunk walk two chunks per step
     uint32_t qnt;  // quad rows, non-temporal loads: bit 0 rows, bit 1 effects (AGN_COUNTER_QUAD_NT)
     uint32_t hints;  // agn_read.hints (k_counter_q8e / k_counter_quad2)
@@ -243,8 +273,7 @@ __global__ __launch_bounds__(64 * WPB) void k_counter_key(
     const int w = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
     // unconditional (as the side loads below): a conditional scalar load is
     // waited for on its own
-    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
-    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t i = uniform_u64((uint64_t)blk * WPB + (uint64_t)w);
     if (i >= a.n_req) return;
     uint64_t r[D], s[D], e[D], ct[D];
@@ -794,8 +823,7 @@ __global__ __launch_bounds__(64, (ANY_WARM && !MSK) ? 6 : 1) void k_counter_quad
     int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
     uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
     uint32_t *__restrict__ o_err) {
-    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
-    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t i0 = uniform_u64((uint64_t)blk * 2u);
     if (i0 >= a.n_req) return;
     const bool two = i0 + 1u < a.n_req;
@@ -860,8 +888,7 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
     int64_t *__restrict__ o_hole, uint64_t *__restrict__ o_lastct,
     uint32_t *__restrict__ o_count, uint32_t *__restrict__ o_flags,
     uint32_t *__restrict__ o_err, uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
-    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
-    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t i = uniform_u64((uint64_t)blk);
     if (i >= a.n_req) return;
     Q2Key k;
@@ -922,8 +949,7 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
 template <bool KEYS>
 __global__ __launch_bounds__(64) void k_counter_q8e2(Q2Params) {
     const DenseArgs a = dense_of(kparams<Q2Params>().a);
-    const uint32_t xb = xcd_block(blockIdx.x, gridDim.x);
-    const uint32_t blk = a.xcd ? xb : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t i0 = uniform_u64((uint64_t)blk * 2u);
     if (i0 >= a.n_req) return;
     const bool two = i0 + 1u < a.n_req;
@@ -1035,7 +1061,7 @@ inline bool sparse_batch(const agn_log &log, const agn_read &req, const agn_resu
 }
 
 int launch_quad2(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_xcd(req.n_req) ? 1u : 0u, 0u, 1u,
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_order(req.n_req, BULK_CHUNK), 0u, 1u,
                 req.hints};
     const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + 1) / 2;
@@ -1076,7 +1102,7 @@ inline bool early_chunk() {
 }
 
 int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_xcd(req.n_req) ? 1u : 0u, 0u, 1u,
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_order(req.n_req, 0u), 0u, 1u,
                 req.hints};
     const MaskArgs mk = mask_args(log, req, out);
     if (req.n_req > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",
@@ -1195,7 +1221,7 @@ int counter_variant() {
 template <int D, int WPB, int VAR, bool KEYS, bool MSK>
 int launch_key_k(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     const char *qv = AGN_KNOB("AGN_COUNTER_QUAD_NT");
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_xcd(req.n_req) ? 1u : 0u, pair_chunks(),
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_order(req.n_req, BULK_CHUNK), pair_chunks(),
                 (qv && qv[0] >= '0' && qv[0] <= '3') ? (uint32_t)(qv[0] - '0') : 1u};
     const MaskArgs mk = mask_args(log, req, out);
     const uint64_t nb = (req.n_req + WPB - 1) / WPB;
