@@ -206,6 +206,20 @@ __device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
     const uint32_t x = b % AGN_XCDS, idx = b / AGN_XCDS;
     return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
 }
+// Chunked XCD order: runs of g consecutive logical blocks per XCD, the eight
+// XCDs on neighbouring runs (a super-run of 8g blocks), so a per-request
+// line stays in one L2 while the chip streams one region at a time; blocks
+// past the last whole super-run keep the identity order.
+__device__ inline uint32_t xcd_chunk_block(uint32_t b, uint32_t nb, uint32_t g) {
+    const uint32_t sup = AGN_XCDS * g;
+    if (b >= (nb / sup) * sup) return b;
+    const uint32_t x = b % AGN_XCDS, idx = b / AGN_XCDS;
+    return ((idx / g) * AGN_XCDS + x) * g + idx % g;
+}
+// A launch's block order: 0 identity, 1 xcd_block, g >= 2 xcd_chunk_block.
+__device__ inline uint32_t block_order(uint32_t mode, uint32_t b, uint32_t nb) {
+    return mode == 0u ? b : mode == 1u ? xcd_block(b, nb) : xcd_chunk_block(b, nb, mode);
+}
 
 // AGN_HINT_MIXED routing threshold: a masked counter batch with more than
 // 1/16 of its keys mixed (entries with different DC sets) is scanned in one
@@ -233,6 +247,17 @@ inline bool xcd_remap_or(bool dflt) {
 // in runs of 64 blocks per XCD (mat_counter_dense.hip counter_order); small
 // batches keep the XCD-aware order (cfg1: 6.5 % faster with it).
 inline bool counter_xcd(uint64_t n_req) { return xcd_remap_or(n_req < (1ull << 20)); }
+// A launcher's block order (block_order's mode), default `dflt`: an explicit
+// AGN_XCD_REMAP=0|1 wins, then AGN_XCD_CHUNK=g (runs of g >= 2 blocks per
+// XCD; any other value the identity order) -- A/B knobs.
+inline uint32_t order_or(uint32_t dflt) {
+    const char *v = AGN_KNOB("AGN_XCD_REMAP");
+    if (v && (v[0] == '0' || v[0] == '1')) return (uint32_t)(v[0] - '0');
+    const char *c = AGN_KNOB("AGN_XCD_CHUNK");
+    if (!c) return dflt;
+    const unsigned long g = strtoul(c, nullptr, 10);
+    return (g >= 2ul && g <= 4096ul) ? (uint32_t)g : 0u;
+}
 
 // Grid sizing for the streaming kernels: enough waves to fill 256 CUs.
 inline unsigned grid_for(uint64_t work_items, unsigned items_per_block, unsigned max_blocks) {

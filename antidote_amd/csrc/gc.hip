@@ -301,7 +301,7 @@ struct InplaceArgs {
     uint64_t n_keys;
     uint32_t D, W;
     int copy_unselected;       // out of place: keys with prune[k] == 0 are copied whole
-    int xcd;                   // XCD-aware block order
+    uint32_t xcd;              // block_order mode
     int late_fields;           // entry fields loaded after the filter (kept entries only)
     // key-list launch (n_keys = list length): entry i is key key_list[i], GC'd
     // iff list_flags[i] != 0; meta is indexed by i.  NULL = every key, by prune[k].
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * WPB, PF == 2 ? 5 : MINW) void k_prune_inplace(
     constexpr int NQ = DPL >= 2 ? DPL / 2 : 1;             // CTL: loads per lane
     // XCD-aware key order: consecutive keys (whose per-key outputs share lines)
     // run on one XCD's L2
-    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t i = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
     if (i >= a.n_keys) return;
     const uint64_t K = a.n_keys;   // launch size (meta stride)
@@ -859,7 +859,7 @@ __global__ __launch_bounds__(64 * WPB, MINW) void k_prune_tail(InplaceArgs a,
     using S = Shape<DPL, LPO>;
     constexpr int OPI = S::OPI;
     constexpr bool QUAD = FULL && DPL == 8 && LPO == 1 && !SPARSE;
-    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t i = (uint64_t)blk * WPB + (WPB == 1 ? 0u : (threadIdx.x >> 6));
     if (i >= a.n_keys) return;
     const uint64_t K = a.n_keys;  // launch size (meta stride)
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(64, MINW) void k_prune_tail_q(InplaceArgs a,
                                                          const uint64_t *__restrict__ thr,
                                                          uint32_t *__restrict__ meta,
                                                          uint32_t *__restrict__ flags) {
-    const uint32_t blk = a.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
     const uint64_t K = a.n_keys;  // launch size (meta stride)
     const int lane = lane_id(), qp = lane & 3;
     TailKey s[KPW];
@@ -1531,7 +1531,7 @@ InplaceArgs seg_args(const agn_log &in, const agn_log &out) {
     a.copy_unselected = 0;
     a.key_list = nullptr;
     a.list_flags = nullptr;
-    a.xcd = xcd_remap() ? 1 : 0;
+    a.xcd = order_or(1u);
     const char *lf = AGN_KNOB("AGN_PRUNE_LATE_FIELDS");  // A/B override: 0 | 1
     a.late_fields = (lf && (lf[0] == '0' || lf[0] == '1')) ? lf[0] - '0' : -1;
     a.meta6 = 0;

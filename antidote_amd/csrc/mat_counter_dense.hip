@@ -41,20 +41,6 @@ namespace {
 // (uint32 words: one 128-byte line each)
 constexpr uint32_t QL_S = 1024, QL_STRIDE = 32;
 
-// Chunked XCD order: runs of g consecutive logical blocks per XCD, the eight
-// XCDs on neighbouring runs (a super-run of 8g blocks), so a per-request
-// line stays in one L2 while the chip streams one region at a time; blocks
-// past the last whole super-run keep the identity order.
-__device__ inline uint32_t xcd_chunk_block(uint32_t b, uint32_t nb, uint32_t g) {
-    const uint32_t sup = AGN_XCDS * g;
-    if (b >= (nb / sup) * sup) return b;
-    const uint32_t x = b % AGN_XCDS, idx = b / AGN_XCDS;
-    return ((idx / g) * AGN_XCDS + x) * g + idx % g;
-}
-// A launch's block order: 0 identity, 1 xcd_block, g >= 2 xcd_chunk_block.
-__device__ inline uint32_t block_order(uint32_t mode, uint32_t b, uint32_t nb) {
-    return mode == 0u ? b : mode == 1u ? xcd_block(b, nb) : xcd_chunk_block(b, nb, mode);
-}
 // The counter launchers' block order (block_order's mode): the XCD-aware
 // order for small batches (counter_xcd), else runs of `bulk` blocks per XCD
 // (AGN_XCD_CHUNK=g overrides; 0 or AGN_XCD_REMAP=0: the identity order).
@@ -62,12 +48,7 @@ __device__ inline uint32_t block_order(uint32_t mode, uint32_t b, uint32_t nb) {
 // 7.57 ms against 7.83 identity and 7.92 XCD-aware; the masked q8e (whose
 // hand-on queue follows the block order) is fastest in the identity order.
 inline uint32_t counter_order(uint64_t n_req, uint32_t bulk) {
-    if (counter_xcd(n_req)) return 1u;
-    const char *v = AGN_KNOB("AGN_XCD_REMAP");
-    if (v && v[0] == '0') return 0u;
-    const char *c = AGN_KNOB("AGN_XCD_CHUNK");
-    const unsigned long g = c ? strtoul(c, nullptr, 10) : bulk;
-    return (g >= 2ul && g <= 4096ul) ? (uint32_t)g : 0u;
+    return order_or(n_req < (1ull << 20) ? 1u : bulk);
 }
 constexpr uint32_t BULK_CHUNK = 64;
 

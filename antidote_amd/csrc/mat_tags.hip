@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     const uint64_t n_items = tl.in ? (uint64_t)__builtin_amdgcn_readfirstlane(ldc(tl.in_n)) : req.n_req;
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
 
-    const uint32_t blk = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = block_order(xcd, blockIdx.x, gridDim.x);
     for (uint64_t it = (uint64_t)blk * WPB + (uint64_t)w; it < n_items; it += nw) {
         // the per-request / per-key words below are read through the scalar
         // cache (ldc: arrays this launch never writes); as plain loads in the
@@ -751,11 +751,16 @@ __global__ __launch_bounds__(64 * WPB) void k_tags(agn_log log, agn_read req, ag
     }
 }
 
-// The XCD-aware block order for the tags pass: kept for up to 32 DCs, the
-// plain order for wider clocks (cfg4, D = 64: 9.08 / 9.08 against 9.25 /
-// 9.23 ms on two boxes; cfg3, D = 16: 6.63 vs 6.64 and 6.97 vs 6.68 --
-// profiles/r06/ab_xcd_remap.log).  AGN_XCD_REMAP=0|1 overrides.
-inline bool tags_xcd(uint32_t D) { return xcd_remap_or(D <= 32); }
+// The tags pass's block order.  A bulk batch (>= 2^16 keys, one wave per
+// block) runs in runs of 128 blocks per XCD: cfg3 6.45 against 6.64 / 6.81
+// ms in the XCD-aware order, cfg4 8.87 against 9.07 in the identity order
+// (profiles/r06/ab_xcd_chunk.log).  Smaller batches and list passes keep
+// the XCD-aware order up to 32 DCs, the identity order for wider clocks
+// (cfg4: 9.08 against 9.25 ms, profiles/r06/ab_xcd_remap.log).
+// AGN_XCD_REMAP / AGN_XCD_CHUNK override (order_or).
+inline uint32_t tags_order(uint32_t D, uint64_t n_req, bool list) {
+    return order_or(!list && n_req >= (1ull << 16) ? 128u : D <= 32 ? 1u : 0u);
+}
 
 // FAST_WPB: one wave per block measured 0.7-1.4 % faster than 4 (cfg3/cfg4,
 // profiles/r01/ab_tags_wpb_unbiased.log)
@@ -779,7 +784,7 @@ hipError_t tags_passes(const agn_log &log, const agn_read &req, const agn_result
         hipLaunchKernelGGL((k_tags<DPL, LPO, SPARSE, FULL, SET, FAST_CAP, FAST_WPB, RBATCH, WARM,
                                    false, CT, MSK>),
                            dim3(blocks), dim3(64 * FAST_WPB), 0, st, log, req, out, fast,
-                           tags_xcd(log.n_dcs) ? 1u : 0u, TagServe{});
+                           tags_order(log.n_dcs, req.n_req, in != nullptr), TagServe{});
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -539,7 +539,7 @@ __global__ __launch_bounds__(64, (NP == 1 && !MSK) ? 6 : 1) void k_read6(R6Param
     using Q = R6Req<D, MSK>;
     __shared__ uint64_t stage[Q::DCP][AGN_WAVE];
     R6K &k0 = kp();
-    const uint32_t blk = k0.xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = block_order(k0.xcd, blockIdx.x, gridDim.x);
     const uint64_t n_req = k0.a.n_req;
     const uint64_t i0 = (uint64_t)blk * NP;
     if (i0 >= n_req) return;
@@ -699,7 +699,7 @@ bool read6_supported(const agn_log &view, uint32_t D) {
 // against one, in one process (profiles/r05/ab_read6_*): 10M reads at D = 8
 // 11.00-11.17 vs 10.88-10.90 ms; 1M at D = 3 0.94-0.96 vs 0.94-0.97 ms.
 // AGN_READ6_XCD=1: the XCD-aware block order (xcd_block; 11.59 vs 11.47 ms at
-// 10M, off).
+// 10M, off); AGN_READ6_XCD=g >= 2: runs of g blocks per XCD (block_order).
 int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     if (a.n_req == 0) return AGN_OK;
     if (a.n_req > 0x7fffffffull) return fail(AGN_ENOTSUP, "read6: batch too large");
@@ -708,7 +708,8 @@ int launch_read6(const agn_ss_cache &c, const Read6Args &a, hipStream_t st) {
     const char *npv = AGN_KNOB("AGN_READ6_NP");
     const bool pair = npv && npv[0] == '2';
     const char *xv = AGN_KNOB("AGN_READ6_XCD");
-    const uint32_t xcd = (xv && xv[0] == '1') ? 1u : 0u;
+    const unsigned long xg = xv ? strtoul(xv, nullptr, 10) : 0ul;
+    const uint32_t xcd = xg <= 4096ul ? (uint32_t)xg : 0u;
     const dim3 grid2((unsigned)((a.n_req + 1) / 2));
     const R6Params prm{c, a, xcd};
 #define AGN_R6(DV)                                                                             \
