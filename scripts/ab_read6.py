@@ -37,6 +37,9 @@ VARS = {
     "np1x": ("cur", {"AGN_READ_CACHED_SPLIT": "0", "AGN_READ6_NP": "1", "AGN_READ6_XCD": "1"}),
     "np2x": ("cur", {"AGN_READ_CACHED_SPLIT": "0", "AGN_READ6_NP": "2", "AGN_READ6_XCD": "1"}),
     "seq": ("cur", {"AGN_READ_CACHED_SPLIT": "1"}),
+    # runs of g blocks per XCD (block_order)
+    **{f"np1c{g}": ("cur", {"AGN_READ_CACHED_SPLIT": "0", "AGN_READ6_NP": "1",
+                            "AGN_READ6_XCD": str(g)}) for g in (16, 64, 128, 256)},
     "default": ("cur", {}),
 }
 # name=path entries of the variant list: another library's fused kernel
