@@ -14,7 +14,8 @@ import pytest
 
 from antidote_amd import _abi
 from oracle import py_oracle as po
-from synth import random_case
+from antidote_amd.encode import alloc_result, log_struct, result_struct
+from synth import compare, random_case
 
 S = 10  # slots
 
@@ -365,18 +366,54 @@ def test_read_cached_vs_sequence(eng, monkeypatch, D, split, np_):
             b.free()
 
 
+def oracle_read_cached(lib, hc, ls, keys, R, tx, gc, D):
+    """read/6 for a batch through the C oracle on the host cache `hc`:
+    oracle_ss_lookup -> oracle_materialize -> oracle_ss_store
+    (materializer_vnode.erl:384-413, 466-509).  Returns (result, status,
+    prune flags per key, thresholds per key)."""
+    nr, K = len(keys), hc.n_keys
+    sct, ign = np.zeros((nr, D), np.uint64), np.zeros(nr, np.uint8)
+    base, first, status = np.zeros(nr, np.int64), np.zeros(nr, np.uint8), np.zeros(nr, np.uint8)
+    assert lib.oracle_ss_lookup(C.byref(hc), nr, ptr(keys), ptr(R), None, ptr(sct), None,
+                                ptr(ign), ptr(base), ptr(first), ptr(status)) == 0
+    rq = _abi.AgnRead()
+    rq.n_req, rq.keys, rq.R, rq.R_mask = nr, ptr(keys), ptr(R), None
+    rq.sct, rq.sct_mask, rq.sct_ignore, rq.txid = ptr(sct), None, ptr(ign), ptr(tx)
+    rq.req_type, rq.base_value = _abi.COUNTER_PN, ptr(base)
+    res = alloc_result(nr, D, sparse=False)
+    rs = result_struct(res)
+    assert lib.oracle_materialize(C.byref(ls), C.byref(rq), C.byref(rs), 4) == 0
+    prune, thr = np.zeros(K, np.uint8), np.zeros((K, D), np.uint64)
+    assert lib.oracle_ss_store(C.byref(hc), C.byref(ls), nr, ptr(keys), ptr(first), ptr(status),
+                               ptr(gc), C.byref(rs), None, ptr(prune), ptr(thr), None) == 0
+    return res, status, prune, thr
+
+
 @pytest.mark.gpu
-def test_read_cached_default_dispatch(eng, monkeypatch):
-    """A bulk batch (36k requests, D = 8) through agn_read_cached's default
-    dispatch (the fused kernel: D = 8 never switches since round 5) equals
-    the batched kernels forced on it (AGN_READ_CACHED_SPLIT=1): outputs,
-    status, prune flags, thresholds and the caches, over a cold round and a
-    warm round with GC reads."""
-    K, D = 40_000, 8
-    log, req, _ = random_case(977, _abi.COUNTER_PN, K, D, 12, txid=0.2, empty=0.05)
+def test_read_cached_default_dispatch(eng, oracle_lib, monkeypatch):
+    """A bulk batch (33k requests, D = 8, keys of up to 64 ops: those past 32
+    take the fused kernel's second chunk) through agn_read_cached's default
+    dispatch (the fused k_read6: D = 8 never switches since round 5) and with
+    the batched kernels forced (AGN_READ_CACHED_SPLIT=1), each against the C
+    oracle's lookup -> materialize -> store chain on a host cache: outputs,
+    status, prune flags, thresholds and the caches, over a cold round and two
+    warm rounds with GC reads (the second with newly included ops)."""
+    K, D, nr = 36_000, 8, 33_000
+    log, req, _ = random_case(977, _abi.COUNTER_PN, K, D, 64, txid=0.2, empty=0.05)
+    lens = np.diff(log.key_off.astype(np.int64))
+    assert (lens > 32).mean() > 0.3
     dlog = eng.upload_log(log)
     dlog.struct.oc_mask = None
+    ls = log_struct(log)
+    ls.oc_mask = None
     rng = np.random.default_rng(5)
+    hcache = {"n": np.zeros(K, np.uint32), "clock": np.zeros((K, S, D), np.uint64),
+              "last_op": np.zeros((K, S), np.int64), "value": np.zeros((K, S), np.int64)}
+    hc = _abi.AgnSsCache()
+    hc.n_dcs, hc.slots, hc.n_keys = D, S, K
+    hc.n, hc.clock, hc.last_op, hc.value = (ptr(hcache[x]) for x in ("n", "clock", "last_op",
+                                                                     "value"))
+    hc.clock_mask = None
 
     def cache():
         bufs = {"n": eng.upload(np.zeros(K, np.uint32)),
@@ -389,16 +426,18 @@ def test_read_cached_default_dispatch(eng, monkeypatch):
         return c, bufs
 
     caches = [cache(), cache()]
-    nr = 36_000
     try:
-        for rnd in range(2):
+        for rnd in range(3):
             keys = rng.permutation(K)[:nr].astype(np.uint64)
-            R = req.R[keys.astype(np.int64)] + rng.integers(0, 3, (nr, D)).astype(np.uint64)
-            tx = req.txid[keys.astype(np.int64)].copy()
-            gc = (rng.random(nr) < 0.2).astype(np.uint8)
-            dk, dR, dtx, dgc = (eng.upload(x) for x in (keys, np.ascontiguousarray(R), tx, gc))
-            got = []
-            for (c, _b), split in zip(caches, (None, "1")):
+            ki = keys.astype(np.int64)
+            R = np.ascontiguousarray(req.R[ki] + rng.integers(0, 3 if rnd < 2 else 40, (nr, D))
+                                     .astype(np.uint64))
+            tx = req.txid[ki].copy()
+            gc = (rng.random(nr) < (0.0 if rnd == 0 else 0.2)).astype(np.uint8)
+            want, wst, wpr, wthr = oracle_read_cached(oracle_lib, hc, ls, keys, R, tx, gc, D)
+            dk, dR, dtx, dgc = (eng.upload(x) for x in (keys, R, tx, gc))
+            for (c, bufs), split in zip(caches, (None, "1")):
+                ctx = (rnd, split)
                 if split is None:
                     monkeypatch.delenv("AGN_READ_CACHED_SPLIT", raising=False)
                 else:
@@ -409,26 +448,29 @@ def test_read_cached_default_dispatch(eng, monkeypatch):
                 eng.read_cached(c, dlog, nr, dk.ptr, dR.ptr, dtx.ptr, dgc.ptr, res, st.ptr, pr.ptr,
                                 thr.ptr)
                 eng.sync()
-                got.append((eng.fetch_result(res), eng.download(st, np.uint8, (nr,)),
-                            eng.download(pr, np.uint8, (nr,)),
-                            eng.download(thr, np.uint64, (K, D))))
+                got = eng.fetch_result(res)
+                bad = compare(_abi.COUNTER_PN, D, got, want, False, nr)
+                assert not bad, (ctx, bad[:10])
+                assert np.array_equal(eng.download(st, np.uint8, (nr,)), wst), ctx
+                # read_cached flags per request, the store per key (keys distinct)
+                gp = eng.download(pr, np.uint8, (nr,))
+                assert np.array_equal(gp, wpr[ki]), ctx
+                pk = ki[gp == 1]
+                assert np.array_equal(eng.download(thr, np.uint64, (K, D))[pk], wthr[pk]), ctx
+                n = eng.download(bufs["n"], np.uint32, (K,))
+                assert np.array_equal(n, hcache["n"]), ctx
+                live = np.arange(S)[None, :] < n[:, None]
+                for name, dt, shape in (("clock", np.uint64, (K, S, D)),
+                                        ("last_op", np.int64, (K, S)),
+                                        ("value", np.int64, (K, S))):
+                    x = eng.download(bufs[name], dt, shape)
+                    assert np.array_equal(x[live], hcache[name][live]), (ctx, name)
                 for b in [st, pr, thr] + list(res.bufs.values()):
                     b.free()
-            (ra, sa, pa, ta), (rb, sb, pb, tb) = got
-            for f in ("value", "hole", "lastct", "count", "flags", "err_pos"):
-                assert np.array_equal(getattr(ra, f), getattr(rb, f)), (rnd, f)
-            assert np.array_equal(sa, sb) and np.array_equal(pa, pb), rnd
-            assert np.array_equal(ta, tb), rnd
-            na = eng.download(caches[0][1]["n"], np.uint32, (K,))
-            assert np.array_equal(na, eng.download(caches[1][1]["n"], np.uint32, (K,))), rnd
-            for name, dt, shape in (("clock", np.uint64, (K, S, D)), ("last_op", np.int64, (K, S)),
-                                    ("value", np.int64, (K, S))):
-                xa = eng.download(caches[0][1][name], dt, shape)
-                xb = eng.download(caches[1][1][name], dt, shape)
-                live = np.arange(S)[None, :] < na[:, None]
-                assert np.array_equal(xa[live], xb[live]), (rnd, name)
-            if rnd == 1:
-                assert (sa == _abi.SS_HIT).any() and pa.any()
+            if rnd >= 1:
+                assert (wst == _abi.SS_HIT).any() and wpr.any()
+            if rnd == 2:
+                assert (want.count > 0).any()
             for b in (dk, dR, dtx, dgc):
                 b.free()
     finally:
