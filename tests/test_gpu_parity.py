@@ -421,6 +421,78 @@ def test_cfg1_all_keys_parity(eng, oracle_lib, warm):
             b.free()
 
 
+# ------------------------------------------------------------------ block orders
+BULK = [
+    # counter_pn just past the 2^20-request threshold (runs of 64 blocks per
+    # XCD), a ragged grid: a tail past the last whole super-run of 8 runs
+    dict(crdt_type=1, n_dcs=8, n_keys=(1 << 20) + 12_345, ops_per_key=8, n_elems=0, seed=777),
+    dict(crdt_type=1, n_dcs=8, n_keys=(1 << 20) + 12_345, ops_per_key=8, n_elems=0, seed=777,
+         warm=1),
+    # tag passes just past 2^16 keys (runs of 128)
+    dict(crdt_type=2, n_dcs=16, n_keys=(1 << 16) + 4_321, ops_per_key=16, n_elems=8, seed=778),
+    dict(crdt_type=3, n_dcs=64, n_keys=(1 << 16) + 999, ops_per_key=8, n_elems=4, seed=779,
+         warm=1),
+]
+ORDERS = {"default": {}, "identity": {"AGN_XCD_REMAP": "0"}, "xcd": {"AGN_XCD_REMAP": "1"},
+          "runs7": {"AGN_XCD_CHUNK": "7"}, "runs300": {"AGN_XCD_CHUNK": "300"}}
+
+
+def _equal_all(crdt, got, want, K):
+    """Every key's result, vectorised (no error flags in generated logs)."""
+    assert np.array_equal(got.flags[:K], want.flags[:K])
+    assert np.array_equal(got.count[:K], want.count[:K])
+    assert np.array_equal(got.hole[:K], want.hole[:K])
+    ct = (want.flags[:K] & _abi.F_CT_IGNORE) == 0
+    assert np.array_equal(got.lastct[:K][ct], want.lastct[:K][ct])
+    if crdt == _abi.COUNTER_PN:
+        assert np.array_equal(got.value[:K], want.value[:K])
+        return
+    assert np.array_equal(got.out_n[:K], want.out_n[:K])
+    assert np.array_equal(got.out_off[:K], want.out_off[:K])
+    n = want.out_n[:K].astype(np.int64)
+    pos = np.repeat(want.out_off[:K].astype(np.int64), n) + \
+        (np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n))
+    assert np.array_equal(got.out_tag[pos], want.out_tag[pos])
+    assert np.array_equal(got.out_tok[pos], want.out_tok[pos])
+
+
+@pytest.mark.parametrize("spec", BULK, ids=["counter_cold", "counter_warm", "set_aw", "register_mv_warm"])
+def test_bulk_block_orders_all_keys(eng, oracle_lib, monkeypatch, spec):
+    """Batches just past the bulk thresholds (counter 2^20 requests, tag passes
+    2^16 keys), every key against the oracle under each block order the
+    launchers choose from (block_order: identity, XCD-aware, runs of g --
+    odd and larger than a super-run's share), the default included."""
+    cfg = _abi.AgnGenCfg(**{"key_base": 0, "key_stride": 1, "warm": 0, **spec})
+    K, D = cfg.n_keys, cfg.n_dcs
+    cap = None if cfg.crdt_type == 1 else \
+        np.arange(K + 1, dtype=np.uint64) * np.uint64(cfg.ops_per_key)
+    hl, hr = gen_host(cfg)
+    want = alloc_result(K, D, sparse=False, cap_off=cap)
+    assert oracle_lib.oracle_materialize(C.byref(hl), C.byref(hr),
+                                         C.byref(result_struct(want)), 4) == 0
+    free_gen_host(hl, hr)
+    assert 0.05 < want.count.mean() / cfg.ops_per_key < 0.95
+    dl, dr = eng.gen_dev(cfg)
+    try:
+        for name, env in ORDERS.items():
+            for k in ("AGN_XCD_REMAP", "AGN_XCD_CHUNK"):
+                monkeypatch.delenv(k, raising=False)
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            res = eng.alloc_result(K, D, sparse=False, cap_off=cap)
+            eng.materialize(dl, dr, res)
+            eng.sync()
+            got = eng.fetch_result(res)
+            for b in res.bufs.values():
+                b.free()
+            try:
+                _equal_all(cfg.crdt_type, got, want, K)
+            except AssertionError as e:
+                raise AssertionError(f"block order {name}") from e
+    finally:
+        eng.free_gen(dl, dr)
+
+
 # ------------------------------------------------------------------ GST / base selection
 @pytest.mark.parametrize("D,P,E,p_undef,p_absent", [(2, 3, 1, 0.0, 0.0), (8, 64, 4, 0.05, 0.1),
                                                     (256, 4096, 2, 0.0, 0.0),
