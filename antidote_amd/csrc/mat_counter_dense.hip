@@ -42,11 +42,12 @@ namespace {
 constexpr uint32_t QL_S = 1024, QL_STRIDE = 32;
 
 // The counter launchers' block order (block_order's mode): the XCD-aware
-// order for small batches (counter_xcd), else runs of `bulk` blocks per XCD
-// (AGN_XCD_CHUNK=g overrides; 0 or AGN_XCD_REMAP=0: the identity order).
-// Same-box A/Bs (profiles/r06/ab_xcd_chunk.log): dense cfg2 runs of 64
-// 7.57 ms against 7.83 identity and 7.92 XCD-aware; the masked q8e (whose
-// hand-on queue follows the block order) is fastest in the identity order.
+// order for small batches, else runs of `bulk` blocks per XCD (order_or:
+// AGN_XCD_REMAP / AGN_XCD_CHUNK override).  Same-box A/Bs
+// (profiles/r06/ab_xcd_chunk.log): dense cfg2 runs of 64 7.57 ms against
+// 7.83 identity and 7.92 XCD-aware, warm 7.43 against 7.69; the masked
+// q8e in one process 8.02 against 8.18 identity and 8.37 XCD-aware (with
+// the bench's hints), its warm two-per-wave form level in every order.
 inline uint32_t counter_order(uint64_t n_req, uint32_t bulk) {
     return order_or(n_req < (1ull << 20) ? 1u : bulk);
 }
@@ -1083,7 +1084,7 @@ inline bool early_chunk() {
 }
 
 int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
-    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_order(req.n_req, 0u), 0u, 1u,
+    DenseArgs a{req.n_req, log.n_entries, req.req_type, counter_order(req.n_req, BULK_CHUNK), 0u, 1u,
                 req.hints};
     const MaskArgs mk = mask_args(log, req, out);
     if (req.n_req > 0x7fffffffull) return fail(AGN_EINVAL, "batch too large: %llu requests",

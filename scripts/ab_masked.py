@@ -50,8 +50,16 @@ VARIANTS = {
     "dense_q1": ("dense", {"AGN_COUNTER_VARIANT": "2"}, 0),
     "masked_quad2": ("masked", {"AGN_COUNTER_VARIANT": "3"}, HINTS),
     "masked_old_hints": ("masked", {"AGN_COUNTER_EARLY": "0"}, HINTS),
+    # round 6: block orders (identity by default for the masked forms)
+    "masked_x1": ("masked", {"AGN_XCD_REMAP": "1"}, 0),
+    "masked_c64": ("masked", {"AGN_XCD_CHUNK": "64"}, 0),
+    "masked_two_x1": ("masked", {"AGN_Q8E_TWO": "1", "AGN_XCD_REMAP": "1"}, 0x2),
+    "masked_two_c64": ("masked", {"AGN_Q8E_TWO": "1", "AGN_XCD_CHUNK": "64"}, 0x2),
+    "masked_hints_x1": ("masked", {"AGN_XCD_REMAP": "1"}, HINTS),
+    "masked_hints_c64": ("masked", {"AGN_XCD_CHUNK": "64"}, HINTS),
 }
-KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM", "AGN_Q8E_TWO", "AGN_COUNTER_VARIANT")
+KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM", "AGN_Q8E_TWO", "AGN_COUNTER_VARIANT", "AGN_XCD_REMAP",
+         "AGN_XCD_CHUNK")
 
 
 def main():
