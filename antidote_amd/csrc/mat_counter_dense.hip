@@ -1257,15 +1257,17 @@ int launch_var(int v, const agn_log &log, const agn_read &req, const agn_result 
 template <int D, int WPB>
 int launch_key(const agn_log &log, const agn_read &req, const agn_result &out, hipStream_t st) {
     const int v = counter_variant<D>();
-    // quad rows, warm batch (SCT given), not forced: two requests per wave
-    // (warm cfg2 8.37-8.45 vs 8.83-9.02 ms; cold no change,
-    // profiles/r02/ab_counter_quad2.log) -- for dense batches: a masked warm
-    // batch keeps one request per wave (its two-request form takes 118
-    // VGPRs, 4 waves per SIMD: warm masked cfg2 13.06 vs 11.06 ms, mixed keys
-    // 17.32 vs 13.00; profiles/r03/ab_masked_warm_quad{2,1}.log)
+    // quad rows, dense batch, not forced: two requests per wave -- warm cfg2
+    // 8.37-8.45 vs 8.83-9.02 ms (profiles/r02/ab_counter_quad2.log); cold
+    // batches too since the blocks go to the XCDs in runs (block_order):
+    // cold cfg2 7.28 vs 7.46 ms in one process (round 2, identity order: no
+    // change; profiles/r06/ab_counter_quad2_cold.log).  A masked batch keeps
+    // one request per wave (its two-request form takes 118 VGPRs, 4 waves per
+    // SIMD: warm masked cfg2 13.06 vs 11.06 ms, mixed keys 17.32 vs 13.00;
+    // profiles/r03/ab_masked_warm_quad{2,1}.log)
     const bool masked = sparse_batch(log, req, out);
     if constexpr (D == 8)
-        if (v == ROWS_QUAD2 || (v == ROWS_QUAD && req.sct && !masked && forced_variant() < 0))
+        if (v == ROWS_QUAD2 || (v == ROWS_QUAD && !masked && forced_variant() < 0))
             return launch_quad2(log, req, out, st);
     const int v2 = v == ROWS_QUAD2 ? default_variant<D>() : v;
     return masked ? launch_var<D, WPB, true>(v2, log, req, out, st)
@@ -1412,7 +1414,12 @@ int tune_dense(const agn_log &log, const agn_read &req, const agn_result &out, h
             const int var = (r & 1) ? NV - 1 - k : k;  // alternate which variant goes first
             if (!has_variant<D>(var)) continue;
             if (hipEventRecord(e0, st) != hipSuccess) { rc = fail(AGN_EHIP, "tune: record"); break; }
-            rc = launch_var<D, 1, false>(var, log, req, out, st);
+            // quad rows run two requests per wave on a dense batch (launch_key)
+            if constexpr (D == 8)
+                rc = var == ROWS_QUAD ? launch_quad2(log, req, out, st)
+                                      : launch_var<D, 1, false>(var, log, req, out, st);
+            else
+                rc = launch_var<D, 1, false>(var, log, req, out, st);
             if (rc) break;
             float t = 0.f;
             if (hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||

@@ -711,6 +711,10 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
         traffic, traffic_src = pmc_traffic(a.config, n_keys,
                                            f"cfg{a.config}_sparse_{a.sparse}" if a.sparse else None)
         kname = KERNEL_NAME[a.config]
+        if (not a.sparse and cfg["crdt_type"] == 1 and cfg["n_dcs"] == 8 and
+                (tune is None or tune["selected"] == "quad_rows")):
+            # dense D = 8 batches run quad rows two requests per wave
+            kname = "k_counter_quad2 (two requests per wave)"
         if a.sparse and cfg["crdt_type"] == 1 and cfg["n_dcs"] == 8 and not many_mixed:
             # the masked D = 8 batch: chunk 0 issued under the key's metadata,
             # keys whose entries differ handed to a list pass (empty here)

@@ -14,7 +14,7 @@ import sys
 
 # bench line -> a substring of its dominant kernel's demangled name
 KERNELS = {
-    "cfg2": "k_counter_key<8, false, 1, 2, false, false>",
+    "cfg2": "k_counter_quad2<false, false>",
     "cfg1": "k_counter_key<3,",
     "cfg2_masked_full": "k_counter_q8e<",
     "cfg3": "k_tags<4, 4, false, true, true, 256, 1, 2, false, false, true, false",

@@ -54,7 +54,7 @@ expand() {
     pmc)
       # one counter block per run (FETCH_SIZE, then WRITE_SIZE), per config
       for c in ${PMC_CONFIGS-1 2 3 4 5}; do
-        case $c in 1) k=k_counter_key; n=10000;; 2) k=k_counter_key; n=10000000;;
+        case $c in 1) k=k_counter_key; n=10000;; 2) k=k_counter_quad2; n=10000000;;
                    3) k=k_tags; n=1000000;; 4) k=k_tags; n=1000000;; 5) k=k_gst_cols; n=4096;; esac
         echo "fetch$c|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "write$c|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
