@@ -922,13 +922,13 @@ __global__ __launch_bounds__(64) void k_counter_q8e(
                       o_err, mk.o_mask);
 }
 
-// Warm sparse batches (SCT given), AGN_Q8E_TWO=1: k_counter_q8e with two requests per wave,
+// Sparse batches, cold and warm: k_counter_q8e with two requests per wave,
 // as k_counter_quad2 serves dense warm batches -- both keys' segment
 // metadata in one scalar round trip, both first chunks issued under it, the
 // side loads (R, SCT, the DC sets) under the chunks.  Mixed keys are handed
 // on to k_counter_q8m as in q8e.  (Round 3's two-request masked form carried
 // the per-entry-mask scan inline: 118 VGPRs, slower than one request.)
-template <bool KEYS>
+template <bool ANY_WARM, bool KEYS>
 __global__ __launch_bounds__(64) void k_counter_q8e2(Q2Params) {
     const DenseArgs a = dense_of(kparams<Q2Params>().a);
     const uint32_t blk = block_order(a.xcd, blockIdx.x, gridDim.x);
@@ -953,10 +953,10 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(Q2Params) {
     const auto &ps = kparams<Q2Params>();
     const MaskArgs mk = mask_of(ps.mk);
     const uint64_t kmw0 = key_word(mk, k0.key, ps.key_off), kmw1 = key_word(mk, k1.key, ps.key_off);
-    q2_side<true, true>(k0, a, mk, kmw0, ps.key_off, ps.key_type, ps.R, ps.sct, ps.sct_ignore,
-                        ps.req_txid);
-    q2_side<true, true>(k1, a, mk, kmw1, ps.key_off, ps.key_type, ps.R, ps.sct, ps.sct_ignore,
-                        ps.req_txid);
+    q2_side<ANY_WARM, true>(k0, a, mk, kmw0, ps.key_off, ps.key_type, ps.R, ps.sct,
+                            ps.sct_ignore, ps.req_txid);
+    q2_side<ANY_WARM, true>(k1, a, mk, kmw1, ps.key_off, ps.key_type, ps.R, ps.sct,
+                            ps.sct_ignore, ps.req_txid);
     auto mixed = [&](const Q2Key &k, uint64_t kmw) {
         return !(mk.oc_mask == nullptr || (mk.key_mask && (kmw & 0xFFull)) || k.n == 0);
     };
@@ -978,10 +978,10 @@ __global__ __launch_bounds__(64) void k_counter_q8e2(Q2Params) {
     const bool d0 = any && !k0.corrupt && !m0, d1 = two && any && !k1.corrupt && !m1;
     {
         const auto &p = kparams<Q2Params>();
-        if (d0) q2_fold<true>(k0, c0, 0, p.log_txid, a.n_entries, s0);
-        if (d1) q2_fold<true>(k1, c1, 0, p.log_txid, a.n_entries, s1);
-        if (d0) q2_rest<true>(k0, p.oc, p.eff, p.log_txid, a.n_entries, s0);
-        if (d1) q2_rest<true>(k1, p.oc, p.eff, p.log_txid, a.n_entries, s1);
+        if (d0) q2_fold<ANY_WARM>(k0, c0, 0, p.log_txid, a.n_entries, s0);
+        if (d1) q2_fold<ANY_WARM>(k1, c1, 0, p.log_txid, a.n_entries, s1);
+        if (d0) q2_rest<ANY_WARM>(k0, p.oc, p.eff, p.log_txid, a.n_entries, s0);
+        if (d1) q2_rest<ANY_WARM>(k1, p.oc, p.eff, p.log_txid, a.n_entries, s1);
     }
     const auto &pe = kparams<Q2Params>();
     if (!m0)
@@ -1117,18 +1117,25 @@ int launch_q8e(const agn_log &log, const agn_read &req, const agn_result &out, h
     const unsigned mb = QL_S * 16u;  // a multiple of QL_S
 #define AGN_Q8M(W, K)                                                                           \
     hipLaunchKernelGGL((k_counter_q8m<W, K>), dim3(mb), dim3(64), 0, st, AGN_ARGS)
-    // warm: two requests per wave (k_counter_q8e2; AGN_Q8E_TWO=0: one).
+    // two requests per wave (k_counter_q8e2; AGN_Q8E_TWO=0: one).
     // Warm masked cfg2 8.55 ms against q8e's 9.27 and the dense warm
     // kernel's 8.27 (profiles/r05/ab_masked_warm_q8e2_ldc.log)
+    // cold batches too since the dense path went two per wave: masked cfg2
+    // with the bench's hints 7.36 against 8.00 ms in one process
+    // (profiles/r06/ab_masked_cold_two.log); AGN_Q8E_TWO=1: warm batches only
     const char *tv = AGN_KNOB("AGN_Q8E_TWO");
     const bool two = !(tv && tv[0] == '0');
+    const bool two_cold = two && !(tv && tv[0] == '1');
     const unsigned nb2 = (unsigned)((req.n_req + 1) / 2);
-#define AGN_Q8E2(K)                                                                             \
-    hipLaunchKernelGGL((k_counter_q8e2<K>), dim3(nb2), dim3(64), 0, st, Q2Params{AGN_ARGS})
+#define AGN_Q8E2(W, K)                                                                          \
+    hipLaunchKernelGGL((k_counter_q8e2<W, K>), dim3(nb2), dim3(64), 0, st, Q2Params{AGN_ARGS})
     if (rc == AGN_OK) {
         if (req.sct && two) {
-            if (req.keys) { AGN_Q8E2(true); AGN_Q8M(true, true); }
-            else { AGN_Q8E2(false); AGN_Q8M(true, false); }
+            if (req.keys) { AGN_Q8E2(true, true); AGN_Q8M(true, true); }
+            else { AGN_Q8E2(true, false); AGN_Q8M(true, false); }
+        } else if (two_cold) {
+            if (req.keys) { AGN_Q8E2(false, true); AGN_Q8M(false, true); }
+            else { AGN_Q8E2(false, false); AGN_Q8M(false, false); }
         } else if (req.sct) {
             if (req.keys) { AGN_Q8E(true, true); AGN_Q8M(true, true); }
             else { AGN_Q8E(true, false); AGN_Q8M(true, false); }

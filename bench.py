@@ -718,7 +718,7 @@ def materialize_main(a, torch, dist, world, rank, local, backend):
         if a.sparse and cfg["crdt_type"] == 1 and cfg["n_dcs"] == 8 and not many_mixed:
             # the masked D = 8 batch: chunk 0 issued under the key's metadata,
             # keys whose entries differ handed to a list pass (empty here)
-            kname = "k_counter_q8e (+ k_counter_q8m)"
+            kname = "k_counter_q8e2 (two requests per wave; + k_counter_q8m)"
 
         workload = cfg["name"].format(keys=fmt_keys(n_keys))
         if a.sparse:

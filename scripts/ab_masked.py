@@ -57,6 +57,10 @@ VARIANTS = {
     "masked_two_c64": ("masked", {"AGN_Q8E_TWO": "1", "AGN_XCD_CHUNK": "64"}, 0x2),
     "masked_hints_x1": ("masked", {"AGN_XCD_REMAP": "1"}, HINTS),
     "masked_hints_c64": ("masked", {"AGN_XCD_CHUNK": "64"}, HINTS),
+    # cold batches two requests per wave (k_counter_q8e2's cold form)
+    "masked_cold2": ("masked", {"AGN_Q8E_TWO": "2"}, 0),
+    "masked_hints_cold2": ("masked", {"AGN_Q8E_TWO": "2"}, HINTS),
+    "mixed_cold2": ("mixed", {"AGN_Q8E_TWO": "2"}, 0),
 }
 KNOBS = ("AGN_COUNTER_EARLY", "AGN_Q8E_KM", "AGN_Q8E_TWO", "AGN_COUNTER_VARIANT", "AGN_XCD_REMAP",
          "AGN_XCD_CHUNK")

@@ -16,7 +16,7 @@ import sys
 KERNELS = {
     "cfg2": "k_counter_quad2<false, false>",
     "cfg1": "k_counter_key<3,",
-    "cfg2_masked_full": "k_counter_q8e<",
+    "cfg2_masked_full": "k_counter_q8e2<false",
     "cfg3": "k_tags<4, 4, false, true, true, 256, 1, 2, false, false, true, false",
     "cfg4": "k_tags<4, 16, false, true, false, 256, 1, 2, false, false",
     "cfg5": "k_gst_cols",

@@ -72,7 +72,7 @@ expand() {
       for m in ${PMC_SPARSE-full mixed}; do
         echo "sfetch$m|180|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_sfetch$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "swrite$m|180|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_swrite$m -o run -- python3 bench.py --config 2 --sparse $m --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
-        case $m in mixed) sk=k_counter_key;; *) sk=k_counter_q8e;; esac
+        case $m in mixed) sk=k_counter_key;; *) sk=k_counter_q8e2;; esac
         echo "spmcj$m|60|python3 scripts/pmc_traffic.py gpurun_out/prof_sfetch$m/run_counter_collection.csv gpurun_out/prof_swrite$m/run_counter_collection.csv $sk 10000000 2 gpurun_out/pmc/cfg2_sparse_$m.json"
       done;;
     pmcwarm)

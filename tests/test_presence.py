@@ -87,12 +87,14 @@ def device_result(eng, log, req, index, hints=0):
 
 
 IMPLS = {"vgpr": "0", "quad": "2", "quad2": "3", "split": "2", "split_km1": "2",
-         "split_ctflag": "2", "split_mixed": "2", "split_two": "2"}
+         "split_ctflag": "2", "split_mixed": "2", "split_two": "2", "split_cold": "2",
+         "split_one_cold": "2"}
 
 
 @pytest.mark.parametrize("path", ["host", "device_indexed", "device_no_index"])
 @pytest.mark.parametrize("impl", ["vgpr", "quad", "quad2", "general", "split", "split_km1",
-                                  "split_ctflag", "split_mixed", "split_two"])
+                                  "split_ctflag", "split_mixed", "split_two", "split_cold",
+                                  "split_one_cold"])
 @pytest.mark.parametrize("D", [1, 3, 5, 8])
 def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
     """quad / quad2 / vgpr: k_counter_key (AGN_COUNTER_EARLY=0); split: the
@@ -102,12 +104,16 @@ def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
     (LastOpCt masks over every column as AGN_F_CT_FULL), _mixed with
     AGN_HINT_MIXED (k_counter_key: the mixed keys in the same pass), _two with
     the warm requests (SCT given) two per wave (k_counter_q8e2,
-    AGN_Q8E_TWO=1)."""
+    AGN_Q8E_TWO=1); _cold a batch without SCT two per wave (q8e2's cold form,
+    the default), _one_cold the same batch one per wave (AGN_Q8E_TWO=0)."""
     monkeypatch.delenv("AGN_COUNTER_GLDS", raising=False)
     monkeypatch.setenv("AGN_COUNTER_VARIANT", IMPLS.get(impl, "0"))
     monkeypatch.setenv("AGN_COUNTER_EARLY", "1" if impl.startswith("split") else "0")
     monkeypatch.setenv("AGN_Q8E_KM", "1" if impl == "split_km1" else "0")
-    monkeypatch.setenv("AGN_Q8E_TWO", "1" if impl == "split_two" else "0")
+    if impl == "split_cold":
+        monkeypatch.delenv("AGN_Q8E_TWO", raising=False)
+    else:
+        monkeypatch.setenv("AGN_Q8E_TWO", "1" if impl == "split_two" else "0")
     if impl == "general":
         monkeypatch.setenv("AGN_COUNTER_IMPL", "general")
     else:
@@ -116,6 +122,8 @@ def test_presence_vs_oracle(eng, oracle_lib, monkeypatch, D, impl, path):
         pytest.skip("the host path has no hints; split covered on the device paths")
     log, req = presence_case(1000 * D + len(impl) + len(path), 260, D, 150, txid=0.3,
                              invalid=0.02, corrupt=0.03, identity=(D % 2 == 0))
+    if impl.endswith("cold"):  # no SCT: the cold kernels
+        req.sct = req.sct_mask = req.sct_ignore = None
     want = oracle_result(oracle_lib, log, req)
     if path == "host":
         got = eng.materialize_host(log, req, sparse=True)
