@@ -40,6 +40,8 @@ VARS = {
     # runs of g blocks per XCD (block_order)
     **{f"np1c{g}": ("cur", {"AGN_READ_CACHED_SPLIT": "0", "AGN_READ6_NP": "1",
                             "AGN_READ6_XCD": str(g)}) for g in (16, 64, 128, 256)},
+    **{f"np2c{g}": ("cur", {"AGN_READ_CACHED_SPLIT": "0", "AGN_READ6_NP": "2",
+                            "AGN_READ6_XCD": str(g)}) for g in (32, 64, 128)},
     "default": ("cur", {}),
 }
 # name=path entries of the variant list: another library's fused kernel
