@@ -117,3 +117,15 @@ def test_final_line_keeps_the_exchange_check():
     assert len(json.dumps(out)) < 8000
     assert out["gst"]["exchange_verified"] is True and out["n_gpus"] == 2
     assert out["configs"]["cfg5"]["exchange_verified"] is True
+
+
+def test_committed_final_line_is_its_detail_compacted():
+    """Round 6's committed final line (profiles/r06/bench_final_line.json, the
+    line DESIGN.md §4.8 quotes) is exactly bench.compact_line of the detail
+    file the same run wrote, and every sub-line carries PMC traffic."""
+    full = json.load(open(os.path.join(ROOT, "profiles", "r06", "bench_final_detail.json")))
+    line = json.load(open(os.path.join(ROOT, "profiles", "r06", "bench_final_line.json")))
+    assert bench.compact_line(full, line.get("detail")) == line
+    assert len(json.dumps(line)) < 8000
+    assert line["roofline"]["traffic"] is not None
+    assert all(sub.get("traffic") is not None for sub in line["configs"].values())
