@@ -782,10 +782,13 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
 
 // agn_read_cached's batch size from which it runs the three batched kernels
 // (k_ss_lookup -> the counter kernel -> k_ss_store, per-request prune flags)
-// instead of the fused one: same results.  D = 8 (quad rows): never -- the
-// fused kernel wins at every size since round 5 (warm cfg2 keys, fused vs
-// batched: 100k 0.099 vs 0.111 ms, 1M 0.97 vs 1.00, 10M 9.45 vs 9.70;
-// profiles/r05/ab_read6_sizes.log).  D < 8: from 2^15 requests, where the
+// instead of the fused one: same results.  D = 8 (quad rows): from 5M
+// requests -- the fused kernel won at every size in round 5 (100k 0.099 vs
+// 0.111 ms, 1M 0.97 vs 1.00, 10M 9.45 vs 9.70; profiles/r05/
+// ab_read6_sizes.log); since the batched scan runs two requests per wave in
+// runs of 64 blocks per XCD it leads from about 5M (warm cfg2 keys, fused vs
+// batched: 2M 1.90 vs 1.93 ms, 4M 3.78 vs 3.83, 6M 5.75 vs 5.56, 8M 7.63 vs
+// 7.49, 10M 9.25 vs 9.05; profiles/r06/ab_read6_xcd.log).  D < 8: from 2^15 requests, where the
 // batched kernels' 8 requests per wave in the cache steps and two per wave in
 // the scan win (D = 3: 100k 0.090 vs 0.090 ms, 1M 0.90 vs 0.84, 10M 8.99 vs
 // 8.20).  AGN_READ_CACHED_SPLIT=<n> moves the switch (0: never).
@@ -795,7 +798,7 @@ static uint64_t read_cached_split(uint32_t D) {
         const uint64_t n = strtoull(v, nullptr, 10);
         return n ? n : ~0ull;
     }
-    return D == 8 ? ~0ull : 1ull << 15;
+    return D == 8 ? 5000000ull : 1ull << 15;
 }
 
 static int read_cached_seq(agn_ss_cache *cache, const agn_log *log, uint64_t n_req,

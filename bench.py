@@ -994,8 +994,8 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     flags = eng.download(res.bufs["flags"], np.uint32, (n_keys,))
     cnt = eng.download(res.bufs["count"], np.uint32, (n_keys,))
     # the same warm step through agn_read_cached on the same cache: its
-    # default dispatch (the batched kernels from 1M requests) and the fused
-    # kernel forced at this size (AGN_READ_CACHED_SPLIT=0)
+    # default dispatch (D = 8: the batched kernels from 5M requests) and the
+    # fused kernel forced at this size (AGN_READ_CACHED_SPLIT=0)
     dkeys = eng.upload(np.arange(n_keys, dtype=np.uint64))
     t_rc = {}
     from antidote_amd._lib import set_knob
@@ -1021,8 +1021,8 @@ def warm_bench(eng, dl, dr, cfg, n_keys, sp, torch, steps, cfg_id=None):
     # ignore flag and the base value per request
     wbytes = algorithmic_bytes(cfg, n_keys) + n_keys * (8 * D + 1 + 8)
     # PMC bytes of the warm k_counter_quad2 launches (scripts/gpu.sh pmcwarm:
-    # the steps launches after the 2 priming ones; agn_read_cached runs the
-    # fused kernel at D = 8, so they are the last quad2 launches)
+    # the steps launches after the 2 priming ones, before the 4 launches of
+    # agn_read_cached's default dispatch, which at 10M requests is batched)
     wtraffic, wsrc = pmc_traffic(cfg_id, n_keys, f"cfg{cfg_id}_warm") if cfg_id else \
         (None, "null: config id not given")
     return {"ms_per_step": ms, "lookup_ms": t_lookup / steps, "materialize_ms": t_mat / steps,

@@ -613,9 +613,9 @@ int agn_ss_store(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t
  * threshold[n_keys][D].  Same results, cache contents and prune flags as the
  * three calls; AGN_ENOTSUP for another type or shape.  One launch, the
  * key's cache slots held in registers (21 us for 10k keys, cfg1, D = 3, where
- * the three calls take 35 us; 10M keys at D = 8: 9.5 vs 9.7 ms); for D < 8
- * from 2^15 requests the batched kernels, which are faster there in bulk;
- * AGN_READ_CACHED_SPLIT=<n> sets the switch (0: always one launch).  Reads
+ * the three calls take 35 us); in bulk the batched kernels, which are faster
+ * there: for D < 8 from 2^15 requests, at D = 8 from 5M (10M keys: 9.05 vs
+ * 9.25 ms); AGN_READ_CACHED_SPLIT=<n> sets the switch (0: always one launch).  Reads
  * at most 16 slots of a key (caches written by these entry points hold at
  * most SNAPSHOT_THRESHOLD - 1). */
 int agn_read_cached(agn_ctx *ctx, agn_ss_cache *cache, const agn_log *log, uint64_t n_req,

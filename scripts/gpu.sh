@@ -78,11 +78,11 @@ expand() {
     pmcwarm)
       # warm cfg2 / cfg3 / cfg4 (bench.py --warm: k_counter_quad2 from the
       # cached base, k_tags from the cached states): the 3 warm steps'
-      # launches -- for set/register before the 4 agn_read_cached ones (the
-      # batched kernels); counter_pn's agn_read_cached is the fused kernel
-      # (k_read6) at D = 8, so its warm steps are the last quad2 launches
+      # launches, before the 4 of agn_read_cached's default dispatch (the
+      # batched kernels: for counter_pn at D = 8 from 5M requests; its fused
+      # form, timed after them, launches k_read6)
       for c in ${PMC_WARM-2 3 4}; do
-        case $c in 2) k=k_counter_quad2; n=10000000; sel=tail:3:0;;
+        case $c in 2) k=k_counter_quad2; n=10000000; sel=tail:3:4;;
                    *) k=k_tags; n=1000000; sel=tail:3:4;; esac
         echo "wfetch$c|240|rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_wfetch$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"
         echo "wwrite$c|240|rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_wwrite$c -o run -- python3 bench.py --config $c --warm --steps 3 --warmup 1 --cpu-keys 0 --tune-rounds 0 --configs none"

@@ -393,7 +393,7 @@ def oracle_read_cached(lib, hc, ls, keys, R, tx, gc, D):
 def test_read_cached_default_dispatch(eng, oracle_lib, monkeypatch):
     """A bulk batch (33k requests, D = 8, keys of up to 64 ops: those past 32
     take the fused kernel's second chunk) through agn_read_cached's default
-    dispatch (the fused k_read6: D = 8 never switches since round 5) and with
+    dispatch (the fused k_read6: D = 8 switches only from 5M requests) and with
     the batched kernels forced (AGN_READ_CACHED_SPLIT=1), each against the C
     oracle's lookup -> materialize -> store chain on a host cache: outputs,
     status, prune flags, thresholds and the caches, over a cold round and two

@@ -329,10 +329,16 @@ def run_rounds(eng, oracle_lib, spec, forms):
         eng.free_gen(dl, dr)
 
 
-def test_warm_cfg2_read_cached_full_size(eng, oracle_lib):
-    """cfg2_warm: 10M keys x 64 ops, D = 8, agn_read_cached's default dispatch
-    (the fused k_read6: lookup -> warm materialize over two 32-op chunks ->
-    store in one launch) for all three rounds."""
+@pytest.mark.parametrize("split", ["0", None], ids=["fused", "default"])
+def test_warm_cfg2_read_cached_full_size(eng, oracle_lib, monkeypatch, split):
+    """cfg2_warm: 10M keys x 64 ops, D = 8, agn_read_cached for all three
+    rounds: the fused k_read6 forced (AGN_READ_CACHED_SPLIT=0: lookup -> warm
+    materialize over two 32-op chunks -> store in one launch) and the default
+    dispatch, which at 10M requests runs the batched kernels."""
+    if split is None:
+        monkeypatch.delenv("AGN_READ_CACHED_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("AGN_READ_CACHED_SPLIT", split)
     run_rounds(eng, oracle_lib, CFG2, ["read_cached"] * 3)
 
 
